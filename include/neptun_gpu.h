@@ -1,0 +1,168 @@
+/*
+ * neptun_gpu.h -- C ABI of the MI355X (gfx950) WireGuard transport-data AEAD.
+ *
+ * Drop-in boundary for NepTUN's per-packet ChaCha20-Poly1305 seal/open, i.e.
+ * the bytes-hot part of Tunn::encapsulate / Tunn::decapsulate
+ * (/root/reference/neptun/src/noise/mod.rs:295-380).  NepTUN exposes no C ABI
+ * of its own; these entry points are what its Rust side binds
+ * through `extern "C"` (INTEGRATION.md shows the binding).  Plain pointers and
+ * sizes only: no HIP or torch types, the stream is an opaque `void *`
+ * (a hipStream_t, NULL = the default stream).
+ *
+ * Semantics per packet are those of
+ *   seal: Session::format_packet_data   session.rs:205-259
+ *         header LE32 4 | LE32 sending_index | LE64 counter, nonce 0^4|LE64
+ *         counter, empty AAD, ciphertext = plaintext length (no padding),
+ *         16-byte tag right after it; wire length = len + 32.
+ *   open: Tunn::parse_incoming_packet (DATA arm, noise/mod.rs:139-199) +
+ *         Session::receive_packet_data session.rs:265-302 without the replay
+ *         window (host-side, wg_replay_* below): header checked (type 4,
+ *         len >= 32, receiver_idx == the slot's receiving index), tag verified
+ *         (ring open_in_place), plaintext written.  On a tag mismatch the
+ *         plaintext bytes are zeroed (ring 0.17 open_within) and the status is
+ *         InvalidAeadTag.
+ *
+ * Per-packet status codes are WireGuardError variant index + 1
+ * (neptun/src/noise/errors.rs:4-28), 0 = Ok; ABI-level codes start at 100.
+ *
+ * Device-resident entry points take DEVICE pointers (src, dst, descs, status)
+ * and are asynchronous on `stream`.  Layout requirement of the GPU path:
+ * 16-byte alignment of every packet's plaintext and ciphertext start (seal:
+ * src_off % 16 == 0 and dst_off % 16 == 0; open: src_off % 16 == 0 and
+ * dst_off % 16 == 0).  A misaligned descriptor gets WG_STATUS_MISALIGNED.
+ *
+ * Thread safety: a context may be used from several host threads; key-table
+ * updates are serialised internally and are stream-ordered against launches
+ * issued on the same stream.
+ */
+#ifndef NEPTUN_GPU_H
+#define NEPTUN_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WG_GPU_ABI_VERSION 1
+
+/* ---- per-packet status: WireGuardError (errors.rs:4-28) index + 1 ------- */
+enum wg_status {
+  WG_STATUS_OK = 0,
+  WG_STATUS_DESTINATION_BUFFER_TOO_SMALL = 1,
+  WG_STATUS_INCORRECT_PACKET_LENGTH = 2,
+  WG_STATUS_UNEXPECTED_PACKET = 3,
+  WG_STATUS_WRONG_PACKET_TYPE = 4,
+  WG_STATUS_WRONG_INDEX = 5,
+  WG_STATUS_WRONG_KEY = 6,
+  WG_STATUS_INVALID_TAI64N_TIMESTAMP = 7,
+  WG_STATUS_WRONG_TAI64N_TIMESTAMP = 8,
+  WG_STATUS_INVALID_MAC = 9,
+  WG_STATUS_INVALID_AEAD_TAG = 10,
+  WG_STATUS_INVALID_COUNTER = 11,
+  WG_STATUS_DUPLICATE_COUNTER = 12,
+  WG_STATUS_INVALID_PACKET = 13,
+  WG_STATUS_NO_CURRENT_SESSION = 14,
+  WG_STATUS_LOCK_FAILED = 15,
+  WG_STATUS_CONNECTION_EXPIRED = 16,
+  WG_STATUS_UNDER_LOAD = 17,
+  WG_STATUS_CRYPTO_FAILED = 18,
+  WG_STATUS_INVALID_LENGTH = 19,
+  WG_STATUS_INVALID_INDEX = 20,
+  WG_STATUS_RING_UNSPECIFIED_ERROR = 21,
+  WG_STATUS_SYSTEM_TIME_ERROR = 22,
+  /* ABI-level (not WireGuardError) */
+  WG_STATUS_MISALIGNED = 100,   /* packet start not 16-byte aligned */
+  WG_STATUS_BAD_KEY_SLOT = 101, /* key_slot >= context key slots */
+};
+
+/* ---- call-level return codes ------------------------------------------- */
+enum wg_rc {
+  WG_RC_OK = 0,
+  WG_RC_INVALID_ARGUMENT = -1,
+  WG_RC_HIP_ERROR = -2,
+  WG_RC_OUT_OF_MEMORY = -3,
+  WG_RC_NO_DEVICE = -4,
+};
+
+/* NepTUN wire constants */
+#define WG_MSG_DATA 4u              /* noise/mod.rs:86  DATA */
+#define WG_DATA_OFFSET 16u          /* session.rs:31    DATA_OFFSET */
+#define WG_AEAD_SIZE 16u            /* session.rs:33    AEAD_SIZE */
+#define WG_DATA_OVERHEAD_SZ 32u     /* noise/mod.rs:91  DATA_OVERHEAD_SZ */
+
+/*
+ * One packet of a batch (32 bytes, device memory for the *_batch calls).
+ *   seal: plaintext at src + src_off (len bytes); wire packet (len + 32 bytes)
+ *         written at dst + dst_off; counter = the sending counter the host
+ *         reserved (Session::sending_key_counter.fetch_add, session.rs:219).
+ *   open: datagram (header | ciphertext | tag, len bytes, len >= 32) at
+ *         src + src_off; plaintext (len - 32 bytes) written at dst + dst_off;
+ *         counter is ignored (parsed from the header on the device).
+ *   key_slot: index into the context key table (seal: the session's sending
+ *         key; open: its receiving key).
+ */
+typedef struct wg_packet_desc {
+  uint64_t src_off;
+  uint64_t dst_off;
+  uint64_t counter;
+  uint32_t len;
+  uint32_t key_slot;
+} wg_packet_desc;
+
+typedef struct wg_gpu_ctx wg_gpu_ctx;
+
+/* ABI version (WG_GPU_ABI_VERSION). */
+int wg_gpu_abi_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char *wg_gpu_last_error(void);
+
+/*
+ * Context = one GPU + a device-resident key table of `key_slots` entries
+ * (32-byte ChaCha20 key + the session index that goes with it).  Replaces
+ * Session::new's UnboundKey/LessSafeKey setup (session.rs:160-180): the keys a
+ * handshake derives (handshake.rs:694, :948) are uploaded with wg_gpu_set_keys.
+ */
+int wg_gpu_ctx_create(int device, uint32_t key_slots, wg_gpu_ctx **out);
+int wg_gpu_ctx_destroy(wg_gpu_ctx *ctx);
+uint32_t wg_gpu_ctx_key_slots(const wg_gpu_ctx *ctx);
+
+/*
+ * Upload keys[n][32] and indices[n] (HOST memory) into slots
+ * [first_slot, first_slot + n).  indices[i] is the session index checked or
+ * written with that key: for a sending-key slot the peer's index written into
+ * the header (Session::sending_index, session.rs:226); for a receiving-key
+ * slot our local index every datagram must carry (Session::receiving_index,
+ * session.rs:275-277).  Stream-ordered on `stream`; returns after the copy is
+ * enqueued (host buffers may be reused on return).
+ */
+int wg_gpu_set_keys(wg_gpu_ctx *ctx, uint32_t first_slot, uint32_t n, const uint8_t *keys,
+                    const uint32_t *indices, void *stream);
+
+/* Batch seal / open over device-resident descriptors (see wg_packet_desc). */
+int wg_gpu_seal_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
+                      const uint8_t *src, uint8_t *dst, int32_t *status, void *stream);
+int wg_gpu_open_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
+                      const uint8_t *src, uint8_t *dst, int32_t *status, void *stream);
+
+/*
+ * Uniform batch: n packets of one session, all `len` bytes, packet i at
+ * src + i*src_stride / dst + i*dst_stride.  Seal uses counter
+ * counter_base + i (one fetch_add(n) per batch instead of per packet,
+ * session.rs:219) -- the nonce is derived from the lane index.  Open parses
+ * each header.  Strides and base pointers must be multiples of 16.
+ * `status` may be NULL (no per-packet status written).
+ */
+int wg_gpu_seal_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_slot,
+                        uint64_t counter_base, const uint8_t *src, uint64_t src_stride,
+                        uint8_t *dst, uint64_t dst_stride, int32_t *status, void *stream);
+int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_slot,
+                        const uint8_t *src, uint64_t src_stride, uint8_t *dst,
+                        uint64_t dst_stride, int32_t *status, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEPTUN_GPU_H */

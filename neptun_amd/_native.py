@@ -1,0 +1,65 @@
+"""Loader for the in-tree C-ABI library ``neptun_amd/libneptun_gpu.so``.
+
+The library is the product: hand-written gfx950 kernels behind the C ABI in
+``include/neptun_gpu.h``.  There is no fallback -- if the library or a GPU is
+missing, calls raise ``NeptunGpuError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libneptun_gpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "neptun_gpu.h")
+
+
+class NeptunGpuError(RuntimeError):
+    pass
+
+
+_lib: ctypes.CDLL | None = None
+
+
+def header_functions(path: str = HEADER_PATH) -> list[str]:
+    """Every function the public header declares (the ABI surface)."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(wg_[a-z0-9_]+)\s*\(", text)))
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NeptunGpuError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (or `make -C neptun_amd/csrc`)")
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    vp, u32, u64, i32 = c.c_void_p, c.c_uint32, c.c_uint64, c.c_int32
+    L.wg_gpu_abi_version.restype = c.c_int
+    L.wg_gpu_last_error.restype = c.c_char_p
+    L.wg_gpu_ctx_create.argtypes = [c.c_int, u32, c.POINTER(vp)]
+    L.wg_gpu_ctx_destroy.argtypes = [vp]
+    L.wg_gpu_ctx_key_slots.argtypes = [vp]
+    L.wg_gpu_ctx_key_slots.restype = u32
+    L.wg_gpu_set_keys.argtypes = [vp, u32, u32, vp, vp, vp]
+    for fn in (L.wg_gpu_seal_batch, L.wg_gpu_open_batch):
+        fn.argtypes = [vp, vp, u32, vp, vp, vp, vp]
+    L.wg_gpu_seal_strided.argtypes = [vp, u32, u32, u32, u64, vp, u64, vp, u64, vp, vp]
+    L.wg_gpu_open_strided.argtypes = [vp, u32, u32, u32, vp, u64, vp, u64, vp, vp]
+    for name in header_functions():
+        fn = getattr(L, name)
+        if fn.restype is c.c_int and name not in ("wg_gpu_abi_version",):
+            fn.restype = i32
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().wg_gpu_last_error().decode(errors="replace")
+        raise NeptunGpuError(f"{what} failed (rc={rc}): {msg}")

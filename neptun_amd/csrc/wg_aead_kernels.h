@@ -1,0 +1,35 @@
+// wg_aead_kernels.h -- kernel parameter blocks shared by wg_aead.hip and wg_gpu.cpp.
+#pragma once
+#include <stdint.h>
+
+#include "neptun_gpu.h"
+
+namespace wg {
+
+constexpr uint32_t kBlockThreads = 256;  // 4 waves per workgroup
+
+struct StridedParams {
+  const uint8_t *keys;        // device key table, 32 B per slot
+  const uint32_t *key_index;  // device session index per slot
+  const uint8_t *src;
+  uint8_t *dst;
+  int32_t *status;            // may be null
+  uint64_t src_stride, dst_stride;
+  uint64_t counter_base;      // seal only
+  uint32_t n, len, key_slot;
+};
+
+struct DescParams {
+  const uint8_t *keys;
+  const uint32_t *key_index;
+  const wg_packet_desc *descs;
+  const uint8_t *src;
+  uint8_t *dst;
+  int32_t *status;
+  uint32_t n, key_slots;
+};
+
+template <bool kSeal> __global__ void aead_strided_kernel(StridedParams prm);
+template <bool kSeal> __global__ void aead_desc_kernel(DescParams prm);
+
+}  // namespace wg

@@ -1,0 +1,192 @@
+// wg_gpu.cpp -- C ABI (include/neptun_gpu.h) over the gfx950 AEAD kernels.
+//
+// Host side of the drop-in boundary: context + device key table (replaces the
+// per-session ring::LessSafeKey objects built in Session::new,
+// neptun/src/noise/session.rs:160-180) and batch launchers.  Nothing here
+// falls back to a CPU implementation: without a usable HIP device every call
+// fails with WG_RC_NO_DEVICE / WG_RC_HIP_ERROR.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "neptun_gpu.h"
+#include "wg_aead_kernels.h"
+
+struct wg_gpu_ctx {
+  int device = 0;
+  uint32_t key_slots = 0;
+  uint8_t *d_keys = nullptr;       // key_slots * 32
+  uint32_t *d_key_index = nullptr; // key_slots
+  std::mutex mu;                   // serialises key-table updates
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int rc, const char *what, hipError_t e = hipSuccess) {
+  char buf[256];
+  if (e != hipSuccess)
+    std::snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+  else
+    std::snprintf(buf, sizeof buf, "%s", what);
+  g_last_error = buf;
+  return rc;
+}
+
+#define WG_HIP(call, what)                                   \
+  do {                                                       \
+    hipError_t e_ = (call);                                  \
+    if (e_ != hipSuccess) return fail(WG_RC_HIP_ERROR, what, e_); \
+  } while (0)
+
+inline uint32_t grid_for(uint32_t n) { return (n + wg::kBlockThreads - 1) / wg::kBlockThreads; }
+
+// Launch on the caller's device; restore the previous current device after.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int wg_gpu_abi_version(void) { return WG_GPU_ABI_VERSION; }
+
+const char *wg_gpu_last_error(void) { return g_last_error.c_str(); }
+
+int wg_gpu_ctx_create(int device, uint32_t key_slots, wg_gpu_ctx **out) {
+  if (!out || key_slots == 0) return fail(WG_RC_INVALID_ARGUMENT, "ctx_create: bad argument");
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(WG_RC_NO_DEVICE, "ctx_create: no HIP device");
+  if (device < 0 || device >= count) return fail(WG_RC_INVALID_ARGUMENT, "ctx_create: bad device");
+  wg_gpu_ctx *ctx = new (std::nothrow) wg_gpu_ctx;
+  if (!ctx) return fail(WG_RC_OUT_OF_MEMORY, "ctx_create: host alloc");
+  ctx->device = device;
+  ctx->key_slots = key_slots;
+  DeviceGuard g(device);
+  hipError_t e = hipMalloc(&ctx->d_keys, (size_t)key_slots * 32);
+  if (e == hipSuccess) e = hipMalloc(&ctx->d_key_index, (size_t)key_slots * 4);
+  if (e == hipSuccess) e = hipMemset(ctx->d_keys, 0, (size_t)key_slots * 32);
+  if (e == hipSuccess) e = hipMemset(ctx->d_key_index, 0, (size_t)key_slots * 4);
+  if (e != hipSuccess) {
+    (void)hipFree(ctx->d_keys);
+    (void)hipFree(ctx->d_key_index);
+    delete ctx;
+    return fail(WG_RC_HIP_ERROR, "ctx_create: device alloc", e);
+  }
+  *out = ctx;
+  return WG_RC_OK;
+}
+
+int wg_gpu_ctx_destroy(wg_gpu_ctx *ctx) {
+  if (!ctx) return WG_RC_OK;
+  DeviceGuard g(ctx->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(ctx->d_keys);
+  (void)hipFree(ctx->d_key_index);
+  delete ctx;
+  return WG_RC_OK;
+}
+
+uint32_t wg_gpu_ctx_key_slots(const wg_gpu_ctx *ctx) { return ctx ? ctx->key_slots : 0; }
+
+int wg_gpu_set_keys(wg_gpu_ctx *ctx, uint32_t first_slot, uint32_t n, const uint8_t *keys,
+                    const uint32_t *indices, void *stream) {
+  if (!ctx || !keys || !indices) return fail(WG_RC_INVALID_ARGUMENT, "set_keys: null argument");
+  if (n == 0) return WG_RC_OK;
+  if ((uint64_t)first_slot + n > ctx->key_slots)
+    return fail(WG_RC_INVALID_ARGUMENT, "set_keys: slot range exceeds the key table");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard g(ctx->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // pageable host source: hipMemcpyAsync stages it before returning
+  WG_HIP(hipMemcpyAsync(ctx->d_keys + (size_t)first_slot * 32, keys, (size_t)n * 32,
+                        hipMemcpyHostToDevice, s),
+         "set_keys: key copy");
+  WG_HIP(hipMemcpyAsync(ctx->d_key_index + first_slot, indices, (size_t)n * 4,
+                        hipMemcpyHostToDevice, s),
+         "set_keys: index copy");
+  WG_HIP(hipStreamSynchronize(s), "set_keys: sync");
+  return WG_RC_OK;
+}
+
+static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, uint32_t n,
+                       const uint8_t *src, uint8_t *dst, int32_t *status, void *stream) {
+  if (!ctx || (n && (!descs || !src || !dst || !status)))
+    return fail(WG_RC_INVALID_ARGUMENT, "batch: null argument");
+  if (n == 0) return WG_RC_OK;
+  DeviceGuard g(ctx->device);
+  wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, src, dst, status, n, ctx->key_slots};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (seal)
+    hipLaunchKernelGGL(wg::aead_desc_kernel<true>, dim3(grid_for(n)), dim3(wg::kBlockThreads), 0,
+                       s, prm);
+  else
+    hipLaunchKernelGGL(wg::aead_desc_kernel<false>, dim3(grid_for(n)), dim3(wg::kBlockThreads), 0,
+                       s, prm);
+  WG_HIP(hipGetLastError(), "batch: launch");
+  return WG_RC_OK;
+}
+
+int wg_gpu_seal_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
+                      const uint8_t *src, uint8_t *dst, int32_t *status, void *stream) {
+  return launch_desc(ctx, true, descs, n, src, dst, status, stream);
+}
+
+int wg_gpu_open_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
+                      const uint8_t *src, uint8_t *dst, int32_t *status, void *stream) {
+  return launch_desc(ctx, false, descs, n, src, dst, status, stream);
+}
+
+static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, uint32_t key_slot,
+                          uint64_t counter_base, const uint8_t *src, uint64_t src_stride,
+                          uint8_t *dst, uint64_t dst_stride, int32_t *status, void *stream) {
+  if (!ctx || (n && (!src || !dst))) return fail(WG_RC_INVALID_ARGUMENT, "strided: null argument");
+  if (key_slot >= ctx->key_slots) return fail(WG_RC_INVALID_ARGUMENT, "strided: bad key slot");
+  if (((uintptr_t)src | (uintptr_t)dst | src_stride | dst_stride) & 15u)
+    return fail(WG_RC_INVALID_ARGUMENT, "strided: pointers and strides must be 16-byte aligned");
+  if (n == 0) return WG_RC_OK;
+  DeviceGuard g(ctx->device);
+  wg::StridedParams prm{ctx->d_keys, ctx->d_key_index, src, dst, status, src_stride,
+                        dst_stride, counter_base, n, len, key_slot};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (seal)
+    hipLaunchKernelGGL(wg::aead_strided_kernel<true>, dim3(grid_for(n)), dim3(wg::kBlockThreads),
+                       0, s, prm);
+  else
+    hipLaunchKernelGGL(wg::aead_strided_kernel<false>, dim3(grid_for(n)),
+                       dim3(wg::kBlockThreads), 0, s, prm);
+  WG_HIP(hipGetLastError(), "strided: launch");
+  return WG_RC_OK;
+}
+
+int wg_gpu_seal_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_slot,
+                        uint64_t counter_base, const uint8_t *src, uint64_t src_stride,
+                        uint8_t *dst, uint64_t dst_stride, int32_t *status, void *stream) {
+  return launch_strided(ctx, true, n, len, key_slot, counter_base, src, src_stride, dst,
+                        dst_stride, status, stream);
+}
+
+int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_slot,
+                        const uint8_t *src, uint64_t src_stride, uint8_t *dst,
+                        uint64_t dst_stride, int32_t *status, void *stream) {
+  return launch_strided(ctx, false, n, len, key_slot, 0, src, src_stride, dst, dst_stride, status,
+                        stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+"""Python face of the MI355X AEAD batch path (thin wrapper over the C ABI).
+
+Mirrors what NepTUN's Rust side would bind: a context per GPU
+holding the device key table (Session::new's keys, session.rs:160-180), batch
+seal = N x Session::format_packet_data (session.rs:205-259), batch open = N x
+Session::receive_packet_data without the replay window (session.rs:265-302).
+PyTorch is used only for device memory and streams; the arithmetic is the
+hand-written gfx950 kernels in neptun_amd/csrc/wg_aead.hip.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._native import NeptunGpuError, check, load
+
+DATA_OFFSET = 16        # session.rs:31
+AEAD_SIZE = 16          # session.rs:33
+DATA_OVERHEAD_SZ = 32   # noise/mod.rs:91
+
+# wg_packet_desc (include/neptun_gpu.h), 32 bytes
+DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("counter", "<u8"),
+                       ("len", "<u4"), ("key_slot", "<u4")])
+
+# per-packet status = WireGuardError index + 1 (neptun/src/noise/errors.rs:4-28)
+STATUS = {
+    0: "Ok", 1: "DestinationBufferTooSmall", 2: "IncorrectPacketLength", 3: "UnexpectedPacket",
+    4: "WrongPacketType", 5: "WrongIndex", 6: "WrongKey", 7: "InvalidTai64nTimestamp",
+    8: "WrongTai64nTimestamp", 9: "InvalidMac", 10: "InvalidAeadTag", 11: "InvalidCounter",
+    12: "DuplicateCounter", 13: "InvalidPacket", 14: "NoCurrentSession", 15: "LockFailed",
+    16: "ConnectionExpired", 17: "UnderLoad", 18: "CryptoFailed", 19: "InvalidLength",
+    20: "InvalidIndex", 21: "RingUnspecifiedError", 22: "SystemTimeError",
+    100: "Misaligned", 101: "BadKeySlot",
+}
+OK = 0
+INVALID_AEAD_TAG = 10
+INVALID_PACKET = 13
+WRONG_INDEX = 5
+
+
+def _ptr(x) -> int:
+    """Device pointer of a torch tensor (or an int already)."""
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    return int(x.data_ptr())
+
+
+def _stream(stream) -> int:
+    if stream is None:
+        import torch
+        return int(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)
+
+
+class GpuContext:
+    """One GPU + device key table.  Replaces per-session ring keys."""
+
+    def __init__(self, device: int = 0, key_slots: int = 1):
+        self._lib = load()
+        h = ctypes.c_void_p()
+        check(self._lib.wg_gpu_ctx_create(device, key_slots, ctypes.byref(h)), "wg_gpu_ctx_create")
+        self._h = h
+        self.device = device
+        self.key_slots = key_slots
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.wg_gpu_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_keys(self, first_slot: int, keys: np.ndarray, indices: np.ndarray, stream=None) -> None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 32)
+        indices = np.ascontiguousarray(indices, dtype=np.uint32).reshape(-1)
+        if len(keys) != len(indices):
+            raise ValueError("keys and indices differ in length")
+        check(self._lib.wg_gpu_set_keys(self._h, first_slot, len(keys), keys.ctypes.data,
+                                        indices.ctypes.data, _stream(stream)), "wg_gpu_set_keys")
+
+    # --- descriptor batches (device tensors) --------------------------------
+    def seal_batch(self, descs, n: int, src, dst, status, stream=None) -> None:
+        check(self._lib.wg_gpu_seal_batch(self._h, _ptr(descs), n, _ptr(src), _ptr(dst),
+                                          _ptr(status), _stream(stream)), "wg_gpu_seal_batch")
+
+    def open_batch(self, descs, n: int, src, dst, status, stream=None) -> None:
+        check(self._lib.wg_gpu_open_batch(self._h, _ptr(descs), n, _ptr(src), _ptr(dst),
+                                          _ptr(status), _stream(stream)), "wg_gpu_open_batch")
+
+    # --- uniform single-session batches -------------------------------------
+    def seal_strided(self, n: int, length: int, key_slot: int, counter_base: int, src,
+                     src_stride: int, dst, dst_stride: int, status=None, stream=None) -> None:
+        check(self._lib.wg_gpu_seal_strided(self._h, n, length, key_slot, counter_base, _ptr(src),
+                                            src_stride, _ptr(dst), dst_stride, _ptr(status),
+                                            _stream(stream)), "wg_gpu_seal_strided")
+
+    def open_strided(self, n: int, length: int, key_slot: int, src, src_stride: int, dst,
+                     dst_stride: int, status=None, stream=None) -> None:
+        check(self._lib.wg_gpu_open_strided(self._h, n, length, key_slot, _ptr(src), src_stride,
+                                            _ptr(dst), dst_stride, _ptr(status), _stream(stream)),
+              "wg_gpu_open_strided")
+
+
+__all__ = ["GpuContext", "NeptunGpuError", "DESC_DTYPE", "STATUS", "DATA_OFFSET", "AEAD_SIZE",
+           "DATA_OVERHEAD_SZ"]

@@ -1,0 +1,72 @@
+"""The C-ABI library loads and exports every symbol include/neptun_gpu.h declares.
+
+No compute calls here (this runs without a GPU).
+"""
+import ctypes
+import re
+
+import numpy as np
+import pytest
+
+import neptun_amd
+from neptun_amd import gpu as G
+from oracle import pyoracle as o
+
+
+def test_library_exports_header_symbols():
+    lib = neptun_amd.load()
+    names = neptun_amd.header_functions()
+    assert len(names) >= 10
+    for name in names:
+        assert hasattr(lib, name), f"{name} declared in include/neptun_gpu.h but not exported"
+    assert lib.wg_gpu_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    data = open(neptun_amd.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"aead_strided_kernel" in data and b"aead_desc_kernel" in data
+
+
+def header_enum():
+    text = open(neptun_amd._native.HEADER_PATH).read()
+    return {int(v): k for k, v in re.findall(r"WG_STATUS_([A-Z0-9_]+)\s*=\s*(\d+)", text)}
+
+
+def test_status_codes_follow_wireguard_error_order():
+    # neptun/src/noise/errors.rs:4-28, variant index + 1
+    variants = ["DestinationBufferTooSmall", "IncorrectPacketLength", "UnexpectedPacket",
+                "WrongPacketType", "WrongIndex", "WrongKey", "InvalidTai64nTimestamp",
+                "WrongTai64nTimestamp", "InvalidMac", "InvalidAeadTag", "InvalidCounter",
+                "DuplicateCounter", "InvalidPacket", "NoCurrentSession", "LockFailed",
+                "ConnectionExpired", "UnderLoad", "CryptoFailed", "InvalidLength",
+                "InvalidIndex", "RingUnspecifiedError", "SystemTimeError"]
+    enum = header_enum()
+    for i, v in enumerate(variants, start=1):
+        assert G.STATUS[i] == v
+        assert enum[i].replace("_", "") == v.upper(), (enum[i], v)
+
+
+def test_descriptor_layout_matches_header_and_oracle():
+    assert G.DESC_DTYPE.itemsize == 32
+    assert G.DESC_DTYPE == o.DESC_DTYPE
+    text = open(neptun_amd._native.HEADER_PATH).read()
+    body = re.search(r"typedef struct wg_packet_desc \{(.*?)\}", text, re.S).group(1)
+    fields = re.findall(r"(uint\d+)_t\s+(\w+);", body)
+    assert [f for _, f in fields] == list(G.DESC_DTYPE.names)
+    assert [int(t[4:]) // 8 for t, _ in fields] == [G.DESC_DTYPE[n].itemsize for n in G.DESC_DTYPE.names]
+
+
+def test_no_gpu_means_loud_failure():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(neptun_amd.NeptunGpuError, match="no HIP device"):
+        neptun_amd.GpuContext(0, 1)
+
+
+def test_invalid_arguments_rejected_without_launch():
+    lib = neptun_amd.load()
+    assert lib.wg_gpu_ctx_create(0, 0, ctypes.byref(ctypes.c_void_p())) == -1
+    assert lib.wg_gpu_seal_batch(None, None, 1, None, None, None, None) == -1
+    assert b"null" in lib.wg_gpu_last_error()

@@ -1,0 +1,281 @@
+"""Parity of the gfx950 kernels (through the C ABI) with the CPU oracle.
+
+Bit-exact: every wire byte of seal (header | ciphertext | tag,
+session.rs:205-259) and every plaintext byte + status of open
+(session.rs:265-302) must equal the oracle's on the same keys, counters and
+payloads.  Golden fixtures pin both to the reference KAT (handshake.rs:957-992)
+and to three independent RFC 8439 implementations (oracle/gen_golden.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as o
+from tools import synth
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+DESC = o.DESC_DTYPE
+
+
+def golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def to_dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def run_desc(torch, gpu, seal, descs, src, dst_size, slot_base=0):
+    """Launch a descriptor batch; returns (dst bytes, status) on the host."""
+    d_descs = to_dev(torch, descs.view(np.uint8))
+    d_src = to_dev(torch, src)
+    d_dst = torch.zeros(max(dst_size, 16), dtype=torch.uint8, device="cuda")
+    d_st = torch.full((len(descs),), -1, dtype=torch.int32, device="cuda")
+    fn = gpu.seal_batch if seal else gpu.open_batch
+    fn(d_descs, len(descs), d_src, d_dst, d_st)
+    torch.cuda.synchronize()
+    return d_dst.cpu().numpy(), d_st.cpu().numpy()
+
+
+def pack(items, align=16, pad=32):
+    """Lay out byte strings at 16-aligned offsets; returns (buffer, offsets)."""
+    offs, pos = [], 0
+    for b in items:
+        offs.append(pos)
+        pos = synth.round_up(pos + len(b) + pad, align)
+    buf = np.zeros(pos + 64, np.uint8)
+    for off, b in zip(offs, items):
+        buf[off:off + len(b)] = np.frombuffer(b, np.uint8)
+    return buf, offs
+
+
+def test_golden_vectors_seal_and_open(torch_cuda, gpu):
+    torch = torch_cuda
+    vecs = golden("data_packets.json")["vectors"]
+    n = len(vecs)
+    keys = np.stack([np.frombuffer(bytes.fromhex(v["key"]), np.uint8) for v in vecs])
+    idx = np.array([v["sending_index"] for v in vecs], np.uint32)
+    gpu.set_keys(0, keys, idx)
+    payloads = [bytes.fromhex(v["payload"]) for v in vecs]
+    src, soffs = pack(payloads)
+    wires = [bytes.fromhex(v["wire"]) for v in vecs]
+    _, doffs = pack(wires)
+    descs = np.zeros(n, DESC)
+    for i, v in enumerate(vecs):
+        descs[i] = (soffs[i], doffs[i], v["counter"], len(payloads[i]), i)
+    dst_size = doffs[-1] + len(wires[-1]) + 64
+    out, st = run_desc(torch, gpu, True, descs, src, dst_size)
+    assert (st == 0).all()
+    for i in range(n):
+        got = out[doffs[i]:doffs[i] + len(wires[i])].tobytes()
+        assert got == wires[i], f"vector {i} (len {len(payloads[i])}) differs"
+    # the bytes between packets were not touched
+    mask = np.ones(len(out), bool)
+    for i in range(n):
+        mask[doffs[i]:doffs[i] + len(wires[i])] = False
+    assert not out[mask].any()
+    # open what the fixtures hold
+    wsrc, woffs = pack(wires)
+    descs2 = np.zeros(n, DESC)
+    for i in range(n):
+        descs2[i] = (woffs[i], soffs[i], 0, len(wires[i]), i)
+    out2, st2 = run_desc(torch, gpu, False, descs2, wsrc, len(src))
+    assert (st2 == 0).all()
+    for i in range(n):
+        assert out2[soffs[i]:soffs[i] + len(payloads[i])].tobytes() == payloads[i]
+
+
+def test_tampered_datagrams_rejected_and_zeroed(torch_cuda, gpu):
+    torch = torch_cuda
+    vecs = golden("tamper.json")["vectors"]
+    n = len(vecs)
+    keys = np.stack([np.frombuffer(bytes.fromhex(v["key"]), np.uint8) for v in vecs])
+    idx = np.array([v["receiving_index"] for v in vecs], np.uint32)
+    gpu.set_keys(0, keys, idx)
+    wires = [bytes.fromhex(v["wire"]) for v in vecs]
+    wsrc, woffs = pack(wires)
+    out_offs, pos = [], 0
+    for w in wires:
+        out_offs.append(pos)
+        pos = synth.round_up(pos + len(w), 16)
+    descs = np.zeros(n, DESC)
+    for i in range(n):
+        descs[i] = (woffs[i], out_offs[i], 0, len(wires[i]), i)
+    # pre-fill the destination with 0xAA so "zeroed" is observable
+    d_descs = to_dev(torch, descs.view(np.uint8))
+    d_src = to_dev(torch, wsrc)
+    d_dst = torch.full((pos + 64,), 0xAA, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.open_batch(d_descs, n, d_src, d_dst, d_st)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    out = d_dst.cpu().numpy()
+    assert (st == 10).all(), st
+    for i in range(n):
+        p = len(wires[i]) - 32
+        assert not out[out_offs[i]:out_offs[i] + p].any(), vecs[i]["case"]
+
+
+def random_batch(rng, n, max_len, n_keys):
+    sizes = rng.integers(0, max_len + 1, n)
+    sizes[:8] = [0, 1, 15, 16, 17, 63, 64, 65][: min(8, n)]
+    keys = rng.integers(0, 256, (n_keys, 32), dtype=np.uint8)
+    kidx = rng.integers(0, 2**32, n_keys, dtype=np.uint64).astype(np.uint32)
+    payloads = synth.host_payloads(sizes, seed=int(rng.integers(1 << 30)))
+    ctrs = rng.integers(0, 2**63, n, dtype=np.uint64) * 2 + rng.integers(0, 2, n, dtype=np.uint64)
+    ctrs[:4] = [0, 2**32 - 1, 2**32, 2**64 - 1][: min(4, n)]
+    slots = rng.integers(0, n_keys, n).astype(np.uint32)
+    return sizes, keys, kidx, payloads, ctrs, slots
+
+
+@pytest.mark.parametrize("seed,n,max_len,n_keys", [(1, 3000, 9000, 64), (2, 20000, 1500, 4096)])
+def test_random_batches_match_oracle(torch_cuda, gpu, seed, n, max_len, n_keys):
+    torch = torch_cuda
+    rng = np.random.default_rng(seed)
+    sizes, keys, kidx, payloads, ctrs, slots = random_batch(rng, n, max_len, n_keys)
+    gpu.set_keys(0, keys, kidx)
+    src, soffs = pack(payloads)
+    # wire slots: shuffled order so neighbouring lanes hit unrelated memory
+    perm = rng.permutation(n)
+    doffs = np.zeros(n, np.int64)
+    pos = 0
+    for i in perm:
+        doffs[i] = pos
+        pos = synth.round_up(pos + int(sizes[i]) + 32, 16)
+    dst_size = pos + 64
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = soffs
+    descs["dst_off"] = doffs
+    descs["counter"] = ctrs
+    descs["len"] = sizes
+    descs["key_slot"] = slots
+    out, st = run_desc(torch, gpu, True, descs, src, dst_size)
+    want = np.zeros(dst_size, np.uint8)
+    wst = o.seal_batch(descs, keys, kidx, src, want)
+    assert (st == wst).all() and (st == 0).all()
+    assert np.array_equal(out, want), "sealed wire bytes differ from the oracle"
+    # open the GPU's own output back
+    descs2 = np.zeros(n, DESC)
+    descs2["src_off"] = doffs
+    descs2["dst_off"] = soffs
+    descs2["len"] = sizes + 32
+    descs2["key_slot"] = slots
+    out2, st2 = run_desc(torch, gpu, False, descs2, out, len(src))
+    assert (st2 == 0).all()
+    assert np.array_equal(out2, src)
+
+
+def test_strided_matches_oracle_and_counter_carry(torch_cuda, gpu):
+    torch = torch_cuda
+    n, P, S = 4096, 1350, 1408
+    keys = synth.keys(1)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    pt = synth.device_payloads(n, P, S, "cuda")
+    wire = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+    back = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    base = 2**32 - 1000  # counters cross 2^32 inside the batch
+    gpu.seal_strided(n, P, 0, base, pt, S, wire, S, st)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    src = pt.cpu().numpy()
+    out = wire.cpu().numpy()
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = np.arange(n) * S
+    descs["dst_off"] = np.arange(n) * S
+    descs["counter"] = base + np.arange(n, dtype=np.uint64)
+    descs["len"] = P
+    want = np.zeros_like(out)
+    assert (o.seal_batch(descs, keys, np.array([synth.RECEIVER_IDX], np.uint32), src, want) == 0).all()
+    rows_out = out.reshape(n, S)[:, :P + 32]
+    rows_want = want.reshape(n, S)[:, :P + 32]
+    assert np.array_equal(rows_out, rows_want)
+    assert not out.reshape(n, S)[:, P + 32:].any()  # nothing written past the packet
+    st.fill_(-1)
+    gpu.open_strided(n, P + 32, 0, wire, S, back, S, st)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    assert torch.equal(back.view(n, S)[:, :P], pt.view(n, S)[:, :P])
+
+
+def test_open_header_checks(torch_cuda, gpu):
+    torch = torch_cuda
+    v = golden("data_packets.json")["vectors"][23]  # 1350 bytes
+    key = np.frombuffer(bytes.fromhex(v["key"]), np.uint8)[None]
+    gpu.set_keys(0, key, np.array([v["sending_index"]], np.uint32))
+    gpu.set_keys(1, key, np.array([v["sending_index"] ^ 0x100], np.uint32))
+    wire = bytearray(bytes.fromhex(v["wire"]))
+    bad_type = bytearray(wire)
+    bad_type[0] = 2
+    items = [bytes(wire), bytes(bad_type), bytes(wire), bytes(wire), bytes(wire), bytes(wire)]
+    src, offs = pack(items)
+    descs = np.zeros(len(items), DESC)
+    for i in range(len(items)):
+        descs[i] = (offs[i], 2048 * i, 0, len(items[i]), 0)
+    descs[2]["key_slot"] = 1          # receiver index mismatch -> WrongIndex
+    descs[3]["len"] = 31              # shorter than a DATA message -> InvalidPacket
+    descs[4]["src_off"] += 4          # misaligned
+    descs[5]["key_slot"] = 4096       # outside the key table
+    _, st = run_desc(torch, gpu, False, descs, src, 2048 * len(items))
+    assert list(st) == [0, 13, 5, 13, 100, 101]
+
+
+def test_in_place_seal_and_open(torch_cuda, gpu):
+    """encapsulate_in_place layout: plaintext at slot+16, wire at slot (noise/mod.rs:303-338)."""
+    torch = torch_cuda
+    n, P, S = 512, 1000, 1056
+    keys = synth.keys(1, seed=99)
+    gpu.set_keys(0, keys, np.array([7], np.uint32))
+    pt = synth.device_payloads(n, P, S - 16, "cuda", seed=5).view(n, S - 16)
+    buf = torch.zeros((n, S), dtype=torch.uint8, device="cuda")
+    buf[:, 16:] = pt
+    ref = buf.clone()
+    base = buf.data_ptr()
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.seal_strided(n, P, 0, 77, base + 16, S, base, S, st)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    src = ref.cpu().numpy().reshape(-1)
+    want = np.zeros_like(src)
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = np.arange(n) * S + 16
+    descs["dst_off"] = np.arange(n) * S
+    descs["counter"] = 77 + np.arange(n, dtype=np.uint64)
+    descs["len"] = P
+    o.seal_batch(descs, keys, np.array([7], np.uint32), src, want)
+    got = buf.cpu().numpy()
+    assert np.array_equal(got[:, :P + 32], want.reshape(n, S)[:, :P + 32])
+    # open in place: plaintext lands at slot+16 (over the ciphertext)
+    gpu.open_strided(n, P + 32, 0, base, S, base + 16, S, st)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    assert torch.equal(buf[:, 16:16 + P], ref[:, 16:16 + P])
+
+
+def test_config2_full_size_round_trip(torch_cuda, gpu):
+    """1M x 1350 B (BASELINE config 2): seal->open identity, status, sampled oracle parity."""
+    torch = torch_cuda
+    n, P, S = 1 << 20, 1350, 1408
+    keys = synth.keys(1)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    pt = synth.device_payloads(n, P, S, "cuda")
+    wire = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+    back = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.seal_strided(n, P, 0, 0, pt, S, wire, S, st)
+    gpu.open_strided(n, P + 32, 0, wire, S, back, S, st)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    assert torch.equal(back.view(n, S)[:, :P], pt.view(n, S)[:, :P])
+    # sampled bit-exactness against the oracle (every 1021st packet)
+    rows = np.arange(0, n, 1021)
+    wire_rows = wire.view(n, S)[torch.from_numpy(rows).cuda()].cpu().numpy()
+    pt_rows = pt.view(n, S)[torch.from_numpy(rows).cuda()].cpu().numpy()
+    for r, w, p in zip(rows, wire_rows, pt_rows):
+        want = o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, int(r), p[:P].tobytes())
+        assert w[:P + 32].tobytes() == want
