@@ -103,12 +103,16 @@ def main():
 
     n, P = args.packets, args.size
     S = args.stride or synth.round_up(P + 32, 128)
+    if S % 16 or S < P + 32:
+        raise SystemExit("--stride must be a multiple of 16 and hold P + 32 bytes")
     ctx = neptun_amd.GpuContext(local, key_slots=1)
     key = synth.keys(1)
     ctx.set_keys(0, key, np.array([synth.RECEIVER_IDX], np.uint32))
     # shard: rank r owns packets [r*n, (r+1)*n) of the global batch; counters follow
     counter_base = rank * n
-    pt = synth.device_payloads(n, P, S, dev, seed=synth.SEED + rank)
+    # NepTUN slot layout (WG_HEADER_OFFSET = 16, device/mod.rs:76): plaintext 16 bytes
+    # into each slot, the datagram at the slot start -- both 128-byte-run aligned
+    pt = synth.device_payloads(n, P, S, dev, seed=synth.SEED + rank, offset=16)
     wire = torch.zeros(n * S, dtype=torch.uint8, device=dev)
     back = torch.zeros(n * S, dtype=torch.uint8, device=dev)
     st_seal = torch.full((n,), -1, dtype=torch.int32, device=dev)
@@ -118,10 +122,10 @@ def main():
     def step(evs=None):
         if evs is not None:
             evs[0].record(stream)
-        ctx.seal_strided(n, P, 0, counter_base, pt, S, wire, S, st_seal, stream)
+        ctx.seal_strided(n, P, 0, counter_base, pt.data_ptr() + 16, S, wire, S, st_seal, stream)
         if evs is not None:
             evs[1].record(stream)
-        ctx.open_strided(n, P + 32, 0, wire, S, back, S, st_open, stream)
+        ctx.open_strided(n, P + 32, 0, wire, S, back.data_ptr() + 16, S, st_open, stream)
         if evs is not None:
             evs[2].record(stream)
 
@@ -149,7 +153,7 @@ def main():
 
     # correctness of what was timed: statuses + round-trip identity (full batch)
     ok = int((st_seal != 0).sum()) == 0 and int((st_open != 0).sum()) == 0
-    ok = ok and torch.equal(back.view(n, S)[:, :P], pt.view(n, S)[:, :P])
+    ok = ok and torch.equal(back.view(n, S)[:, 16:16 + P], pt.view(n, S)[:, 16:16 + P])
     if world > 1:
         f = torch.tensor([0 if ok else 1], dtype=torch.int64)
         dist.all_reduce(f, op=dist.ReduceOp.MAX)

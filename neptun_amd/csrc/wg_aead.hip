@@ -1,4 +1,4 @@
-// wg_aead.hip -- MI355X (gfx950 / CDNA4) WireGuard transport-data AEAD.
+// wg_aead.hip -- MI355X (gfx950 / CDNA4) WireGuard transport-data AEAD kernels.
 //
 // Hand-written HIP for NepTUN's per-packet ChaCha20-Poly1305 seal/open:
 //   seal = Session::format_packet_data   (neptun/src/noise/session.rs:205-259)
@@ -7,390 +7,375 @@
 // The AEAD is RFC 8439 (what ring 0.17.14's CHACHA20_POLY1305 computes).
 //
 // Execution model (DESIGN.md "Kernels"):
-//   * one packet per wavefront lane; a wave64 works on 64 packets in lockstep,
-//     so for a uniform batch every branch below is wave-uniform;
-//   * the 16 ChaCha20 state words live in VGPRs (single-key batches keep the
-//     key in SGPRs), one 64-byte keystream block per loop trip;
-//   * data moves as 16-byte global_load/store_dwordx4 (4 per 64-byte block);
-//   * Poly1305 runs per lane in radix 2^32 (4 x 32-bit limbs + a 3-bit top
-//     limb) on v_mad_u64_u32 chains: measured on MI355X, v_mad_u64_u32 issues at
-//     the same rate as v_alignbit_b32 (tools/microbench_valu.hip), so 20 mads
-//     per 16-byte block beat radix 2^26 (25 mads + limb splitting);
-//   * the nonce is 0^4 | LE64(counter); in the strided form the counter is
-//     counter_base + packet index (derived from the lane index).
+//   * compute: one packet per wavefront lane.  A wave64 owns 64 packets and
+//     walks them in lockstep, one 128-byte "run" of every packet per round;
+//     the 16 ChaCha20 state words of the lane's packet live in VGPRs (the key
+//     in SGPRs for single-session batches), two 64-byte keystream blocks per
+//     round, Poly1305 accumulated per lane in radix 2^32.
+//   * memory: runs are staged through LDS.  Loads are LDS-DMA
+//     (global_load_lds_dwordx4), 8 packets x 128 contiguous bytes per 1 KiB
+//     wave instruction; stores go LDS -> VGPR -> global_store_dwordx4 in the
+//     same shape.  Every 128-byte line of a 128-byte-aligned slot is read or
+//     written whole by one instruction (measured: the lane-strided alternative
+//     moved 2.5-2.9x the algorithmic bytes through HBM, profiles/r01_*).  The
+//     LDS image is XOR-swizzled so a lane reading its own run is bank-
+//     conflict-free.
+//   * coordinates: everything is indexed in "wire coordinates" w = byte offset
+//     in the datagram (header 0..15, ciphertext 16..16+P, tag after it).  The
+//     plaintext side is addressed as base - 16 + w, so when plaintext sits 16
+//     bytes into a slot (NepTUN's WG_HEADER_OFFSET layout, device/mod.rs:76)
+//     both sides' runs are 128-byte aligned.  Any 16-byte-aligned layout is
+//     correct; that one is also fastest.
 // No MFMA: this is a stream cipher + MAC, not a contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "neptun_gpu.h"
 #include "wg_aead_kernels.h"
+#include "wg_crypto.h"
 
 namespace wg {
 
-// ---------------------------------------------------------------------------
-// ChaCha20 (RFC 8439 2.3)
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) {
-  return __builtin_amdgcn_alignbit(x, x, 32u - n);  // v_alignbit_b32: 1 VALU op
-}
+constexpr uint32_t kRun = 128;    // bytes of one packet per round (one cache line)
+constexpr uint32_t kChunks = 8;   // 16-byte chunks per run
+constexpr uint32_t kWaves = kBlockThreads / 64;
 
-#define WG_QR(a, b, c, d)                   \
-  a += b; d ^= a; d = rotl(d, 16);          \
-  c += d; b ^= c; b = rotl(b, 12);          \
-  a += b; d ^= a; d = rotl(d, 8);           \
-  c += d; b ^= c; b = rotl(b, 7);
-
-constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu, kSigma2 = 0x79622d32u,
-                   kSigma3 = 0x6b206574u;
-
-// Keystream block `blk` for key k[8] and nonce (0, n1, n2) -- WireGuard's nonce
-// is 4 zero bytes then LE64(counter) (session.rs:230-235), so word 13 is 0.
-__device__ __forceinline__ void chacha20_block(uint32_t ks[16], const uint32_t k[8], uint32_t blk,
-                                               uint32_t n1, uint32_t n2) {
-  uint32_t x0 = kSigma0, x1 = kSigma1, x2 = kSigma2, x3 = kSigma3;
-  uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3];
-  uint32_t x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
-  uint32_t x12 = blk, x13 = 0, x14 = n1, x15 = n2;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
-    WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
-  }
-  ks[0] = x0 + kSigma0; ks[1] = x1 + kSigma1; ks[2] = x2 + kSigma2; ks[3] = x3 + kSigma3;
-  ks[4] = x4 + k[0]; ks[5] = x5 + k[1]; ks[6] = x6 + k[2]; ks[7] = x7 + k[3];
-  ks[8] = x8 + k[4]; ks[9] = x9 + k[5]; ks[10] = x10 + k[6]; ks[11] = x11 + k[7];
-  ks[12] = x12 + blk; ks[13] = x13; ks[14] = x14 + n1; ks[15] = x15 + n2;
-}
-
-// ---------------------------------------------------------------------------
-// Poly1305 (RFC 8439 2.5), radix 2^32: h = h0..h3 (32-bit) + h4 (< 8)
-// ---------------------------------------------------------------------------
-struct Poly {
-  uint32_t h0, h1, h2, h3, h4;
-  uint32_t r0, r1, r2, r3;  // clamped r
-  uint32_t s1, s2, s3;      // 5*r_i/4 (r1..r3 are multiples of 4)
+struct WaveStage {
+  uint4 run[64 * kChunks];  // [packet][chunk ^ swz(packet)], 8 KiB
+  uint64_t in_base[64];     // wire-coordinate origin of the input side
+  uint64_t out_base[64];    // wire-coordinate origin of the output side
+  uint32_t wlen[64];        // W = datagram length (P + 32)
+  uint32_t nruns[64];       // rounds this packet takes part in; 0 = none
 };
 
-__device__ __forceinline__ uint64_t mad(uint32_t a, uint32_t b, uint64_t c) {
-  return (uint64_t)a * b + c;  // v_mad_u64_u32
-}
+// XOR swizzle of a packet's 8 chunk slots: lane L reading chunk k of its own
+// run hits slot 8L + (k ^ swz(L)); over any ds_read_b128 lane group the banks
+// differ (row stride 128 B puts L&1 and the swizzle in distinct bank quads).
+__device__ __forceinline__ uint32_t swz(uint32_t p) { return (p >> 1) & 7u; }
 
-__device__ __forceinline__ void poly_init(Poly &p, const uint32_t ks0[8]) {
-  p.r0 = ks0[0] & 0x0fffffffu;
-  p.r1 = ks0[1] & 0x0ffffffcu;
-  p.r2 = ks0[2] & 0x0ffffffcu;
-  p.r3 = ks0[3] & 0x0ffffffcu;
-  p.s1 = p.r1 + (p.r1 >> 2);
-  p.s2 = p.r2 + (p.r2 >> 2);
-  p.s3 = p.r3 + (p.r3 >> 2);
-  p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
-}
-
-// h = (h + m + 2^128) * r  (partially reduced mod 2^130 - 5)
-__device__ __forceinline__ void poly_block(Poly &p, uint32_t m0, uint32_t m1, uint32_t m2,
-                                           uint32_t m3) {
-  uint64_t t = (uint64_t)p.h0 + m0;
-  const uint32_t h0 = (uint32_t)t;
-  t = (uint64_t)p.h1 + m1 + (t >> 32);
-  const uint32_t h1 = (uint32_t)t;
-  t = (uint64_t)p.h2 + m2 + (t >> 32);
-  const uint32_t h2 = (uint32_t)t;
-  t = (uint64_t)p.h3 + m3 + (t >> 32);
-  const uint32_t h3 = (uint32_t)t;
-  uint32_t h4 = p.h4 + (uint32_t)(t >> 32) + 1u;  // + 2^128 (full 16-byte block)
-  // d_j = sum_i h_i r_{j-i} with 2^128 == 5/4 folding (h_i r_j, i+j >= 4 -> h_i s_j)
-  const uint64_t d0 = mad(h3, p.s1, mad(h2, p.s2, mad(h1, p.s3, (uint64_t)h0 * p.r0)));
-  const uint64_t d1 =
-      mad(h4, p.s1, mad(h3, p.s2, mad(h2, p.s3, mad(h1, p.r0, mad(h0, p.r1, d0 >> 32)))));
-  const uint64_t d2 =
-      mad(h4, p.s2, mad(h3, p.s3, mad(h2, p.r0, mad(h1, p.r1, mad(h0, p.r2, d1 >> 32)))));
-  const uint64_t d3 =
-      mad(h4, p.s3, mad(h3, p.r0, mad(h2, p.r1, mad(h1, p.r2, mad(h0, p.r3, d2 >> 32)))));
-  h4 = h4 * p.r0 + (uint32_t)(d3 >> 32);
-  // fold bits >= 130: c = 5 * (h4 >> 2)
-  const uint32_t c = (h4 >> 2) + (h4 & ~3u);
-  h4 &= 3u;
-  t = (uint64_t)(uint32_t)d0 + c;
-  p.h0 = (uint32_t)t;
-  t = (uint64_t)(uint32_t)d1 + (t >> 32);
-  p.h1 = (uint32_t)t;
-  t = (uint64_t)(uint32_t)d2 + (t >> 32);
-  p.h2 = (uint32_t)t;
-  t = (uint64_t)(uint32_t)d3 + (t >> 32);
-  p.h3 = (uint32_t)t;
-  p.h4 = h4 + (uint32_t)(t >> 32);
-}
-
-// tag = (h mod p) + s mod 2^128; h < 5*2^128 < 2p so one conditional subtract
-__device__ __forceinline__ void poly_finish(const Poly &p, const uint32_t s[4], uint32_t tag[4]) {
-  uint64_t t = (uint64_t)p.h0 + 5u;
-  const uint32_t g0 = (uint32_t)t;
-  t = (uint64_t)p.h1 + (t >> 32);
-  const uint32_t g1 = (uint32_t)t;
-  t = (uint64_t)p.h2 + (t >> 32);
-  const uint32_t g2 = (uint32_t)t;
-  t = (uint64_t)p.h3 + (t >> 32);
-  const uint32_t g3 = (uint32_t)t;
-  const uint32_t g4 = p.h4 + (uint32_t)(t >> 32);
-  const bool ge = (g4 >> 2) != 0u;  // h + 5 >= 2^130  <=>  h >= p
-  const uint32_t f0 = ge ? g0 : p.h0, f1 = ge ? g1 : p.h1, f2 = ge ? g2 : p.h2,
-                 f3 = ge ? g3 : p.h3;
-  t = (uint64_t)f0 + s[0];
-  tag[0] = (uint32_t)t;
-  t = (uint64_t)f1 + s[1] + (t >> 32);
-  tag[1] = (uint32_t)t;
-  t = (uint64_t)f2 + s[2] + (t >> 32);
-  tag[2] = (uint32_t)t;
-  tag[3] = f3 + s[3] + (uint32_t)(t >> 32);
-}
-
-// ---------------------------------------------------------------------------
-// byte-granular helpers for the packet tail (run once per packet)
-// ---------------------------------------------------------------------------
-// mask of the valid low bytes of word j when `valid` bytes of a 16-byte chunk are live
-__device__ __forceinline__ uint32_t byte_mask(int valid, int j) {
-  const int v = valid - 4 * j;
-  return v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : ((1u << (8 * v)) - 1u));
-}
-
-// select word idx (runtime, may be out of [0,n)) of w[n], 0 outside
-template <int N>
-__device__ __forceinline__ uint32_t pick(const uint32_t (&w)[N], int idx) {
-  uint32_t r = 0;
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 #pragma unroll
-  for (int j = 0; j < N; ++j) r = (idx == j) ? w[j] : r;
-  return r;
+  for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return x;
 }
 
-// 4 bytes of the little-endian stream w[] starting at byte offset `off` (off may be < 0)
-template <int N>
-__device__ __forceinline__ uint32_t bytes_at(const uint32_t (&w)[N], int off) {
-  const int q = off >> 2;  // floor division (arithmetic shift)
-  const uint32_t b = (uint32_t)(off & 3);
-  return __builtin_amdgcn_alignbyte(pick(w, q + 1), pick(w, q), b);
-}
+__device__ __forceinline__ void lds_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// store the first k (1..15) bytes of a 16-byte-aligned chunk
-__device__ __forceinline__ void store_partial(uint8_t *p, const uint32_t w[4], int k) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int v = k - 4 * j;
-    if (v >= 4) {
-      *reinterpret_cast<uint32_t *>(p + 4 * j) = w[j];
-    } else if (v > 0) {
-      uint8_t *pb = p + 4 * j;
-      if (v >= 2) {
-        *reinterpret_cast<uint16_t *>(pb) = (uint16_t)w[j];
-        if (v == 3) pb[2] = (uint8_t)(w[j] >> 16);
-      } else {
-        pb[0] = (uint8_t)w[j];
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-  return *reinterpret_cast<const uint4 *>(p);
-}
-__device__ __forceinline__ void st16(uint8_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  *reinterpret_cast<uint4 *>(p) = make_uint4(a, b, c, d);
-}
-
-// ---------------------------------------------------------------------------
-// one packet, one lane
-// ---------------------------------------------------------------------------
-// body = plaintext (seal: in, open: out) / ciphertext (seal: out, open: in)
-// Returns the per-packet status.
 template <bool kSeal>
-__device__ __forceinline__ int32_t process_packet(const uint8_t *in, uint8_t *out,
-                                                  const uint32_t key[8], uint32_t sess_index,
-                                                  uint64_t counter_in, uint32_t len) {
-  uint64_t counter = counter_in;
-  uint32_t body_len;  // P
-  const uint8_t *body_in;
-  uint8_t *body_out;
-  if (kSeal) {
-    body_len = len;
-    body_in = in;
-    body_out = out + WG_DATA_OFFSET;
-    // header: LE32 DATA | LE32 sending_index | LE64 counter  (session.rs:221-227)
-    st16(out, WG_MSG_DATA, sess_index, (uint32_t)counter, (uint32_t)(counter >> 32));
-  } else {
-    // parse_incoming_packet DATA arm (noise/mod.rs:139-199): type 4, len >= 32
-    if (len < WG_DATA_OVERHEAD_SZ) return WG_STATUS_INVALID_PACKET;
-    const uint4 hdr = ld16(in);
-    if (hdr.x != WG_MSG_DATA) return WG_STATUS_INVALID_PACKET;
-    // receive_packet_data: receiver_idx == receiving_index (session.rs:275-277)
-    if (hdr.y != sess_index) return WG_STATUS_WRONG_INDEX;
-    counter = (uint64_t)hdr.z | ((uint64_t)hdr.w << 32);
-    body_len = len - WG_DATA_OVERHEAD_SZ;
-    body_in = in + WG_DATA_OFFSET;
-    body_out = out;
-  }
-  const uint32_t n1 = (uint32_t)counter, n2 = (uint32_t)(counter >> 32);
+struct Ranges {
+  // input bytes live in [lo, hi) and output bytes in [olo, ohi) of wire coordinates
+  __device__ static uint32_t in_lo() { return kSeal ? 16u : 0u; }
+  __device__ static uint32_t in_hi(uint32_t W) { return kSeal ? W - 16u : W; }
+  __device__ static uint32_t out_lo() { return kSeal ? 0u : 16u; }
+  __device__ static uint32_t out_hi(uint32_t W) { return kSeal ? W : W - 16u; }
+};
 
-  // Poly1305 one-time key = keystream block 0 (RFC 8439 2.6)
-  Poly p;
-  uint32_t s[4];
-  {
-    uint32_t ks[16];
-    chacha20_block(ks, key, 0u, n1, n2);
-    poly_init(p, ks);
-    s[0] = ks[4]; s[1] = ks[5]; s[2] = ks[6]; s[3] = ks[7];
-  }
-
-  const uint32_t nfull = body_len >> 6;  // whole 64-byte keystream blocks
-  for (uint32_t b = 0; b < nfull; ++b) {
-    const uint8_t *ip = body_in + 64u * b;
-    uint8_t *op = body_out + 64u * b;
-    const uint4 c0 = ld16(ip), c1 = ld16(ip + 16), c2 = ld16(ip + 32), c3 = ld16(ip + 48);
-    uint32_t ks[16];
-    chacha20_block(ks, key, b + 1u, n1, n2);
-    const uint32_t o0 = c0.x ^ ks[0], o1 = c0.y ^ ks[1], o2 = c0.z ^ ks[2], o3 = c0.w ^ ks[3];
-    const uint32_t o4 = c1.x ^ ks[4], o5 = c1.y ^ ks[5], o6 = c1.z ^ ks[6], o7 = c1.w ^ ks[7];
-    const uint32_t o8 = c2.x ^ ks[8], o9 = c2.y ^ ks[9], o10 = c2.z ^ ks[10], o11 = c2.w ^ ks[11];
-    const uint32_t o12 = c3.x ^ ks[12], o13 = c3.y ^ ks[13], o14 = c3.z ^ ks[14],
-                   o15 = c3.w ^ ks[15];
-    st16(op, o0, o1, o2, o3);
-    st16(op + 16, o4, o5, o6, o7);
-    st16(op + 32, o8, o9, o10, o11);
-    st16(op + 48, o12, o13, o14, o15);
-    if (kSeal) {  // MAC the ciphertext
-      poly_block(p, o0, o1, o2, o3);
-      poly_block(p, o4, o5, o6, o7);
-      poly_block(p, o8, o9, o10, o11);
-      poly_block(p, o12, o13, o14, o15);
-    } else {
-      poly_block(p, c0.x, c0.y, c0.z, c0.w);
-      poly_block(p, c1.x, c1.y, c1.z, c1.w);
-      poly_block(p, c2.x, c2.y, c2.z, c2.w);
-      poly_block(p, c3.x, c3.y, c3.z, c3.w);
+// Cooperative LDS-DMA load of round r: instruction j carries packets 8j..8j+7,
+// lane i moves 16 bytes (chunk (i&7)^swz(p)) of packet p = 8j + i/8.
+template <bool kSeal>
+__device__ __forceinline__ void stage_in(WaveStage &S, uint32_t lane, uint32_t r) {
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j) {
+    const uint32_t p = 8u * j + (lane >> 3);
+    const uint32_t k = (lane & 7u) ^ swz(p);
+    const uint32_t w = kRun * r + 16u * k;
+    const uint32_t W = S.wlen[p];
+    if (r < S.nruns[p] && w >= Ranges<kSeal>::in_lo() && w < Ranges<kSeal>::in_hi(W)) {
+      const uint8_t *g = reinterpret_cast<const uint8_t *>(S.in_base[p]) + w;
+      __builtin_amdgcn_global_load_lds(g, &S.run[64u * j], 16, 0, 0);
     }
   }
+}
 
-  // last, partial keystream block (1..63 bytes)
-  const int rem = (int)(body_len & 63u);
-  const int k = (int)(body_len & 15u);        // bytes in the partial 16-byte chunk
-  const uint32_t tail_off = body_len & ~15u;  // offset of that chunk (or of the tag if k == 0)
-  uint32_t tail_in[4] = {0, 0, 0, 0};         // input bytes of the partial chunk (masked)
-  uint32_t tail_out[4] = {0, 0, 0, 0};        // output bytes of the partial chunk (masked)
-  if (rem) {
-    uint32_t ks[16];
-    chacha20_block(ks, key, nfull + 1u, n1, n2);
-    const uint8_t *ip = body_in + 64u * nfull;
-    uint8_t *op = body_out + 64u * nfull;
+// Cooperative store of round r (same shape); the last chunk of a packet may be partial.
+template <bool kSeal>
+__device__ __forceinline__ void stage_out(WaveStage &S, uint32_t lane, uint32_t r) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int valid = rem - 16 * c;
-      if (valid > 0) {
-        const uint4 v = ld16(ip + 16 * c);  // aligned 16-byte chunk: over-read stays in it
-        uint32_t iw[4] = {v.x, v.y, v.z, v.w}, ow[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t m = byte_mask(valid, j);
-          iw[j] &= m;
-          ow[j] = (iw[j] ^ ks[4 * c + j]) & m;
-        }
-        if (valid >= 16) {
-          st16(op + 16 * c, ow[0], ow[1], ow[2], ow[3]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { tail_in[j] = iw[j]; tail_out[j] = ow[j]; }
-        }
-        // AEAD pad16: the zero-padded chunk is MACed as a full block
-        if (kSeal) poly_block(p, ow[0], ow[1], ow[2], ow[3]);
-        else poly_block(p, iw[0], iw[1], iw[2], iw[3]);
+  for (uint32_t j = 0; j < kChunks; ++j) {
+    const uint32_t p = 8u * j + (lane >> 3);
+    const uint32_t k = (lane & 7u) ^ swz(p);
+    const uint32_t w = kRun * r + 16u * k;
+    const uint32_t W = S.wlen[p];
+    const uint32_t hi = Ranges<kSeal>::out_hi(W);
+    if (r < S.nruns[p] && w >= Ranges<kSeal>::out_lo() && w < hi) {
+      const uint4 v = S.run[64u * j + lane];
+      uint8_t *g = reinterpret_cast<uint8_t *>(S.out_base[p]) + w;
+      const uint32_t n = hi - w;
+      if (n >= 16u) {
+        *reinterpret_cast<uint4 *>(g) = v;
+      } else {
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+        store_partial(g, wv, (int)n);
       }
     }
   }
-  // LE64(aad_len = 0) | LE64(ct_len)   (RFC 8439 2.8)
-  poly_block(p, 0u, 0u, body_len, 0u);
-  uint32_t tag[4];
-  poly_finish(p, s, tag);
+}
 
-  if (kSeal) {
-    // tail region at ct + tail_off: k ciphertext bytes then the 16-byte tag
-    uint8_t *tp = body_out + tail_off;
-    const uint32_t r[8] = {tail_out[0], tail_out[1], tail_out[2], tail_out[3], 0, 0, 0, 0};
-    uint32_t w[8];
+// One lane's chunk of ciphertext work.  m = plaintext/ciphertext byte index of
+// the chunk (wire w - 16); `ks` = its 4 keystream words.  Returns via LDS.
+template <bool kSeal>
+__device__ __forceinline__ void crypt_chunk(uint4 &slot, Poly &p, int m, uint32_t P,
+                                            uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint4 v = slot;
+  uint32_t i0 = v.x, i1 = v.y, i2 = v.z, i3 = v.w;
+  uint32_t o0 = i0 ^ a, o1 = i1 ^ b, o2 = i2 ^ c, o3 = i3 ^ d;
+  const int valid = (int)P - m;
+  if (valid < 16) {  // the packet's last, partial chunk: AEAD pad16 zero-fills it
+    const uint32_t m0 = byte_mask(valid, 0), m1 = byte_mask(valid, 1), m2 = byte_mask(valid, 2),
+                   m3 = byte_mask(valid, 3);
+    i0 &= m0; i1 &= m1; i2 &= m2; i3 &= m3;
+    o0 &= m0; o1 &= m1; o2 &= m2; o3 &= m3;
+  }
+  if (kSeal) poly_block(p, o0, o1, o2, o3);  // MAC the ciphertext
+  else poly_block(p, i0, i1, i2, i3);
+  slot = make_uint4(o0, o1, o2, o3);
+}
+
+// Process round r of this lane's packet: chunk k sits at wire w = 128r + 16k,
+// i.e. text byte m = 128r - 16 + 16k.  Keystream: chunk 0 is the last chunk of
+// block 2r (saved from the previous round), chunks 1-4 are block 2r+1, chunks
+// 5-7 the first three of block 2r+2 (its fourth is saved for round r+1).
+template <bool kSeal>
+__device__ __forceinline__ void crypt_round(WaveStage &S, uint32_t lane, uint32_t r, uint32_t P,
+                                            const uint32_t key[8], uint32_t n1, uint32_t n2,
+                                            Poly &p, uint32_t ks_save[4]) {
+  const int m0 = (int)(kRun * r) - 16;
+  const uint32_t row = 8u * lane, sw = swz(lane);
+  if (r > 0 && m0 < (int)P)
+    crypt_chunk<kSeal>(S.run[row + (0u ^ sw)], p, m0, P, ks_save[0], ks_save[1], ks_save[2],
+                       ks_save[3]);
+  if ((int)(kRun * r) < (int)P) {
+    uint32_t ks[16];
+    chacha20_block(ks, key, 2u * r + 1u, n1, n2);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) w[j] = r[j] | bytes_at(tag, 4 * j - k);
-    st16(tp, w[0], w[1], w[2], w[3]);
-    if (k) store_partial(tp + 16, &w[4], k);
-    return WG_STATUS_OK;
+    for (int k = 1; k <= 4; ++k) {
+      const int m = m0 + 16 * k;
+      if (m < (int)P)
+        crypt_chunk<kSeal>(S.run[row + ((uint32_t)k ^ sw)], p, m, P, ks[4 * k - 4],
+                           ks[4 * k - 3], ks[4 * k - 2], ks[4 * k - 1]);
+    }
+  }
+  if ((int)(kRun * r) + 64 < (int)P) {
+    uint32_t ks[16];
+    chacha20_block(ks, key, 2u * r + 2u, n1, n2);
+#pragma unroll
+    for (int k = 5; k <= 7; ++k) {
+      const int m = m0 + 16 * k;
+      if (m < (int)P)
+        crypt_chunk<kSeal>(S.run[row + ((uint32_t)k ^ sw)], p, m, P, ks[4 * k - 20],
+                           ks[4 * k - 19], ks[4 * k - 18], ks[4 * k - 17]);
+    }
+    ks_save[0] = ks[12]; ks_save[1] = ks[13]; ks_save[2] = ks[14]; ks_save[3] = ks[15];
+  }
+}
+
+// 32 bytes starting at the tail chunk: k ciphertext bytes then the 16-byte tag
+__device__ __forceinline__ void tail_words(const uint32_t (&ct)[4], const uint32_t (&tag)[4], int q,
+                                           uint32_t out[8]) {
+  const uint32_t r[8] = {ct[0], ct[1], ct[2], ct[3], 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = r[j] | bytes_at(tag, 4 * j - q);
+}
+
+struct PacketJob {
+  uint64_t in_base, out_base;  // wire-coordinate origins (see WaveStage)
+  uint64_t counter;            // seal: nonce counter; open: from the header
+  uint32_t len;                // seal: payload P; open: datagram length
+  uint32_t slot;
+  int32_t status;
+};
+
+template <bool kSeal, bool kUniformKey>
+__device__ __forceinline__ void run_wave(WaveStage &S, uint32_t lane, PacketJob job,
+                                         const uint8_t *keys, const uint32_t *key_index,
+                                         int32_t *status_out) {
+  // ---- per-packet setup (owner lane) ------------------------------------
+  uint32_t W = 0, P = 0;
+  if (job.status == WG_STATUS_OK) {
+    if (kSeal) {
+      P = job.len;
+      W = P + WG_DATA_OVERHEAD_SZ;
+    } else if (job.len < WG_DATA_OVERHEAD_SZ) {
+      job.status = WG_STATUS_INVALID_PACKET;  // parse_incoming_packet: DATA needs len >= 32
+    } else {
+      W = job.len;
+      P = W - WG_DATA_OVERHEAD_SZ;
+    }
+  }
+  uint32_t my_runs = job.status == WG_STATUS_OK ? (W + kRun - 1) / kRun : 0u;
+  S.in_base[lane] = job.in_base;
+  S.out_base[lane] = job.out_base;
+  S.wlen[lane] = W;
+  S.nruns[lane] = my_runs;
+  const uint32_t rounds = wave_max(my_runs);
+
+  uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t sidx = 0;
+  if (job.status == WG_STATUS_OK) {
+    const uint4 a = ld16(keys + 32u * job.slot), b = ld16(keys + 32u * job.slot + 16u);
+    key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
+    key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
+    sidx = key_index[job.slot];
+  }
+  (void)kUniformKey;
+
+  Poly poly;
+  uint32_t s[4] = {0, 0, 0, 0}, ks_save[4] = {0, 0, 0, 0};
+  uint32_t n1 = (uint32_t)job.counter, n2 = (uint32_t)(job.counter >> 32);
+  const uint32_t q = P & 15u;                    // bytes in the partial ciphertext chunk
+  const uint32_t wt = 16u + (P & ~15u);          // wire offset of the tail chunk
+  uint32_t tailB[4] = {0, 0, 0, 0};              // seal: chunk after the tail chunk (tag rest)
+  uint32_t rx[8] = {0, 0, 0, 0, 0, 0, 0, 0};     // open: raw bytes [wt, wt + 32)
+
+  auto one_time_key = [&]() {
+    uint32_t ks[16];
+    chacha20_block(ks, key, 0u, n1, n2);  // RFC 8439 2.6: block 0 -> r | s
+    poly_init(poly, ks);
+    s[0] = ks[4]; s[1] = ks[5]; s[2] = ks[6]; s[3] = ks[7];
+  };
+  if (kSeal && my_runs) one_time_key();  // overlaps the first DMA
+
+  for (uint32_t r = 0; r < rounds; ++r) {
+    stage_in<kSeal>(S, lane, r);
+    lds_wait_dma();
+    if (r < my_runs) {
+      const uint32_t row = 8u * lane, sw = swz(lane);
+      if (!kSeal) {
+        if (r == 0) {
+          // header: LE32 type | LE32 receiver_idx | LE64 counter (noise/mod.rs:170-180)
+          const uint4 h = S.run[row + (0u ^ sw)];
+          if (h.x != WG_MSG_DATA) job.status = WG_STATUS_INVALID_PACKET;
+          else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
+          if (job.status != WG_STATUS_OK) {
+            my_runs = 0;
+            S.nruns[lane] = 0;  // nothing of this packet is stored
+          } else {
+            n1 = h.z;
+            n2 = h.w;
+            one_time_key();
+          }
+        }
+        // keep the raw tail bytes before the slots are decrypted in place
+        if (my_runs) {
+          const uint32_t ra = wt >> 7, rb = (wt + 16u) >> 7;
+          if (ra == r) {
+            const uint4 v = S.run[row + (((wt >> 4) & 7u) ^ sw)];
+            rx[0] = v.x; rx[1] = v.y; rx[2] = v.z; rx[3] = v.w;
+          }
+          if (q && rb == r) {
+            const uint4 v = S.run[row + ((((wt + 16u) >> 4) & 7u) ^ sw)];
+            rx[4] = v.x; rx[5] = v.y; rx[6] = v.z; rx[7] = v.w;
+          }
+        }
+      } else if (r == 0) {
+        // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
+        S.run[row + (0u ^ sw)] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
+      }
+      if (my_runs) {
+        crypt_round<kSeal>(S, lane, r, P, key, n1, n2, poly, ks_save);
+        if (kSeal) {
+          if (r > 0 && ((wt + 16u) >> 7) == r && (wt >> 7) == r - 1u && q) {
+            // tag remainder spilled into this round's first chunk
+            S.run[row + (0u ^ sw)] = make_uint4(tailB[0], tailB[1], tailB[2], tailB[3]);
+          }
+          if ((wt >> 7) == r) {
+            // all ciphertext is MACed: LE64(aad_len=0) | LE64(ct_len), then the tag
+            poly_block(poly, 0u, 0u, P, 0u);
+            uint32_t tag[4];
+            poly_finish(poly, s, tag);
+            const uint32_t ka = (wt >> 4) & 7u;
+            uint32_t ct[4] = {0, 0, 0, 0};
+            if (q) {
+              const uint4 v = S.run[row + (ka ^ sw)];
+              ct[0] = v.x; ct[1] = v.y; ct[2] = v.z; ct[3] = v.w;
+            }
+            uint32_t w8[8];
+            tail_words(ct, tag, (int)q, w8);
+            S.run[row + (ka ^ sw)] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
+            tailB[0] = w8[4]; tailB[1] = w8[5]; tailB[2] = w8[6]; tailB[3] = w8[7];
+            if (q && ka < 7u)
+              S.run[row + ((ka + 1u) ^ sw)] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
+          }
+        }
+      }
+    }
+    stage_out<kSeal>(S, lane, r);
   }
 
-  // open: the received tag sits at ct + body_len (k bytes into the tail chunk)
-  const uint8_t *tp = body_in + tail_off;
-  uint32_t rx[8];
-  if (k) {
-    // tail_in holds only the k ciphertext bytes; the chunk (L1/L2-hot) carries tag bytes too
-    const uint4 lo = ld16(tp), hi = ld16(tp + 16);
-    rx[0] = lo.x; rx[1] = lo.y; rx[2] = lo.z; rx[3] = lo.w;
-    rx[4] = hi.x; rx[5] = hi.y; rx[6] = hi.z; rx[7] = hi.w;
-  } else {
-    const uint4 lo = ld16(tp);
-    rx[0] = lo.x; rx[1] = lo.y; rx[2] = lo.z; rx[3] = lo.w;
-    rx[4] = rx[5] = rx[6] = rx[7] = 0;
-  }
-  uint32_t diff = 0;
+  if (!kSeal && job.status == WG_STATUS_OK) {
+    poly_block(poly, 0u, 0u, P, 0u);
+    uint32_t tag[4];
+    poly_finish(poly, s, tag);
+    uint32_t diff = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) diff |= bytes_at(rx, k + 4 * j) ^ tag[j];
-  if (diff == 0u) {
-    if (k) store_partial(body_out + tail_off, tail_out, k);
-    return WG_STATUS_OK;
+    for (int j = 0; j < 4; ++j) diff |= bytes_at(rx, (int)q + 4 * j) ^ tag[j];
+    if (diff) {
+      // tag mismatch: never expose unauthenticated plaintext (ring open_within
+      // zeroes it); the streamed stores of this wave land first (same wave, in order)
+      job.status = WG_STATUS_INVALID_AEAD_TAG;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint8_t *pt = reinterpret_cast<uint8_t *>(job.out_base) + 16u;
+      for (uint32_t off = 0; off + 16u <= P; off += 16u) st16(pt + off, 0, 0, 0, 0);
+      if (q) {
+        const uint32_t z[4] = {0, 0, 0, 0};
+        store_partial(pt + (P & ~15u), z, (int)q);
+      }
+    }
   }
-  // tag mismatch: never expose unauthenticated plaintext (ring open_within zeroes it)
-  for (uint32_t off = 0; off + 16u <= body_len; off += 16u) st16(body_out + off, 0, 0, 0, 0);
-  if (k) {
-    const uint32_t z[4] = {0, 0, 0, 0};
-    store_partial(body_out + tail_off, z, k);
-  }
-  return WG_STATUS_INVALID_AEAD_TAG;
+  if (status_out) *status_out = job.status;
 }
 
 // ---------------------------------------------------------------------------
-// kernels
+// kernels: 4 independent waves per workgroup, each with its own LDS stage
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void load_key(const uint8_t *keys, uint32_t slot, uint32_t k[8]) {
-  const uint4 a = ld16(keys + 32u * slot), b = ld16(keys + 32u * slot + 16u);
-  k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
-  k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
-}
-
 template <bool kSeal>
 __global__ __launch_bounds__(kBlockThreads) void aead_strided_kernel(StridedParams prm) {
-  const uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x;
-  if (i >= prm.n) return;
-  // single session: key and index are wave-uniform (scalar loads, SGPRs)
-  uint32_t key[8];
-  load_key(prm.keys, prm.key_slot, key);
-  const uint32_t sidx = prm.key_index[prm.key_slot];
-  const uint8_t *in = prm.src + (uint64_t)i * prm.src_stride;
-  uint8_t *out = prm.dst + (uint64_t)i * prm.dst_stride;
-  const int32_t st =
-      process_packet<kSeal>(in, out, key, sidx, prm.counter_base + i, prm.len);
-  if (prm.status) prm.status[i] = st;
+  __shared__ WaveStage stage[kWaves];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t pkt0 = (blockIdx.x * kWaves + wave) * 64u;
+  if (pkt0 >= prm.n) return;  // wave-uniform
+  const uint32_t i = pkt0 + lane;
+  PacketJob job;
+  job.slot = prm.key_slot;
+  job.len = prm.len;
+  job.counter = prm.counter_base + i;
+  job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
+  const uint64_t src = reinterpret_cast<uint64_t>(prm.src) + (uint64_t)i * prm.src_stride;
+  const uint64_t dst = reinterpret_cast<uint64_t>(prm.dst) + (uint64_t)i * prm.dst_stride;
+  job.in_base = kSeal ? src - 16u : src;    // plaintext side is addressed at w - 16
+  job.out_base = kSeal ? dst : dst - 16u;
+  run_wave<kSeal, true>(stage[wave], lane, job, prm.keys, prm.key_index,
+                        (prm.status && i < prm.n) ? prm.status + i : nullptr);
 }
 
 template <bool kSeal>
 __global__ __launch_bounds__(kBlockThreads) void aead_desc_kernel(DescParams prm) {
-  const uint32_t i = blockIdx.x * kBlockThreads + threadIdx.x;
-  if (i >= prm.n) return;
-  const wg_packet_desc d = prm.descs[i];
-  int32_t st;
-  if (d.key_slot >= prm.key_slots) {
-    st = WG_STATUS_BAD_KEY_SLOT;
-  } else if (((d.src_off | d.dst_off) & 15u) != 0u) {
-    st = WG_STATUS_MISALIGNED;
-  } else {
-    uint32_t key[8];
-    load_key(prm.keys, d.key_slot, key);
-    const uint32_t sidx = prm.key_index[d.key_slot];
-    st = process_packet<kSeal>(prm.src + d.src_off, prm.dst + d.dst_off, key, sidx, d.counter,
-                               d.len);
+  __shared__ WaveStage stage[kWaves];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t pkt0 = (blockIdx.x * kWaves + wave) * 64u;
+  if (pkt0 >= prm.n) return;
+  const uint32_t i = pkt0 + lane;
+  PacketJob job;
+  job.status = -1;
+  job.in_base = job.out_base = 0;
+  job.counter = 0;
+  job.len = 0;
+  job.slot = 0;
+  if (i < prm.n) {
+    const wg_packet_desc d = prm.descs[i];
+    job.len = d.len;
+    job.slot = d.key_slot;
+    job.counter = d.counter;
+    const uint64_t src = reinterpret_cast<uint64_t>(prm.src) + d.src_off;
+    const uint64_t dst = reinterpret_cast<uint64_t>(prm.dst) + d.dst_off;
+    job.in_base = kSeal ? src - 16u : src;
+    job.out_base = kSeal ? dst : dst - 16u;
+    if (d.key_slot >= prm.key_slots) job.status = WG_STATUS_BAD_KEY_SLOT;
+    else if (((d.src_off | d.dst_off) & 15u) != 0u) job.status = WG_STATUS_MISALIGNED;
+    else job.status = WG_STATUS_OK;
   }
-  prm.status[i] = st;
+  run_wave<kSeal, false>(stage[wave], lane, job, prm.keys, prm.key_index,
+                         i < prm.n ? prm.status + i : nullptr);
 }
 
 template __global__ void aead_strided_kernel<true>(StridedParams);

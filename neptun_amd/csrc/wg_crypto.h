@@ -1,0 +1,185 @@
+// wg_crypto.h -- device primitives for the gfx950 AEAD kernels: ChaCha20 block
+// function (RFC 8439 2.3), Poly1305 in radix 2^32 (RFC 8439 2.5) and the
+// byte-granular helpers used once per packet at its tail.
+//
+// Poly1305 radix choice: on MI355X v_mad_u64_u32 issues at the same rate as
+// v_alignbit_b32 (tools/microbench_valu.hip, profiles/r01_microbench_valu.txt),
+// so 4 x 32-bit limbs + a 3-bit top limb (20 mads per 16-byte block, no limb
+// splitting) beat radix 2^26 (25 mads + splitting + 64-bit carries).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wg {
+
+
+// ---------------------------------------------------------------------------
+// ChaCha20 (RFC 8439 2.3)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) {
+  return __builtin_amdgcn_alignbit(x, x, 32u - n);  // v_alignbit_b32: 1 VALU op
+}
+
+#define WG_QR(a, b, c, d)                   \
+  a += b; d ^= a; d = rotl(d, 16);          \
+  c += d; b ^= c; b = rotl(b, 12);          \
+  a += b; d ^= a; d = rotl(d, 8);           \
+  c += d; b ^= c; b = rotl(b, 7);
+
+constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu, kSigma2 = 0x79622d32u,
+                   kSigma3 = 0x6b206574u;
+
+// Keystream block `blk` for key k[8] and nonce (0, n1, n2) -- WireGuard's nonce
+// is 4 zero bytes then LE64(counter) (session.rs:230-235), so word 13 is 0.
+__device__ __forceinline__ void chacha20_block(uint32_t ks[16], const uint32_t k[8], uint32_t blk,
+                                               uint32_t n1, uint32_t n2) {
+  uint32_t x0 = kSigma0, x1 = kSigma1, x2 = kSigma2, x3 = kSigma3;
+  uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3];
+  uint32_t x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+  uint32_t x12 = blk, x13 = 0, x14 = n1, x15 = n2;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
+    WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
+  }
+  ks[0] = x0 + kSigma0; ks[1] = x1 + kSigma1; ks[2] = x2 + kSigma2; ks[3] = x3 + kSigma3;
+  ks[4] = x4 + k[0]; ks[5] = x5 + k[1]; ks[6] = x6 + k[2]; ks[7] = x7 + k[3];
+  ks[8] = x8 + k[4]; ks[9] = x9 + k[5]; ks[10] = x10 + k[6]; ks[11] = x11 + k[7];
+  ks[12] = x12 + blk; ks[13] = x13; ks[14] = x14 + n1; ks[15] = x15 + n2;
+}
+
+// ---------------------------------------------------------------------------
+// Poly1305 (RFC 8439 2.5), radix 2^32: h = h0..h3 (32-bit) + h4 (< 8)
+// ---------------------------------------------------------------------------
+struct Poly {
+  uint32_t h0, h1, h2, h3, h4;
+  uint32_t r0, r1, r2, r3;  // clamped r
+  uint32_t s1, s2, s3;      // 5*r_i/4 (r1..r3 are multiples of 4)
+};
+
+__device__ __forceinline__ uint64_t mad(uint32_t a, uint32_t b, uint64_t c) {
+  return (uint64_t)a * b + c;  // v_mad_u64_u32
+}
+
+__device__ __forceinline__ void poly_init(Poly &p, const uint32_t ks0[8]) {
+  p.r0 = ks0[0] & 0x0fffffffu;
+  p.r1 = ks0[1] & 0x0ffffffcu;
+  p.r2 = ks0[2] & 0x0ffffffcu;
+  p.r3 = ks0[3] & 0x0ffffffcu;
+  p.s1 = p.r1 + (p.r1 >> 2);
+  p.s2 = p.r2 + (p.r2 >> 2);
+  p.s3 = p.r3 + (p.r3 >> 2);
+  p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
+}
+
+// h = (h + m + 2^128) * r  (partially reduced mod 2^130 - 5)
+__device__ __forceinline__ void poly_block(Poly &p, uint32_t m0, uint32_t m1, uint32_t m2,
+                                           uint32_t m3) {
+  uint64_t t = (uint64_t)p.h0 + m0;
+  const uint32_t h0 = (uint32_t)t;
+  t = (uint64_t)p.h1 + m1 + (t >> 32);
+  const uint32_t h1 = (uint32_t)t;
+  t = (uint64_t)p.h2 + m2 + (t >> 32);
+  const uint32_t h2 = (uint32_t)t;
+  t = (uint64_t)p.h3 + m3 + (t >> 32);
+  const uint32_t h3 = (uint32_t)t;
+  uint32_t h4 = p.h4 + (uint32_t)(t >> 32) + 1u;  // + 2^128 (full 16-byte block)
+  // d_j = sum_i h_i r_{j-i} with 2^128 == 5/4 folding (h_i r_j, i+j >= 4 -> h_i s_j)
+  const uint64_t d0 = mad(h3, p.s1, mad(h2, p.s2, mad(h1, p.s3, (uint64_t)h0 * p.r0)));
+  const uint64_t d1 =
+      mad(h4, p.s1, mad(h3, p.s2, mad(h2, p.s3, mad(h1, p.r0, mad(h0, p.r1, d0 >> 32)))));
+  const uint64_t d2 =
+      mad(h4, p.s2, mad(h3, p.s3, mad(h2, p.r0, mad(h1, p.r1, mad(h0, p.r2, d1 >> 32)))));
+  const uint64_t d3 =
+      mad(h4, p.s3, mad(h3, p.r0, mad(h2, p.r1, mad(h1, p.r2, mad(h0, p.r3, d2 >> 32)))));
+  h4 = h4 * p.r0 + (uint32_t)(d3 >> 32);
+  // fold bits >= 130: c = 5 * (h4 >> 2)
+  const uint32_t c = (h4 >> 2) + (h4 & ~3u);
+  h4 &= 3u;
+  t = (uint64_t)(uint32_t)d0 + c;
+  p.h0 = (uint32_t)t;
+  t = (uint64_t)(uint32_t)d1 + (t >> 32);
+  p.h1 = (uint32_t)t;
+  t = (uint64_t)(uint32_t)d2 + (t >> 32);
+  p.h2 = (uint32_t)t;
+  t = (uint64_t)(uint32_t)d3 + (t >> 32);
+  p.h3 = (uint32_t)t;
+  p.h4 = h4 + (uint32_t)(t >> 32);
+}
+
+// tag = (h mod p) + s mod 2^128; h < 5*2^128 < 2p so one conditional subtract
+__device__ __forceinline__ void poly_finish(const Poly &p, const uint32_t s[4], uint32_t tag[4]) {
+  uint64_t t = (uint64_t)p.h0 + 5u;
+  const uint32_t g0 = (uint32_t)t;
+  t = (uint64_t)p.h1 + (t >> 32);
+  const uint32_t g1 = (uint32_t)t;
+  t = (uint64_t)p.h2 + (t >> 32);
+  const uint32_t g2 = (uint32_t)t;
+  t = (uint64_t)p.h3 + (t >> 32);
+  const uint32_t g3 = (uint32_t)t;
+  const uint32_t g4 = p.h4 + (uint32_t)(t >> 32);
+  const bool ge = (g4 >> 2) != 0u;  // h + 5 >= 2^130  <=>  h >= p
+  const uint32_t f0 = ge ? g0 : p.h0, f1 = ge ? g1 : p.h1, f2 = ge ? g2 : p.h2,
+                 f3 = ge ? g3 : p.h3;
+  t = (uint64_t)f0 + s[0];
+  tag[0] = (uint32_t)t;
+  t = (uint64_t)f1 + s[1] + (t >> 32);
+  tag[1] = (uint32_t)t;
+  t = (uint64_t)f2 + s[2] + (t >> 32);
+  tag[2] = (uint32_t)t;
+  tag[3] = f3 + s[3] + (uint32_t)(t >> 32);
+}
+
+// ---------------------------------------------------------------------------
+// byte-granular helpers for the packet tail (run once per packet)
+// ---------------------------------------------------------------------------
+// mask of the valid low bytes of word j when `valid` bytes of a 16-byte chunk are live
+__device__ __forceinline__ uint32_t byte_mask(int valid, int j) {
+  const int v = valid - 4 * j;
+  return v >= 4 ? 0xffffffffu : (v <= 0 ? 0u : ((1u << (8 * v)) - 1u));
+}
+
+// select word idx (runtime, may be out of [0,n)) of w[n], 0 outside
+template <int N>
+__device__ __forceinline__ uint32_t pick(const uint32_t (&w)[N], int idx) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) r = (idx == j) ? w[j] : r;
+  return r;
+}
+
+// 4 bytes of the little-endian stream w[] starting at byte offset `off` (off may be < 0)
+template <int N>
+__device__ __forceinline__ uint32_t bytes_at(const uint32_t (&w)[N], int off) {
+  const int q = off >> 2;  // floor division (arithmetic shift)
+  const uint32_t b = (uint32_t)(off & 3);
+  return __builtin_amdgcn_alignbyte(pick(w, q + 1), pick(w, q), b);
+}
+
+// store the first k (1..15) bytes of a 16-byte-aligned chunk
+__device__ __forceinline__ void store_partial(uint8_t *p, const uint32_t w[4], int k) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int v = k - 4 * j;
+    if (v >= 4) {
+      *reinterpret_cast<uint32_t *>(p + 4 * j) = w[j];
+    } else if (v > 0) {
+      uint8_t *pb = p + 4 * j;
+      if (v >= 2) {
+        *reinterpret_cast<uint16_t *>(pb) = (uint16_t)w[j];
+        if (v == 3) pb[2] = (uint8_t)(w[j] >> 16);
+      } else {
+        pb[0] = (uint8_t)w[j];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+  return *reinterpret_cast<const uint4 *>(p);
+}
+__device__ __forceinline__ void st16(uint8_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  *reinterpret_cast<uint4 *>(p) = make_uint4(a, b, c, d);
+}
+
+}  // namespace wg

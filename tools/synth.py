@@ -42,15 +42,18 @@ def ipv4_header(total_len: int) -> bytes:
     return bytes(h)
 
 
-def device_payloads(n: int, size: int, stride: int, device, seed: int = SEED):
-    """uint8 tensor [n * stride] with n plaintexts of `size` bytes at stride."""
+def device_payloads(n: int, size: int, stride: int, device, seed: int = SEED, offset: int = 0):
+    """uint8 tensor [n * stride] with n plaintexts of `size` bytes at stride.
+
+    Plaintext i occupies [i*stride + offset, i*stride + offset + size); offset 16
+    is NepTUN's in-place layout (WG_HEADER_OFFSET, device/mod.rs:76)."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
     buf = torch.randint(0, 256, (n, stride), dtype=torch.uint8, device=device, generator=g)
     if size >= 20:
         hdr = torch.tensor(list(ipv4_header(size)), dtype=torch.uint8, device=device)
-        buf[:, :20] = hdr
+        buf[:, offset:offset + 20] = hdr
     return buf.reshape(-1)
 
 
