@@ -40,6 +40,10 @@ constexpr uint32_t kRun = 128;    // bytes of one packet per round (one cache li
 constexpr uint32_t kChunks = 8;   // 16-byte chunks per run
 constexpr uint32_t kWaves = kBlockThreads / 64;
 
+#ifndef WG_WAVES_PER_SIMD
+#define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
+#endif
+
 struct WaveStage {
   uint4 run[64 * kChunks];  // [packet][chunk ^ swz(packet)], 8 KiB
   uint64_t in_base[64];     // wire-coordinate origin of the input side
@@ -63,49 +67,131 @@ __device__ __forceinline__ void lds_wait_dma() { asm volatile("s_waitcnt vmcnt(0
 
 template <bool kSeal>
 struct Ranges {
-  // input bytes live in [lo, hi) and output bytes in [olo, ohi) of wire coordinates
+  // input bytes live in [in_lo, in_hi) and output bytes in [out_lo, out_hi) of wire coordinates
   __device__ static uint32_t in_lo() { return kSeal ? 16u : 0u; }
   __device__ static uint32_t in_hi(uint32_t W) { return kSeal ? W - 16u : W; }
   __device__ static uint32_t out_lo() { return kSeal ? 0u : 16u; }
   __device__ static uint32_t out_hi(uint32_t W) { return kSeal ? W : W - 16u; }
 };
 
+// Per-packet geometry of the wave's 64 packets, two flavours:
+//  * LdsGeom: arbitrary per-packet layout (descriptor batches, or the last,
+//    partial wave of a strided batch) -- read from the WaveStage tables;
+//  * UniformGeom: one length, strided slots, all 64 lanes live -- arithmetic,
+//    wave-uniform lengths, so every length-dependent branch is a scalar one.
+struct LdsGeom {
+  WaveStage &S;
+  __device__ bool live(uint32_t p, uint32_t r) const { return r < S.nruns[p]; }
+  __device__ uint32_t wlen(uint32_t p) const { return S.wlen[p]; }
+  __device__ uint64_t in_base(uint32_t p) const { return S.in_base[p]; }
+  __device__ uint64_t out_base(uint32_t p) const { return S.out_base[p]; }
+};
+
+struct UniformGeom {
+  uint64_t in0, out0, in_stride, out_stride;
+  uint64_t dead;   // wave mask of packets dropped at the header check (open)
+  uint32_t W, nr;  // datagram length and rounds, same for every packet
+  __device__ bool live(uint32_t p, uint32_t r) const { return r < nr && !((dead >> p) & 1u); }
+  __device__ uint32_t wlen(uint32_t) const { return W; }
+  __device__ uint64_t in_base(uint32_t p) const { return in0 + (uint64_t)p * in_stride; }
+  __device__ uint64_t out_base(uint32_t p) const { return out0 + (uint64_t)p * out_stride; }
+};
+
 // Cooperative LDS-DMA load of round r: instruction j carries packets 8j..8j+7,
 // lane i moves 16 bytes (chunk (i&7)^swz(p)) of packet p = 8j + i/8.
-template <bool kSeal>
-__device__ __forceinline__ void stage_in(WaveStage &S, uint32_t lane, uint32_t r) {
+template <bool kSeal, class Geom>
+__device__ __forceinline__ void stage_in(WaveStage &S, const Geom &g, uint32_t lane, uint32_t r) {
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t p = 8u * j + (lane >> 3);
     const uint32_t k = (lane & 7u) ^ swz(p);
     const uint32_t w = kRun * r + 16u * k;
-    const uint32_t W = S.wlen[p];
-    if (r < S.nruns[p] && w >= Ranges<kSeal>::in_lo() && w < Ranges<kSeal>::in_hi(W)) {
-      const uint8_t *g = reinterpret_cast<const uint8_t *>(S.in_base[p]) + w;
-      __builtin_amdgcn_global_load_lds(g, &S.run[64u * j], 16, 0, 0);
+    if (g.live(p, r) && w >= Ranges<kSeal>::in_lo() && w < Ranges<kSeal>::in_hi(g.wlen(p))) {
+      const uint8_t *src = reinterpret_cast<const uint8_t *>(g.in_base(p)) + w;
+      __builtin_amdgcn_global_load_lds(src, &S.run[64u * j], 16, 0, 0);
     }
   }
 }
 
 // Cooperative store of round r (same shape); the last chunk of a packet may be partial.
-template <bool kSeal>
-__device__ __forceinline__ void stage_out(WaveStage &S, uint32_t lane, uint32_t r) {
+template <bool kSeal, class Geom>
+__device__ __forceinline__ void stage_out(WaveStage &S, const Geom &g, uint32_t lane, uint32_t r) {
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t p = 8u * j + (lane >> 3);
     const uint32_t k = (lane & 7u) ^ swz(p);
     const uint32_t w = kRun * r + 16u * k;
-    const uint32_t W = S.wlen[p];
-    const uint32_t hi = Ranges<kSeal>::out_hi(W);
-    if (r < S.nruns[p] && w >= Ranges<kSeal>::out_lo() && w < hi) {
+    const uint32_t hi = Ranges<kSeal>::out_hi(g.wlen(p));
+    if (g.live(p, r) && w >= Ranges<kSeal>::out_lo() && w < hi) {
       const uint4 v = S.run[64u * j + lane];
-      uint8_t *g = reinterpret_cast<uint8_t *>(S.out_base[p]) + w;
+      uint8_t *dst = reinterpret_cast<uint8_t *>(g.out_base(p)) + w;
       const uint32_t n = hi - w;
       if (n >= 16u) {
-        *reinterpret_cast<uint4 *>(g) = v;
+        *reinterpret_cast<uint4 *>(dst) = v;
       } else {
         const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-        store_partial(g, wv, (int)n);
+        store_partial(dst, wv, (int)n);
+      }
+    }
+  }
+}
+
+// Uniform-geometry forms: buffer instructions with a wave-uniform resource
+// (SGPRs) whose base is the wave's first packet, a wave-uniform soffset
+// (8j packets + 128r bytes) and a 32-bit per-lane voffset -- 2 offset VGPRs
+// for all 16 memory instructions of a round instead of 16 64-bit addresses.
+// For p = 8j + (lane>>3): swz(p) = (lane>>4) ^ 4*(j&1).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(uint64_t base) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+
+template <bool kSeal>
+__device__ __forceinline__ void stage_in(WaveStage &S, const UniformGeom &g, uint32_t lane,
+                                         uint32_t r) {
+  if (r >= g.nr) return;
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0);
+  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
+  const uint32_t stride = (uint32_t)g.in_stride;
+  const uint32_t off0 = y * stride + 16u * k0, off1 = y * stride + 16u * k1;
+  const uint32_t hi = Ranges<kSeal>::in_hi(g.W);
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j) {
+    const uint32_t k = (j & 1u) ? k1 : k0;
+    const uint32_t w = kRun * r + 16u * k;
+    const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
+    if (!dead && w >= Ranges<kSeal>::in_lo() && w < hi)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &S.run[64u * j], 16, (j & 1u) ? off1 : off0,
+                                               8u * j * stride + kRun * r, 0, 0);
+  }
+}
+
+template <bool kSeal>
+__device__ __forceinline__ void stage_out(WaveStage &S, const UniformGeom &g, uint32_t lane,
+                                          uint32_t r) {
+  if (r >= g.nr) return;
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0);
+  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
+  const uint32_t stride = (uint32_t)g.out_stride;
+  const uint32_t off0 = y * stride + 16u * k0, off1 = y * stride + 16u * k1;
+  const uint32_t hi = Ranges<kSeal>::out_hi(g.W);
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j) {
+    const uint32_t k = (j & 1u) ? k1 : k0;
+    const uint32_t w = kRun * r + 16u * k;
+    const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
+    if (!dead && w >= Ranges<kSeal>::out_lo() && w < hi) {
+      const uint4 v = S.run[64u * j + lane];
+      const uint32_t voff = (j & 1u) ? off1 : off0, soff = 8u * j * stride + kRun * r;
+      const uint32_t n = hi - w;
+      if (n >= 16u) {
+        const u32x4 vv = {v.x, v.y, v.z, v.w};
+        __builtin_amdgcn_raw_buffer_store_b128(vv, rs, voff, soff, 0);
+      } else {
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+        store_partial(reinterpret_cast<uint8_t *>(g.out0) + soff + voff, wv, (int)n);
       }
     }
   }
@@ -185,13 +271,16 @@ struct PacketJob {
   int32_t status;
 };
 
-template <bool kSeal, bool kUniformKey>
-__device__ __forceinline__ void run_wave(WaveStage &S, uint32_t lane, PacketJob job,
+// The owner lane's side of a packet: everything but the cooperative memory
+// moves.  kUniform = every lane of the wave is live with the same length
+// (strided batches); then P, W and the round count are wave-uniform.
+template <bool kSeal, bool kUniform, class Geom>
+__device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
                                          int32_t *status_out) {
   // ---- per-packet setup (owner lane) ------------------------------------
   uint32_t W = 0, P = 0;
-  if (job.status == WG_STATUS_OK) {
+  if (kUniform || job.status == WG_STATUS_OK) {
     if (kSeal) {
       P = job.len;
       W = P + WG_DATA_OVERHEAD_SZ;
@@ -203,21 +292,25 @@ __device__ __forceinline__ void run_wave(WaveStage &S, uint32_t lane, PacketJob 
     }
   }
   uint32_t my_runs = job.status == WG_STATUS_OK ? (W + kRun - 1) / kRun : 0u;
-  S.in_base[lane] = job.in_base;
-  S.out_base[lane] = job.out_base;
-  S.wlen[lane] = W;
-  S.nruns[lane] = my_runs;
-  const uint32_t rounds = wave_max(my_runs);
+  uint32_t rounds;
+  if constexpr (kUniform) {
+    rounds = my_runs;  // uniform: job.len is a kernel argument
+  } else {
+    S.in_base[lane] = job.in_base;
+    S.out_base[lane] = job.out_base;
+    S.wlen[lane] = W;
+    S.nruns[lane] = my_runs;
+    rounds = wave_max(my_runs);
+  }
 
   uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t sidx = 0;
-  if (job.status == WG_STATUS_OK) {
+  if (kUniform || job.status == WG_STATUS_OK) {
     const uint4 a = ld16(keys + 32u * job.slot), b = ld16(keys + 32u * job.slot + 16u);
     key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
     key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
     sidx = key_index[job.slot];
   }
-  (void)kUniformKey;
 
   Poly poly;
   uint32_t s[4] = {0, 0, 0, 0}, ks_save[4] = {0, 0, 0, 0};
@@ -236,7 +329,7 @@ __device__ __forceinline__ void run_wave(WaveStage &S, uint32_t lane, PacketJob 
   if (kSeal && my_runs) one_time_key();  // overlaps the first DMA
 
   for (uint32_t r = 0; r < rounds; ++r) {
-    stage_in<kSeal>(S, lane, r);
+    stage_in<kSeal>(S, g, lane, r);
     lds_wait_dma();
     if (r < my_runs) {
       const uint32_t row = 8u * lane, sw = swz(lane);
@@ -247,13 +340,14 @@ __device__ __forceinline__ void run_wave(WaveStage &S, uint32_t lane, PacketJob 
           if (h.x != WG_MSG_DATA) job.status = WG_STATUS_INVALID_PACKET;
           else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
           if (job.status != WG_STATUS_OK) {
-            my_runs = 0;
-            S.nruns[lane] = 0;  // nothing of this packet is stored
+            my_runs = 0;  // nothing of this packet is stored
+            if (!kUniform) S.nruns[lane] = 0;
           } else {
             n1 = h.z;
             n2 = h.w;
             one_time_key();
           }
+          if constexpr (kUniform) g.dead = __ballot(job.status != WG_STATUS_OK);
         }
         // keep the raw tail bytes before the slots are decrypted in place
         if (my_runs) {
@@ -299,7 +393,7 @@ __device__ __forceinline__ void run_wave(WaveStage &S, uint32_t lane, PacketJob 
         }
       }
     }
-    stage_out<kSeal>(S, lane, r);
+    stage_out<kSeal>(S, g, lane, r);
   }
 
   if (!kSeal && job.status == WG_STATUS_OK) {
@@ -328,28 +422,45 @@ __device__ __forceinline__ void run_wave(WaveStage &S, uint32_t lane, PacketJob 
 // ---------------------------------------------------------------------------
 // kernels: 4 independent waves per workgroup, each with its own LDS stage
 // ---------------------------------------------------------------------------
-template <bool kSeal>
-__global__ __launch_bounds__(kBlockThreads) void aead_strided_kernel(StridedParams prm) {
+// Strided batches: kTail = false covers the whole waves [0, n & ~63) with the
+// uniform geometry; kTail = true is a one-wave launch for the n % 64 packets
+// left over (generic geometry), so the hot kernel carries no generic path.
+template <bool kSeal, bool kTail>
+__global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_strided_kernel(
+    StridedParams prm) {
   __shared__ WaveStage stage[kWaves];
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint32_t pkt0 = (blockIdx.x * kWaves + wave) * 64u;
-  if (pkt0 >= prm.n) return;  // wave-uniform
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform
+  const uint32_t pkt0 = kTail ? (prm.n & ~63u) : (blockIdx.x * kWaves + wave) * 64u;
+  if (kTail ? wave != 0 : pkt0 + 64u > prm.n) return;  // wave-uniform
   const uint32_t i = pkt0 + lane;
   PacketJob job;
   job.slot = prm.key_slot;
   job.len = prm.len;
   job.counter = prm.counter_base + i;
-  job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
-  const uint64_t src = reinterpret_cast<uint64_t>(prm.src) + (uint64_t)i * prm.src_stride;
-  const uint64_t dst = reinterpret_cast<uint64_t>(prm.dst) + (uint64_t)i * prm.dst_stride;
-  job.in_base = kSeal ? src - 16u : src;    // plaintext side is addressed at w - 16
-  job.out_base = kSeal ? dst : dst - 16u;
-  run_wave<kSeal, true>(stage[wave], lane, job, prm.keys, prm.key_index,
-                        (prm.status && i < prm.n) ? prm.status + i : nullptr);
+  const uint64_t src0 = reinterpret_cast<uint64_t>(prm.src) + (uint64_t)pkt0 * prm.src_stride;
+  const uint64_t dst0 = reinterpret_cast<uint64_t>(prm.dst) + (uint64_t)pkt0 * prm.dst_stride;
+  // the plaintext side is addressed at wire coordinate - 16
+  const uint64_t in0 = kSeal ? src0 - 16u : src0, out0 = kSeal ? dst0 : dst0 - 16u;
+  job.in_base = in0 + (uint64_t)lane * prm.src_stride;
+  job.out_base = out0 + (uint64_t)lane * prm.dst_stride;
+  int32_t *st = (prm.status && i < prm.n) ? prm.status + i : nullptr;
+  if constexpr (!kTail) {
+    job.status = WG_STATUS_OK;
+    const uint32_t W = kSeal ? prm.len + WG_DATA_OVERHEAD_SZ : prm.len;
+    UniformGeom g{in0, out0, prm.src_stride, prm.dst_stride, 0ull, W,
+                  (kSeal || prm.len >= WG_DATA_OVERHEAD_SZ) ? (W + kRun - 1) / kRun : 0u};
+    run_wave<kSeal, true>(stage[wave], g, lane, job, prm.keys, prm.key_index, st);
+  } else {
+    job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
+    LdsGeom g{stage[wave]};
+    run_wave<kSeal, false>(stage[wave], g, lane, job, prm.keys, prm.key_index, st);
+  }
 }
 
 template <bool kSeal>
-__global__ __launch_bounds__(kBlockThreads) void aead_desc_kernel(DescParams prm) {
+__global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_desc_kernel(
+    DescParams prm) {
   __shared__ WaveStage stage[kWaves];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t pkt0 = (blockIdx.x * kWaves + wave) * 64u;
@@ -374,12 +485,15 @@ __global__ __launch_bounds__(kBlockThreads) void aead_desc_kernel(DescParams prm
     else if (((d.src_off | d.dst_off) & 15u) != 0u) job.status = WG_STATUS_MISALIGNED;
     else job.status = WG_STATUS_OK;
   }
-  run_wave<kSeal, false>(stage[wave], lane, job, prm.keys, prm.key_index,
+  LdsGeom g{stage[wave]};
+  run_wave<kSeal, false>(stage[wave], g, lane, job, prm.keys, prm.key_index,
                          i < prm.n ? prm.status + i : nullptr);
 }
 
-template __global__ void aead_strided_kernel<true>(StridedParams);
-template __global__ void aead_strided_kernel<false>(StridedParams);
+template __global__ void aead_strided_kernel<true, false>(StridedParams);
+template __global__ void aead_strided_kernel<false, false>(StridedParams);
+template __global__ void aead_strided_kernel<true, true>(StridedParams);
+template __global__ void aead_strided_kernel<false, true>(StridedParams);
 template __global__ void aead_desc_kernel<true>(DescParams);
 template __global__ void aead_desc_kernel<false>(DescParams);
 

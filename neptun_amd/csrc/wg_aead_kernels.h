@@ -29,7 +29,7 @@ struct DescParams {
   uint32_t n, key_slots;
 };
 
-template <bool kSeal> __global__ void aead_strided_kernel(StridedParams prm);
+template <bool kSeal, bool kTail> __global__ void aead_strided_kernel(StridedParams prm);
 template <bool kSeal> __global__ void aead_desc_kernel(DescParams prm);
 
 }  // namespace wg

@@ -72,39 +72,82 @@ __device__ __forceinline__ void poly_init(Poly &p, const uint32_t ks0[8]) {
   p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
 }
 
+#ifndef WG_POLY_ASM
+#define WG_POLY_ASM 1
+#endif
+
+#if WG_POLY_ASM
+// 32x32+64 -> 64 multiply-add, kept as written: hipcc otherwise re-associates
+// the carry-seeded chains below into zero-seeded mads + v_lshl_add_u64 adds,
+// which costs ~13 extra half-rate ops per 16-byte block.
+__device__ __forceinline__ uint64_t mad_c(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t d, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+#else
+__device__ __forceinline__ uint64_t mad_c(uint32_t a, uint32_t b, uint64_t c) { return mad(a, b, c); }
+#endif
+
 // h = (h + m + 2^128) * r  (partially reduced mod 2^130 - 5)
 __device__ __forceinline__ void poly_block(Poly &p, uint32_t m0, uint32_t m1, uint32_t m2,
                                            uint32_t m3) {
+  uint32_t h0, h1, h2, h3, h4;
+#if WG_POLY_ASM
+  // h += m + 2^128: one carry chain through vcc
+  asm("v_add_co_u32 %0, vcc, %5, %6\n\t"
+      "v_addc_co_u32 %1, vcc, %7, %8, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, %9, %10, vcc\n\t"
+      "v_addc_co_u32 %3, vcc, %11, %12, vcc\n\t"
+      "v_addc_co_u32 %4, vcc, 1, %13, vcc"
+      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(h4)
+      : "v"(p.h0), "v"(m0), "v"(p.h1), "v"(m1), "v"(p.h2), "v"(m2), "v"(p.h3), "v"(m3), "v"(p.h4)
+      : "vcc");
+#else
   uint64_t t = (uint64_t)p.h0 + m0;
-  const uint32_t h0 = (uint32_t)t;
+  h0 = (uint32_t)t;
   t = (uint64_t)p.h1 + m1 + (t >> 32);
-  const uint32_t h1 = (uint32_t)t;
+  h1 = (uint32_t)t;
   t = (uint64_t)p.h2 + m2 + (t >> 32);
-  const uint32_t h2 = (uint32_t)t;
+  h2 = (uint32_t)t;
   t = (uint64_t)p.h3 + m3 + (t >> 32);
-  const uint32_t h3 = (uint32_t)t;
-  uint32_t h4 = p.h4 + (uint32_t)(t >> 32) + 1u;  // + 2^128 (full 16-byte block)
-  // d_j = sum_i h_i r_{j-i} with 2^128 == 5/4 folding (h_i r_j, i+j >= 4 -> h_i s_j)
-  const uint64_t d0 = mad(h3, p.s1, mad(h2, p.s2, mad(h1, p.s3, (uint64_t)h0 * p.r0)));
+  h3 = (uint32_t)t;
+  h4 = p.h4 + (uint32_t)(t >> 32) + 1u;  // + 2^128 (full 16-byte block)
+#endif
+  // d_j = sum_i h_i r_{j-i} with 2^128 == 5/4 folding (h_i r_j, i+j >= 4 -> h_i s_j);
+  // each chain is seeded with the carry out of the previous one
+  const uint64_t d0 = mad_c(h3, p.s1, mad_c(h2, p.s2, mad_c(h1, p.s3, mad_c(h0, p.r0, 0ull))));
   const uint64_t d1 =
-      mad(h4, p.s1, mad(h3, p.s2, mad(h2, p.s3, mad(h1, p.r0, mad(h0, p.r1, d0 >> 32)))));
+      mad_c(h4, p.s1, mad_c(h3, p.s2, mad_c(h2, p.s3, mad_c(h1, p.r0, mad_c(h0, p.r1, d0 >> 32)))));
   const uint64_t d2 =
-      mad(h4, p.s2, mad(h3, p.s3, mad(h2, p.r0, mad(h1, p.r1, mad(h0, p.r2, d1 >> 32)))));
+      mad_c(h4, p.s2, mad_c(h3, p.s3, mad_c(h2, p.r0, mad_c(h1, p.r1, mad_c(h0, p.r2, d1 >> 32)))));
   const uint64_t d3 =
-      mad(h4, p.s3, mad(h3, p.r0, mad(h2, p.r1, mad(h1, p.r2, mad(h0, p.r3, d2 >> 32)))));
-  h4 = h4 * p.r0 + (uint32_t)(d3 >> 32);
+      mad_c(h4, p.s3, mad_c(h3, p.r0, mad_c(h2, p.r1, mad_c(h1, p.r2, mad_c(h0, p.r3, d2 >> 32)))));
+  h4 = (uint32_t)mad_c(h4, p.r0, d3 >> 32);
   // fold bits >= 130: c = 5 * (h4 >> 2)
   const uint32_t c = (h4 >> 2) + (h4 & ~3u);
   h4 &= 3u;
-  t = (uint64_t)(uint32_t)d0 + c;
-  p.h0 = (uint32_t)t;
-  t = (uint64_t)(uint32_t)d1 + (t >> 32);
-  p.h1 = (uint32_t)t;
-  t = (uint64_t)(uint32_t)d2 + (t >> 32);
-  p.h2 = (uint32_t)t;
-  t = (uint64_t)(uint32_t)d3 + (t >> 32);
-  p.h3 = (uint32_t)t;
-  p.h4 = h4 + (uint32_t)(t >> 32);
+#if WG_POLY_ASM
+  asm("v_add_co_u32 %0, vcc, %5, %6\n\t"
+      "v_addc_co_u32 %1, vcc, 0, %7, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, 0, %8, vcc\n\t"
+      "v_addc_co_u32 %3, vcc, 0, %9, vcc\n\t"
+      "v_addc_co_u32 %4, vcc, 0, %10, vcc"
+      : "=&v"(p.h0), "=&v"(p.h1), "=&v"(p.h2), "=&v"(p.h3), "=&v"(p.h4)
+      : "v"(c), "v"((uint32_t)d0), "v"((uint32_t)d1), "v"((uint32_t)d2), "v"((uint32_t)d3),
+        "v"(h4)
+      : "vcc");
+#else
+  uint64_t t2 = (uint64_t)(uint32_t)d0 + c;
+  p.h0 = (uint32_t)t2;
+  t2 = (uint64_t)(uint32_t)d1 + (t2 >> 32);
+  p.h1 = (uint32_t)t2;
+  t2 = (uint64_t)(uint32_t)d2 + (t2 >> 32);
+  p.h2 = (uint32_t)t2;
+  t2 = (uint64_t)(uint32_t)d3 + (t2 >> 32);
+  p.h3 = (uint32_t)t2;
+  p.h4 = h4 + (uint32_t)(t2 >> 32);
+#endif
 }
 
 // tag = (h mod p) + s mod 2^128; h < 5*2^128 < 2p so one conditional subtract

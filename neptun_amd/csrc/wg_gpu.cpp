@@ -165,12 +165,24 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
   wg::StridedParams prm{ctx->d_keys, ctx->d_key_index, src, dst, status, src_stride,
                         dst_stride, counter_base, n, len, key_slot};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (seal)
-    hipLaunchKernelGGL(wg::aead_strided_kernel<true>, dim3(grid_for(n)), dim3(wg::kBlockThreads),
-                       0, s, prm);
-  else
-    hipLaunchKernelGGL(wg::aead_strided_kernel<false>, dim3(grid_for(n)),
-                       dim3(wg::kBlockThreads), 0, s, prm);
+  const uint32_t full_waves = n / 64u, waves_per_block = wg::kBlockThreads / 64u;
+  if (full_waves) {
+    const dim3 grid((full_waves + waves_per_block - 1) / waves_per_block);
+    if (seal)
+      hipLaunchKernelGGL((wg::aead_strided_kernel<true, false>), grid, dim3(wg::kBlockThreads), 0,
+                         s, prm);
+    else
+      hipLaunchKernelGGL((wg::aead_strided_kernel<false, false>), grid, dim3(wg::kBlockThreads), 0,
+                         s, prm);
+  }
+  if (n % 64u) {  // the last, partial wave: generic per-lane geometry
+    if (seal)
+      hipLaunchKernelGGL((wg::aead_strided_kernel<true, true>), dim3(1), dim3(wg::kBlockThreads), 0,
+                         s, prm);
+    else
+      hipLaunchKernelGGL((wg::aead_strided_kernel<false, true>), dim3(1), dim3(wg::kBlockThreads),
+                         0, s, prm);
+  }
   WG_HIP(hipGetLastError(), "strided: launch");
   return WG_RC_OK;
 }
