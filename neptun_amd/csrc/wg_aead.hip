@@ -40,6 +40,14 @@ constexpr uint32_t kRun = 128;    // bytes of one packet per round (one cache li
 constexpr uint32_t kChunks = 8;   // 16-byte chunks per run
 constexpr uint32_t kWaves = kBlockThreads / 64;
 
+// timing-only ablations (wrong outputs): skip the HBM traffic / skip the crypto
+#ifndef WG_ABLATE_NO_MEM
+#define WG_ABLATE_NO_MEM 0
+#endif
+#ifndef WG_ABLATE_NO_CRYPT
+#define WG_ABLATE_NO_CRYPT 0
+#endif
+
 #ifndef WG_WAVES_PER_SIMD
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
 #endif
@@ -329,7 +337,9 @@ __device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, P
   if (kSeal && my_runs) one_time_key();  // overlaps the first DMA
 
   for (uint32_t r = 0; r < rounds; ++r) {
+#if !WG_ABLATE_NO_MEM
     stage_in<kSeal>(S, g, lane, r);
+#endif
     lds_wait_dma();
     if (r < my_runs) {
       const uint32_t row = 8u * lane, sw = swz(lane);
@@ -365,7 +375,7 @@ __device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, P
         // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
         S.run[row + (0u ^ sw)] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
       }
-      if (my_runs) {
+      if (my_runs && !WG_ABLATE_NO_CRYPT) {
         crypt_round<kSeal>(S, lane, r, P, key, n1, n2, poly, ks_save);
         if (kSeal) {
           if (r > 0 && ((wt + 16u) >> 7) == r && (wt >> 7) == r - 1u && q) {
@@ -393,7 +403,9 @@ __device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, P
         }
       }
     }
+#if !WG_ABLATE_NO_MEM
     stage_out<kSeal>(S, g, lane, r);
+#endif
   }
 
   if (!kSeal && job.status == WG_STATUS_OK) {

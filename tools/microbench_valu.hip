@@ -39,6 +39,12 @@ __global__ void NAME(uint32_t* out, uint32_t seed) {                            
 #define MULHI24(k) "v_mul_hi_u32_u24 %" #k ", %" #k ", %8\n"
 #define DOT2(k) "v_dot2_u32_u16 %" #k ", %" #k ", %8, %9\n"
 #define LSHLADD(k) "v_lshl_add_u32 %" #k ", %" #k ", 3, %9\n"
+#define XORSDWA(k) "v_xor_b32_sdwa %" #k ", %" #k ", %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n"
+#define ADDSDWA(k) "v_add_u32_sdwa %" #k ", %" #k ", %8 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1\n"
+#define PKADD16(k) "v_pk_add_u16 %" #k ", %" #k ", %8\n"
+#define LSHLOR(k) "v_lshl_or_b32 %" #k ", %" #k ", 7, %9\n"
+#define ALIGNBYTE(k) "v_alignbyte_b32 %" #k ", %" #k ", %" #k ", 2\n"
+#define ADDCO(k) "v_add_co_u32 %" #k ", vcc, %" #k ", %8\n"
 
 KERNEL32(k_add, OP8(ADD))
 KERNEL32(k_xor, OP8(XOR))
@@ -53,6 +59,34 @@ KERNEL32(k_mul24, OP8(MUL24))
 KERNEL32(k_mulhi24, OP8(MULHI24))
 KERNEL32(k_dot2, OP8(DOT2))
 KERNEL32(k_lshladd, OP8(LSHLADD))
+KERNEL32(k_xorsdwa, OP8(XORSDWA))
+KERNEL32(k_addsdwa, OP8(ADDSDWA))
+KERNEL32(k_pkadd16, OP8(PKADD16))
+KERNEL32(k_lshlor, OP8(LSHLOR))
+KERNEL32(k_alignbyte, OP8(ALIGNBYTE))
+KERNEL32(k_addco, OP8(ADDCO))
+// mixes: per chain k one add, one xor, one alignbit (ChaCha's 2:1 full:half ratio)
+#define MIX_AXR(k) "v_add_u32 %" #k ", %" #k ", %8\n" "v_xor_b32 %" #k ", %" #k ", %9\n" "v_alignbit_b32 %" #k ", %" #k ", %" #k ", 20\n"
+#define MIX_AX(k) "v_add_u32 %" #k ", %" #k ", %8\n" "v_xor_b32 %" #k ", %" #k ", %9\n"
+#define MIX_AR(k) "v_add_u32 %" #k ", %" #k ", %8\n" "v_alignbit_b32 %" #k ", %" #k ", %" #k ", 20\n"
+#define SHL(k) "v_lshlrev_b32 %" #k ", 3, %" #k "\n"
+#define ORR(k) "v_or_b32 %" #k ", %" #k ", %8\n"
+#define ANDD(k) "v_and_b32 %" #k ", %" #k ", %8\n"
+KERNEL32(k_mix_axr, OP8(MIX_AXR))
+KERNEL32(k_mix_ax, OP8(MIX_AX))
+KERNEL32(k_mix_ar, OP8(MIX_AR))
+KERNEL32(k_shl, OP8(SHL))
+KERNEL32(k_or, OP8(ORR))
+KERNEL32(k_and, OP8(ANDD))
+// grouped runs: all 8 chains' adds, then all xors, then all rotates (4 parallel QRs' shape)
+#define GRP_AXR OP8(ADD) OP8(XOR) OP8(ALIGNBIT)
+#define GRP_AR OP8(ADD) OP8(ALIGNBIT)
+#define GRP_AAXR OP8(ADD) OP8(XOR) OP8(ADD) OP8(ALIGNBIT)
+#define GRP_16R OP8(ADD) OP8(XOR) OP8(ADD) OP8(XOR) OP8(ADD) OP8(XOR) OP8(ADD) OP8(XOR) OP8(ALIGNBIT)
+KERNEL32(k_grp_axr, GRP_AXR)
+KERNEL32(k_grp_ar, GRP_AR)
+KERNEL32(k_grp_aaxr, GRP_AAXR)
+KERNEL32(k_grp_16r, GRP_16R)
 
 // 64-bit destination ops: 8 chains of u64
 #define KERNEL64(NAME, ASM)                                                     \
@@ -88,11 +122,17 @@ int main() {
     {"v_perm_b32", k_perm}, {"v_add3_u32", k_add3}, {"v_xad_u32", k_xad},
     {"v_bitop3_b32", k_bitop3}, {"v_mul_lo_u32", k_mullo}, {"v_mul_hi_u32", k_mulhi},
     {"v_mul_u32_u24", k_mul24}, {"v_mul_hi_u32_u24", k_mulhi24}, {"v_dot2_u32_u16", k_dot2},
-    {"v_lshl_add_u32", k_lshladd}, {"v_mad_u64_u32", k_mad64}, {"v_fma_f64", k_fma64},
+    {"v_lshl_add_u32", k_lshladd}, {"v_xor_b32_sdwa", k_xorsdwa}, {"v_add_u32_sdwa", k_addsdwa},
+    {"v_pk_add_u16", k_pkadd16}, {"v_lshl_or_b32", k_lshlor}, {"v_alignbyte_b32", k_alignbyte},
+    {"v_add_co_u32(vcc)", k_addco}, {"mix add,xor,alignbit /3", k_mix_axr},
+    {"mix add,xor /2", k_mix_ax}, {"mix add,alignbit /2", k_mix_ar}, {"v_lshlrev_b32", k_shl},
+    {"v_or_b32", k_or}, {"v_and_b32", k_and}, {"grp add8,xor8,rot8 /3", k_grp_axr},
+    {"grp add8,rot8 /2", k_grp_ar}, {"grp add8,xor8,add8,rot8 /4", k_grp_aaxr},
+    {"grp 64 simple, rot8 /9", k_grp_16r}, {"v_mad_u64_u32", k_mad64}, {"v_fma_f64", k_fma64},
     {"v_lshl_add_u64", k_lshladd64}, {"v_lshrrev_b64", k_lshr64},
   };
   const int threads = 256;
-  for (int wps : {4, 8}) {  // waves per SIMD
+  for (int wps : {2, 4}) {  // waves per SIMD
     int blocks = cus * wps;  // 256 threads = 4 waves = 1 per SIMD per block
     uint32_t* out;
     CHECK(hipMalloc(&out, (size_t)blocks * threads * 4));
