@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "neptun_gpu.h"
 #include "wg_aead_kernels.h"
 #include "wg_crypto.h"
@@ -52,12 +54,22 @@ constexpr uint32_t kWaves = kBlockThreads / 64;
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
 #endif
 
+#ifndef WG_PREFETCH
+#define WG_PREFETCH 0  // 1: double-buffered LDS stage (round r+1 DMA overlaps round r)
+#endif
+constexpr uint32_t kBufs = WG_PREFETCH ? 2 : 1;
+
+// LDS of one wave.  Generic geometry: one 8 KiB run buffer + per-packet tables.
 struct WaveStage {
-  uint4 run[64 * kChunks];  // [packet][chunk ^ swz(packet)], 8 KiB
-  uint64_t in_base[64];     // wire-coordinate origin of the input side
-  uint64_t out_base[64];    // wire-coordinate origin of the output side
-  uint32_t wlen[64];        // W = datagram length (P + 32)
-  uint32_t nruns[64];       // rounds this packet takes part in; 0 = none
+  uint4 run[1][64 * kChunks];  // [buffer][packet][chunk ^ swz(packet)], 8 KiB
+  uint64_t in_base[64];        // wire-coordinate origin of the input side
+  uint64_t out_base[64];       // wire-coordinate origin of the output side
+  uint32_t wlen[64];           // W = datagram length (P + 32)
+  uint32_t nruns[64];          // rounds this packet takes part in; 0 = none
+};
+// Uniform geometry: kBufs run buffers, no tables (addresses are arithmetic).
+struct WaveStageUniform {
+  uint4 run[kBufs][64 * kChunks];
 };
 
 // XOR swizzle of a packet's 8 chunk slots: lane L reading chunk k of its own
@@ -108,7 +120,7 @@ struct UniformGeom {
 // Cooperative LDS-DMA load of round r: instruction j carries packets 8j..8j+7,
 // lane i moves 16 bytes (chunk (i&7)^swz(p)) of packet p = 8j + i/8.
 template <bool kSeal, class Geom>
-__device__ __forceinline__ void stage_in(WaveStage &S, const Geom &g, uint32_t lane, uint32_t r) {
+__device__ __forceinline__ void stage_in(uint4 *run, const Geom &g, uint32_t lane, uint32_t r) {
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t p = 8u * j + (lane >> 3);
@@ -116,14 +128,14 @@ __device__ __forceinline__ void stage_in(WaveStage &S, const Geom &g, uint32_t l
     const uint32_t w = kRun * r + 16u * k;
     if (g.live(p, r) && w >= Ranges<kSeal>::in_lo() && w < Ranges<kSeal>::in_hi(g.wlen(p))) {
       const uint8_t *src = reinterpret_cast<const uint8_t *>(g.in_base(p)) + w;
-      __builtin_amdgcn_global_load_lds(src, &S.run[64u * j], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, &run[64u * j], 16, 0, 0);
     }
   }
 }
 
 // Cooperative store of round r (same shape); the last chunk of a packet may be partial.
 template <bool kSeal, class Geom>
-__device__ __forceinline__ void stage_out(WaveStage &S, const Geom &g, uint32_t lane, uint32_t r) {
+__device__ __forceinline__ void stage_out(uint4 *run, const Geom &g, uint32_t lane, uint32_t r) {
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t p = 8u * j + (lane >> 3);
@@ -131,7 +143,7 @@ __device__ __forceinline__ void stage_out(WaveStage &S, const Geom &g, uint32_t 
     const uint32_t w = kRun * r + 16u * k;
     const uint32_t hi = Ranges<kSeal>::out_hi(g.wlen(p));
     if (g.live(p, r) && w >= Ranges<kSeal>::out_lo() && w < hi) {
-      const uint4 v = S.run[64u * j + lane];
+      const uint4 v = run[64u * j + lane];
       uint8_t *dst = reinterpret_cast<uint8_t *>(g.out_base(p)) + w;
       const uint32_t n = hi - w;
       if (n >= 16u) {
@@ -149,57 +161,70 @@ __device__ __forceinline__ void stage_out(WaveStage &S, const Geom &g, uint32_t 
 // (8j packets + 128r bytes) and a 32-bit per-lane voffset -- 2 offset VGPRs
 // for all 16 memory instructions of a round instead of 16 64-bit addresses.
 // For p = 8j + (lane>>3): swz(p) = (lane>>4) ^ 4*(j&1).
+// Every round issues exactly 8 loads and 8 full-chunk stores: a lane with no
+// byte to move gets an offset past the resource's num_records, which the
+// buffer range check turns into no memory access.  That keeps vmcnt counts
+// static, which the double-buffered prefetch relies on.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kNoAccess = 0x7ffffff0u;  // >= any num_records used below
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(uint64_t base) {
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, 0x7fffffff,
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(uint64_t base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)bytes,
                                            0x00020000);
 }
 
 template <bool kSeal>
-__device__ __forceinline__ void stage_in(WaveStage &S, const UniformGeom &g, uint32_t lane,
+__device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint32_t lane,
                                          uint32_t r) {
-  if (r >= g.nr) return;
-  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0);
-  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
   const uint32_t stride = (uint32_t)g.in_stride;
-  const uint32_t off0 = y * stride + 16u * k0, off1 = y * stride + 16u * k1;
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 64u * stride);
+  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
   const uint32_t hi = Ranges<kSeal>::in_hi(g.W);
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
     const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
-    if (!dead && w >= Ranges<kSeal>::in_lo() && w < hi)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &S.run[64u * j], 16, (j & 1u) ? off1 : off0,
-                                               8u * j * stride + kRun * r, 0, 0);
+    const bool ok = !dead && w >= Ranges<kSeal>::in_lo() && w < hi;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16,
+                                             ok ? y * stride + 16u * k : kNoAccess,
+                                             8u * j * stride + kRun * r, 0, 0);
   }
 }
 
 template <bool kSeal>
-__device__ __forceinline__ void stage_out(WaveStage &S, const UniformGeom &g, uint32_t lane,
+__device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint32_t lane,
                                           uint32_t r) {
-  if (r >= g.nr) return;
-  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0);
-  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
   const uint32_t stride = (uint32_t)g.out_stride;
-  const uint32_t off0 = y * stride + 16u * k0, off1 = y * stride + 16u * k1;
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, 64u * stride);
+  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
   const uint32_t hi = Ranges<kSeal>::out_hi(g.W);
+  bool partial = false;
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
     const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
-    if (!dead && w >= Ranges<kSeal>::out_lo() && w < hi) {
-      const uint4 v = S.run[64u * j + lane];
-      const uint32_t voff = (j & 1u) ? off1 : off0, soff = 8u * j * stride + kRun * r;
-      const uint32_t n = hi - w;
-      if (n >= 16u) {
-        const u32x4 vv = {v.x, v.y, v.z, v.w};
-        __builtin_amdgcn_raw_buffer_store_b128(vv, rs, voff, soff, 0);
-      } else {
+    const bool ok = !dead && w >= Ranges<kSeal>::out_lo() && w < hi;
+    const uint4 v = run[64u * j + lane];
+    const u32x4 vv = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(vv, rs, ok && hi - w >= 16u ? y * stride + 16u * k
+                                                                        : kNoAccess,
+                                           8u * j * stride + kRun * r, 0);
+    partial |= ok && hi - w < 16u;
+  }
+  if (partial) {  // the packet's last, partial chunk (last round only)
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j) {
+      const uint32_t k = (j & 1u) ? k1 : k0;
+      const uint32_t w = kRun * r + 16u * k;
+      const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
+      if (!dead && w >= Ranges<kSeal>::out_lo() && w < hi && hi - w < 16u) {
+        const uint4 v = run[64u * j + lane];
         const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-        store_partial(reinterpret_cast<uint8_t *>(g.out0) + soff + voff, wv, (int)n);
+        store_partial(reinterpret_cast<uint8_t *>(g.out0) + 8u * j * stride + kRun * r +
+                          y * stride + 16u * k,
+                      wv, (int)(hi - w));
       }
     }
   }
@@ -230,13 +255,13 @@ __device__ __forceinline__ void crypt_chunk(uint4 &slot, Poly &p, int m, uint32_
 // block 2r (saved from the previous round), chunks 1-4 are block 2r+1, chunks
 // 5-7 the first three of block 2r+2 (its fourth is saved for round r+1).
 template <bool kSeal>
-__device__ __forceinline__ void crypt_round(WaveStage &S, uint32_t lane, uint32_t r, uint32_t P,
+__device__ __forceinline__ void crypt_round(uint4 *run, uint32_t lane, uint32_t r, uint32_t P,
                                             const uint32_t key[8], uint32_t n1, uint32_t n2,
                                             Poly &p, uint32_t ks_save[4]) {
   const int m0 = (int)(kRun * r) - 16;
   const uint32_t row = 8u * lane, sw = swz(lane);
   if (r > 0 && m0 < (int)P)
-    crypt_chunk<kSeal>(S.run[row + (0u ^ sw)], p, m0, P, ks_save[0], ks_save[1], ks_save[2],
+    crypt_chunk<kSeal>(run[row + (0u ^ sw)], p, m0, P, ks_save[0], ks_save[1], ks_save[2],
                        ks_save[3]);
   if ((int)(kRun * r) < (int)P) {
     uint32_t ks[16];
@@ -245,7 +270,7 @@ __device__ __forceinline__ void crypt_round(WaveStage &S, uint32_t lane, uint32_
     for (int k = 1; k <= 4; ++k) {
       const int m = m0 + 16 * k;
       if (m < (int)P)
-        crypt_chunk<kSeal>(S.run[row + ((uint32_t)k ^ sw)], p, m, P, ks[4 * k - 4],
+        crypt_chunk<kSeal>(run[row + ((uint32_t)k ^ sw)], p, m, P, ks[4 * k - 4],
                            ks[4 * k - 3], ks[4 * k - 2], ks[4 * k - 1]);
     }
   }
@@ -256,7 +281,7 @@ __device__ __forceinline__ void crypt_round(WaveStage &S, uint32_t lane, uint32_
     for (int k = 5; k <= 7; ++k) {
       const int m = m0 + 16 * k;
       if (m < (int)P)
-        crypt_chunk<kSeal>(S.run[row + ((uint32_t)k ^ sw)], p, m, P, ks[4 * k - 20],
+        crypt_chunk<kSeal>(run[row + ((uint32_t)k ^ sw)], p, m, P, ks[4 * k - 20],
                            ks[4 * k - 19], ks[4 * k - 18], ks[4 * k - 17]);
     }
     ks_save[0] = ks[12]; ks_save[1] = ks[13]; ks_save[2] = ks[14]; ks_save[3] = ks[15];
@@ -282,8 +307,8 @@ struct PacketJob {
 // The owner lane's side of a packet: everything but the cooperative memory
 // moves.  kUniform = every lane of the wave is live with the same length
 // (strided batches); then P, W and the round count are wave-uniform.
-template <bool kSeal, bool kUniform, class Geom>
-__device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, PacketJob job,
+template <bool kSeal, bool kUniform, class Stage, class Geom>
+__device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
                                          int32_t *status_out) {
   // ---- per-packet setup (owner lane) ------------------------------------
@@ -336,22 +361,40 @@ __device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, P
   };
   if (kSeal && my_runs) one_time_key();  // overlaps the first DMA
 
-  for (uint32_t r = 0; r < rounds; ++r) {
+  // double buffering only for the uniform geometry (static vmcnt counts)
+  constexpr bool kPrefetch = kUniform && sizeof(S.run) / sizeof(S.run[0]) == 2;
 #if !WG_ABLATE_NO_MEM
-    stage_in<kSeal>(S, g, lane, r);
+  if constexpr (kPrefetch) stage_in<kSeal>(S.run[0], g, lane, 0);
 #endif
+  for (uint32_t r = 0; r < rounds; ++r) {
+    uint4 *run = S.run[kPrefetch ? (r & 1u) : 0u];
+#if !WG_ABLATE_NO_MEM
+    if constexpr (kPrefetch) {
+      if (r + 1u < rounds) {
+        stage_in<kSeal>(S.run[(r + 1u) & 1u], g, lane, r + 1u);
+        // everything older than round r+1's 8 loads is done (round r's DMA)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        lds_wait_dma();
+      }
+    } else {
+      stage_in<kSeal>(run, g, lane, r);
+      lds_wait_dma();
+    }
+#else
     lds_wait_dma();
+#endif
     if (r < my_runs) {
       const uint32_t row = 8u * lane, sw = swz(lane);
       if (!kSeal) {
         if (r == 0) {
           // header: LE32 type | LE32 receiver_idx | LE64 counter (noise/mod.rs:170-180)
-          const uint4 h = S.run[row + (0u ^ sw)];
+          const uint4 h = run[row + (0u ^ sw)];
           if (h.x != WG_MSG_DATA) job.status = WG_STATUS_INVALID_PACKET;
           else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
           if (job.status != WG_STATUS_OK) {
             my_runs = 0;  // nothing of this packet is stored
-            if (!kUniform) S.nruns[lane] = 0;
+            if constexpr (!kUniform) S.nruns[lane] = 0;
           } else {
             n1 = h.z;
             n2 = h.w;
@@ -363,24 +406,24 @@ __device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, P
         if (my_runs) {
           const uint32_t ra = wt >> 7, rb = (wt + 16u) >> 7;
           if (ra == r) {
-            const uint4 v = S.run[row + (((wt >> 4) & 7u) ^ sw)];
+            const uint4 v = run[row + (((wt >> 4) & 7u) ^ sw)];
             rx[0] = v.x; rx[1] = v.y; rx[2] = v.z; rx[3] = v.w;
           }
           if (q && rb == r) {
-            const uint4 v = S.run[row + ((((wt + 16u) >> 4) & 7u) ^ sw)];
+            const uint4 v = run[row + ((((wt + 16u) >> 4) & 7u) ^ sw)];
             rx[4] = v.x; rx[5] = v.y; rx[6] = v.z; rx[7] = v.w;
           }
         }
       } else if (r == 0) {
         // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
-        S.run[row + (0u ^ sw)] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
+        run[row + (0u ^ sw)] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
       }
       if (my_runs && !WG_ABLATE_NO_CRYPT) {
-        crypt_round<kSeal>(S, lane, r, P, key, n1, n2, poly, ks_save);
+        crypt_round<kSeal>(run, lane, r, P, key, n1, n2, poly, ks_save);
         if (kSeal) {
           if (r > 0 && ((wt + 16u) >> 7) == r && (wt >> 7) == r - 1u && q) {
             // tag remainder spilled into this round's first chunk
-            S.run[row + (0u ^ sw)] = make_uint4(tailB[0], tailB[1], tailB[2], tailB[3]);
+            run[row + (0u ^ sw)] = make_uint4(tailB[0], tailB[1], tailB[2], tailB[3]);
           }
           if ((wt >> 7) == r) {
             // all ciphertext is MACed: LE64(aad_len=0) | LE64(ct_len), then the tag
@@ -390,21 +433,21 @@ __device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, P
             const uint32_t ka = (wt >> 4) & 7u;
             uint32_t ct[4] = {0, 0, 0, 0};
             if (q) {
-              const uint4 v = S.run[row + (ka ^ sw)];
+              const uint4 v = run[row + (ka ^ sw)];
               ct[0] = v.x; ct[1] = v.y; ct[2] = v.z; ct[3] = v.w;
             }
             uint32_t w8[8];
             tail_words(ct, tag, (int)q, w8);
-            S.run[row + (ka ^ sw)] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
+            run[row + (ka ^ sw)] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
             tailB[0] = w8[4]; tailB[1] = w8[5]; tailB[2] = w8[6]; tailB[3] = w8[7];
             if (q && ka < 7u)
-              S.run[row + ((ka + 1u) ^ sw)] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
+              run[row + ((ka + 1u) ^ sw)] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
           }
         }
       }
     }
 #if !WG_ABLATE_NO_MEM
-    stage_out<kSeal>(S, g, lane, r);
+    stage_out<kSeal>(run, g, lane, r);
 #endif
   }
 
@@ -440,7 +483,8 @@ __device__ __forceinline__ void run_wave(WaveStage &S, Geom &g, uint32_t lane, P
 template <bool kSeal, bool kTail>
 __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_strided_kernel(
     StridedParams prm) {
-  __shared__ WaveStage stage[kWaves];
+  using Stage = typename std::conditional<kTail, WaveStage, WaveStageUniform>::type;
+  __shared__ Stage stage[kWaves];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform
   const uint32_t pkt0 = kTail ? (prm.n & ~63u) : (blockIdx.x * kWaves + wave) * 64u;
