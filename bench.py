@@ -9,9 +9,11 @@ GPU, contiguous shards, no collective on the data path -> "scaling": "weak").
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+    python bench.py --config 3|4   (supplementary lines for DESIGN.md)
 
 Rank 0 prints one JSON line.  value = Gbit/s of plaintext round-trip goodput
-over all ranks = world * n * P * 8 * K / max_rank(time of K steps).
+over all ranks = sum_ranks(payload bytes per step) * 8 * K / max_rank(time of
+K steps).
 """
 from __future__ import annotations
 
@@ -29,20 +31,163 @@ METRIC = "Gbit/s device-resident ChaCha20-Poly1305 seal+open, 1350B pkts, 1/2/4/
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
+    ap.add_argument("--packets", type=int, default=1 << 20, help="config 2: packets per GPU")
     ap.add_argument("--size", type=int, default=1350)
-    ap.add_argument("--stride", type=int, default=0, help="slot stride (0 = round up to 128)")
+    ap.add_argument("--stride", type=int, default=0, help="config 2 slot stride (0 = round up to 128)")
+    ap.add_argument("--per-size", type=int, default=1 << 18, help="config 3: packets per size")
+    ap.add_argument("--peers", type=int, default=4096, help="config 4")
+    ap.add_argument("--per-peer", type=int, default=4096, help="config 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(threads: int) -> dict | None:
+# ---------------------------------------------------------------------------
+# workloads: each has .step(stream, evs) (events: before seal, between, after
+# open), .verify() -> bool, .packets, .payload_bytes, .launch_bytes
+# {seal, open}, .kernels {seal, open} (rocprof names), .describe() -> dict
+# ---------------------------------------------------------------------------
+class StridedWorkload:
+    """Config 2 / 5: one session, uniform 1350 B, counters = base + lane index."""
+
+    def __init__(self, args, dev, rank, world):
+        import numpy as np
+        import torch
+
+        import neptun_amd
+        from tools import synth
+        self.n, self.P = n, P = args.packets, args.size
+        S = args.stride or synth.round_up(P + 32, 128)
+        if S % 16 or S < P + 32:
+            raise SystemExit("--stride must be a multiple of 16 and hold P + 32 bytes")
+        self.S = S
+        self.ctx = neptun_amd.GpuContext(dev.index, key_slots=1)
+        self.ctx.set_keys(0, synth.keys(1), np.array([synth.RECEIVER_IDX], np.uint32))
+        # shard: rank r owns packets [r*n, (r+1)*n) of the global batch; counters follow
+        self.counter_base = rank * n
+        # NepTUN slot layout (WG_HEADER_OFFSET = 16, device/mod.rs:76): plaintext 16
+        # bytes into each slot, the datagram at the slot start -- both run-aligned
+        self.pt = synth.device_payloads(n, P, S, dev, seed=synth.SEED + rank, offset=16)
+        self.wire = torch.zeros(n * S, dtype=torch.uint8, device=dev)
+        self.back = torch.zeros(n * S, dtype=torch.uint8, device=dev)
+        self.st_seal = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        self.st_open = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        self.packets = n
+        self.payload_bytes = n * P
+        # algorithmic HBM bytes per launch: seal reads P, writes P+32; open the reverse
+        self.launch_bytes = {"seal": n * (2 * P + 32), "open": n * (2 * P + 32)}
+        self.kernels = {"seal": "aead_strided_kernel<true, false>",
+                        "open": "aead_strided_kernel<false, false>"}
+
+    def step(self, stream, evs=None):
+        S, P, n = self.S, self.P, self.n
+        if evs:
+            evs[0].record(stream)
+        self.ctx.seal_strided(n, P, 0, self.counter_base, self.pt.data_ptr() + 16, S, self.wire, S,
+                              self.st_seal, stream)
+        if evs:
+            evs[1].record(stream)
+        self.ctx.open_strided(n, P + 32, 0, self.wire, S, self.back.data_ptr() + 16, S,
+                              self.st_open, stream)
+        if evs:
+            evs[2].record(stream)
+
+    def verify(self):
+        import torch
+        n, S, P = self.n, self.S, self.P
+        ok = int((self.st_seal != 0).sum()) == 0 and int((self.st_open != 0).sum()) == 0
+        return ok and torch.equal(self.back.view(n, S)[:, 16:16 + P], self.pt.view(n, S)[:, 16:16 + P])
+
+    def describe(self, world):
+        return {"workload": f"BASELINE config {'2' if world == 1 else '5'}: {self.n} x {self.P} B "
+                            "packets per GPU, single session, seal then open, device-resident",
+                "packets_per_gpu": self.n, "packet_bytes": self.P, "slot_stride": self.S,
+                "global_packets": world * self.n, "parallelism": f"{world} shard(s), no collective"}
+
+    def close(self):
+        self.ctx.close()
+
+
+class DescWorkload:
+    """Config 3 (mixed MTU, device-side length scheduling) and 4 (4096 peers)."""
+
+    def __init__(self, args, dev, rank, world):
+        import numpy as np
+
+        import neptun_amd
+        from tools import synth, workloads
+        self.cfg = args.config
+        if self.cfg == 3:
+            self.b = workloads.config3(args.per_size, dev, seed=synth.SEED + rank)
+            nkeys = 1
+        else:
+            self.b = workloads.config4(args.peers, args.per_peer, args.size, dev,
+                                       seed=synth.SEED + rank)
+            nkeys = args.peers
+        self.ctx = neptun_amd.GpuContext(dev.index, key_slots=nkeys)
+        keys = synth.keys(nkeys)
+        idx = np.full(nkeys, synth.RECEIVER_IDX, np.uint32) + np.arange(nkeys, dtype=np.uint32)
+        self.ctx.set_keys(0, keys, idx)
+        b = self.b
+        self.packets = b.n
+        P = b.sizes.astype(np.int64)
+        self.payload_bytes = int(P.sum())
+        key_bytes = 32 * b.n if self.cfg == 4 else 0  # per-lane key reads (BASELINE.md config 4)
+        self.launch_bytes = {"seal": int((2 * P + 32).sum()) + key_bytes,
+                             "open": int((2 * P + 32).sum()) + key_bytes}
+        self.kernels = {"seal": "aead_desc_kernel<true>", "open": "aead_desc_kernel<false>"}
+
+    def step(self, stream, evs=None):
+        b, ctx = self.b, self.ctx
+        if evs:
+            evs[0].record(stream)
+        if self.cfg == 3:  # scheduling pass is part of the timed work
+            ctx.plan_batch(True, b.d_seal, b.n, b.order, b.scratch, stream)
+            ctx.seal_batch_ordered(b.d_seal, b.order, b.n, b.pt, b.wire, b.st_seal, stream)
+        else:
+            ctx.seal_batch(b.d_seal, b.n, b.pt, b.wire, b.st_seal, stream)
+        if evs:
+            evs[1].record(stream)
+        if self.cfg == 3:  # open rounds = seal rounds (W = P + 32): same order
+            ctx.open_batch_ordered(b.d_open, b.order, b.n, b.wire, b.out, b.st_open, stream)
+        else:
+            ctx.open_batch(b.d_open, b.n, b.wire, b.out, b.st_open, stream)
+        if evs:
+            evs[2].record(stream)
+
+    def verify(self):
+        b = self.b
+        ok = int((b.st_seal != 0).sum()) == 0 and int((b.st_open != 0).sum()) == 0
+        return ok and b.round_trip_equal()
+
+    def describe(self, world):
+        b = self.b
+        if self.cfg == 3:
+            w = (f"BASELINE config 3: mixed MTU {{64,256,576,1350,8900}} x {b.n // 5} each, seeded "
+                 "interleave, single session, device-side length scheduling included")
+        else:
+            w = (f"BASELINE config 4: {b.n} x {int(b.sizes[0])} B packets over "
+                 f"{self.ctx.key_slots} peers (per-lane key lookup from HBM)")
+        return {"workload": w, "packets_per_gpu": b.n, "payload_bytes_per_gpu": self.payload_bytes,
+                "global_packets": world * b.n, "parallelism": f"{world} shard(s), no collective"}
+
+    def close(self):
+        self.ctx.close()
+
+
+def make_workload(args, dev, rank, world):
+    return StridedWorkload(args, dev, rank, world) if args.config == 2 else DescWorkload(
+        args, dev, rank, world)
+
+
+# ---------------------------------------------------------------------------
+def cpu_baseline(threads: int) -> dict:
     """Config 1 on the host cores: oracle/build/cpu_baseline (NepTUN framing over
     OpenSSL EVP, the stand-in for ring's asm; see oracle/cpu_baseline.c)."""
     exe = os.path.join(ROOT, "oracle", "build", "cpu_baseline")
@@ -71,7 +216,7 @@ def cpu_baseline(threads: int) -> dict | None:
     }
 
 
-def load_traffic(kernel: str) -> dict | None:
+def load_traffic(kernel: str, config: int) -> dict | None:
     """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -79,120 +224,87 @@ def load_traffic(kernel: str) -> dict | None:
     with open(path) as f:
         d = json.load(f)
     k = d.get("kernels", {}).get(kernel)
-    if not k:
+    if not k or d.get("config", 2) != config:
         return None
     return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
 
 
-def main():
-    args = parse()
-    import numpy as np
+def run(args, factory=None, device_fn=None):
+    """Bench body.  `factory`/`device_fn` are injection points for the CPU tests
+    of the multi-rank path (tests/test_bench_dist.py); production uses HIP."""
     import torch
     import torch.distributed as dist
-
-    import neptun_amd
-    from tools import synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if device_fn is None:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        stream = torch.cuda.current_stream(dev)
+        sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+        new_event = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    else:
+        dev, stream, sync, new_event = device_fn(local)
 
-    n, P = args.packets, args.size
-    S = args.stride or synth.round_up(P + 32, 128)
-    if S % 16 or S < P + 32:
-        raise SystemExit("--stride must be a multiple of 16 and hold P + 32 bytes")
-    ctx = neptun_amd.GpuContext(local, key_slots=1)
-    key = synth.keys(1)
-    ctx.set_keys(0, key, np.array([synth.RECEIVER_IDX], np.uint32))
-    # shard: rank r owns packets [r*n, (r+1)*n) of the global batch; counters follow
-    counter_base = rank * n
-    # NepTUN slot layout (WG_HEADER_OFFSET = 16, device/mod.rs:76): plaintext 16 bytes
-    # into each slot, the datagram at the slot start -- both 128-byte-run aligned
-    pt = synth.device_payloads(n, P, S, dev, seed=synth.SEED + rank, offset=16)
-    wire = torch.zeros(n * S, dtype=torch.uint8, device=dev)
-    back = torch.zeros(n * S, dtype=torch.uint8, device=dev)
-    st_seal = torch.full((n,), -1, dtype=torch.int32, device=dev)
-    st_open = torch.full((n,), -1, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-
-    def step(evs=None):
-        if evs is not None:
-            evs[0].record(stream)
-        ctx.seal_strided(n, P, 0, counter_base, pt.data_ptr() + 16, S, wire, S, st_seal, stream)
-        if evs is not None:
-            evs[1].record(stream)
-        ctx.open_strided(n, P + 32, 0, wire, S, back.data_ptr() + 16, S, st_open, stream)
-        if evs is not None:
-            evs[2].record(stream)
-
+    wl = (factory or make_workload)(args, dev, rank, world)
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
+        wl.step(stream)
+    sync()
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    events = [[new_event() for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize(dev)
+        wl.step(stream, events[k])
+    sync()
     elapsed = time.perf_counter() - t0
+    totals = torch.tensor([wl.payload_bytes, wl.packets], dtype=torch.float64)
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM)
 
     seal_ms = [e[0].elapsed_time(e[1]) for e in events]
     open_ms = [e[1].elapsed_time(e[2]) for e in events]
 
-    # correctness of what was timed: statuses + round-trip identity (full batch)
-    ok = int((st_seal != 0).sum()) == 0 and int((st_open != 0).sum()) == 0
-    ok = ok and torch.equal(back.view(n, S)[:, 16:16 + P], pt.view(n, S)[:, 16:16 + P])
+    # correctness of what was timed: statuses + round-trip identity (whole batch)
+    ok = bool(wl.verify())
     if world > 1:
         f = torch.tensor([0 if ok else 1], dtype=torch.int64)
         dist.all_reduce(f, op=dist.ReduceOp.MAX)
         ok = int(f.item()) == 0
+    line = None
     if not ok:
-        print(json.dumps({"error": "round-trip verification failed", "rank": rank}), flush=True)
-        sys.exit(1)
-
-    if rank == 0:
-        total_pkts = world * n * args.steps
-        gbps = total_pkts * P * 8 / elapsed / 1e9
-        ms_step = elapsed / args.steps * 1e3
-        avg_seal = sum(seal_ms) / len(seal_ms)
-        avg_open = sum(open_ms) / len(open_ms)
-        # algorithmic HBM bytes per launch: seal reads P, writes P+32; open reads P+32, writes P
-        launch_bytes = n * (2 * P + 32)
-        dom, dom_ms = ("seal", avg_seal) if avg_seal >= avg_open else ("open", avg_open)
-        achieved = launch_bytes / (dom_ms * 1e-3) / 1e9
-        kname = "aead_strided_kernel<true>" if dom == "seal" else "aead_strided_kernel<false>"
-        tr = load_traffic(kname)
+        line = {"error": "round-trip verification failed", "rank": rank}
+    elif rank == 0:
+        total_payload, total_pkts = float(totals[0]), float(totals[1])
+        gbps = total_payload * 8 * args.steps / elapsed / 1e9
+        avg = {"seal": sum(seal_ms) / len(seal_ms), "open": sum(open_ms) / len(open_ms)}
+        dom = "seal" if avg["seal"] >= avg["open"] else "open"
+        achieved = wl.launch_bytes[dom] / (avg[dom] * 1e-3) / 1e9
+        tr = load_traffic(wl.kernels[dom], args.config)
         line = {
-            "metric": METRIC,
+            "metric": METRIC if args.config == 2 else
+            f"Gbit/s device-resident ChaCha20-Poly1305 seal+open, BASELINE config {args.config}",
             "value": round(gbps, 2),
             "unit": "Gbit/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 4),
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (seeded IPv4/UDP-shaped payloads, one session key, counters = lane index)",
-            "config": {
-                "workload": f"BASELINE config {'2' if world == 1 else '5'}: {n} x {P} B packets per GPU, "
-                            "single session, seal then open, device-resident",
-                "packets_per_gpu": n, "packet_bytes": P, "slot_stride": S,
-                "global_packets": world * n, "parallelism": f"{world} shard(s), no collective",
-            },
+            "data": "synthetic (seeded payloads and keys; counters = lane index / per-peer rank)",
+            "config": wl.describe(world),
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
@@ -202,26 +314,33 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": tr["bytes_per_launch"] if tr else None,
                 "traffic_source": tr["source"] if tr else None,
-                "algorithmic_bytes_per_launch": launch_bytes,
+                "algorithmic_bytes_per_launch": wl.launch_bytes[dom],
             },
-            "kernel_ms": {"seal": round(avg_seal, 4), "open": round(avg_open, 4)},
-            "seal_gbps": round(n * P * 8 / (avg_seal * 1e-3) / 1e9, 1),
-            "open_gbps": round(n * P * 8 / (avg_open * 1e-3) / 1e9, 1),
-            "roundtrip_hbm_frac": round(n * (4 * P + 64) / ((avg_seal + avg_open) * 1e-3) / 1e9
-                                        / HBM_PEAK_GBS, 4),
+            "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+            "seal_gbps": round(wl.payload_bytes * 8 / (avg["seal"] * 1e-3) / 1e9, 1),
+            "open_gbps": round(wl.payload_bytes * 8 / (avg["open"] * 1e-3) / 1e9, 1),
+            "roundtrip_hbm_frac": round((wl.launch_bytes["seal"] + wl.launch_bytes["open"]) /
+                                        ((avg["seal"] + avg["open"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "packets_per_step": int(total_pkts),
             "verified": "all statuses Ok and open(seal(x)) == x over the whole batch",
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.config == 2:
             threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
             try:
                 line["cpu_baseline"] = cpu_baseline(threads)
             except Exception as e:  # reported, never fatal to the GPU number
                 line["cpu_baseline"] = {"error": str(e)[:200]}
+    if line is not None:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    ctx.close()
+    wl.close()
+    return 0 if ok else 1
+
+
+def main():
+    sys.exit(run(parse()))
 
 
 if __name__ == "__main__":

@@ -148,6 +148,26 @@ int wg_gpu_open_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
                       const uint8_t *src, uint8_t *dst, int32_t *status, void *stream);
 
 /*
+ * Mixed-length batches.  The kernels run one packet per wavefront lane, so a
+ * wave costs as much as its longest packet; wg_gpu_plan_batch writes a
+ * permutation `order` (n device uint32) grouping packets by length, longest
+ * first (a device counting sort; `scratch` = WG_PLAN_SCRATCH_BYTES of device
+ * memory, private to the call until it completes on `stream`).  The _ordered
+ * calls process descs[order[i]] and write status[order[i]] -- the results are
+ * identical to the unordered calls, only the scheduling differs.  `seal` != 0
+ * plans for a seal (datagram = len + 32), 0 for an open.
+ */
+#define WG_PLAN_SCRATCH_BYTES 262144u
+int wg_gpu_plan_batch(wg_gpu_ctx *ctx, int seal, const wg_packet_desc *descs, uint32_t n,
+                      uint32_t *order, uint32_t *scratch, void *stream);
+int wg_gpu_seal_batch_ordered(wg_gpu_ctx *ctx, const wg_packet_desc *descs,
+                              const uint32_t *order, uint32_t n, const uint8_t *src,
+                              uint8_t *dst, int32_t *status, void *stream);
+int wg_gpu_open_batch_ordered(wg_gpu_ctx *ctx, const wg_packet_desc *descs,
+                              const uint32_t *order, uint32_t n, const uint8_t *src,
+                              uint8_t *dst, int32_t *status, void *stream);
+
+/*
  * Uniform batch: n packets of one session, all `len` bytes, packet i at
  * src + i*src_stride / dst + i*dst_stride.  Seal uses counter
  * counter_base + i (one fetch_add(n) per batch instead of per packet,

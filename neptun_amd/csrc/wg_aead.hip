@@ -522,6 +522,7 @@ __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_desc_ke
   const uint32_t pkt0 = (blockIdx.x * kWaves + wave) * 64u;
   if (pkt0 >= prm.n) return;
   const uint32_t i = pkt0 + lane;
+  uint32_t idx = i;  // descriptor (and status) index this lane serves
   PacketJob job;
   job.status = -1;
   job.in_base = job.out_base = 0;
@@ -529,7 +530,8 @@ __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_desc_ke
   job.len = 0;
   job.slot = 0;
   if (i < prm.n) {
-    const wg_packet_desc d = prm.descs[i];
+    if (prm.order) idx = prm.order[i];
+    const wg_packet_desc d = prm.descs[idx];
     job.len = d.len;
     job.slot = d.key_slot;
     job.counter = d.counter;
@@ -543,7 +545,7 @@ __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_desc_ke
   }
   LdsGeom g{stage[wave]};
   run_wave<kSeal, false>(stage[wave], g, lane, job, prm.keys, prm.key_index,
-                         i < prm.n ? prm.status + i : nullptr);
+                         i < prm.n ? prm.status + idx : nullptr);
 }
 
 template __global__ void aead_strided_kernel<true, false>(StridedParams);

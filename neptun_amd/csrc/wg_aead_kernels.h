@@ -23,6 +23,7 @@ struct DescParams {
   const uint8_t *keys;
   const uint32_t *key_index;
   const wg_packet_desc *descs;
+  const uint32_t *order;  // optional permutation (wg_gpu_plan_batch); null = identity
   const uint8_t *src;
   uint8_t *dst;
   int32_t *status;
@@ -31,5 +32,15 @@ struct DescParams {
 
 template <bool kSeal, bool kTail> __global__ void aead_strided_kernel(StridedParams prm);
 template <bool kSeal> __global__ void aead_desc_kernel(DescParams prm);
+
+// wg_plan.hip: counting sort of a descriptor batch by rounds (longest first)
+constexpr uint32_t kPlanBins = 256;   // rounds 0..254, 255+ share the top bin
+constexpr uint32_t kPlanTiles = 256;  // contiguous descriptor tiles, one block each
+static_assert(kPlanBins * kPlanTiles * 4 == WG_PLAN_SCRATCH_BYTES, "scratch size");
+__global__ void plan_hist_kernel(const wg_packet_desc *descs, uint32_t n, uint32_t extra,
+                                 uint32_t *table);
+__global__ void plan_scan_kernel(uint32_t *table);
+__global__ void plan_scatter_kernel(const wg_packet_desc *descs, uint32_t n, uint32_t extra,
+                                    const uint32_t *table, uint32_t *order);
 
 }  // namespace wg

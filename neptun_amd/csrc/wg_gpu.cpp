@@ -7,6 +7,7 @@
 // fails with WG_RC_NO_DEVICE / WG_RC_HIP_ERROR.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -125,13 +126,15 @@ int wg_gpu_set_keys(wg_gpu_ctx *ctx, uint32_t first_slot, uint32_t n, const uint
   return WG_RC_OK;
 }
 
-static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, uint32_t n,
-                       const uint8_t *src, uint8_t *dst, int32_t *status, void *stream) {
+static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
+                       const uint32_t *order, uint32_t n, const uint8_t *src, uint8_t *dst,
+                       int32_t *status, void *stream) {
   if (!ctx || (n && (!descs || !src || !dst || !status)))
     return fail(WG_RC_INVALID_ARGUMENT, "batch: null argument");
   if (n == 0) return WG_RC_OK;
   DeviceGuard g(ctx->device);
-  wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, src, dst, status, n, ctx->key_slots};
+  wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, order, src, dst, status, n,
+                     ctx->key_slots};
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (seal)
     hipLaunchKernelGGL(wg::aead_desc_kernel<true>, dim3(grid_for(n)), dim3(wg::kBlockThreads), 0,
@@ -145,12 +148,43 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, 
 
 int wg_gpu_seal_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
                       const uint8_t *src, uint8_t *dst, int32_t *status, void *stream) {
-  return launch_desc(ctx, true, descs, n, src, dst, status, stream);
+  return launch_desc(ctx, true, descs, nullptr, n, src, dst, status, stream);
 }
 
 int wg_gpu_open_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
                       const uint8_t *src, uint8_t *dst, int32_t *status, void *stream) {
-  return launch_desc(ctx, false, descs, n, src, dst, status, stream);
+  return launch_desc(ctx, false, descs, nullptr, n, src, dst, status, stream);
+}
+
+int wg_gpu_seal_batch_ordered(wg_gpu_ctx *ctx, const wg_packet_desc *descs,
+                              const uint32_t *order, uint32_t n, const uint8_t *src,
+                              uint8_t *dst, int32_t *status, void *stream) {
+  if (n && !order) return fail(WG_RC_INVALID_ARGUMENT, "batch_ordered: null order");
+  return launch_desc(ctx, true, descs, order, n, src, dst, status, stream);
+}
+
+int wg_gpu_open_batch_ordered(wg_gpu_ctx *ctx, const wg_packet_desc *descs,
+                              const uint32_t *order, uint32_t n, const uint8_t *src,
+                              uint8_t *dst, int32_t *status, void *stream) {
+  if (n && !order) return fail(WG_RC_INVALID_ARGUMENT, "batch_ordered: null order");
+  return launch_desc(ctx, false, descs, order, n, src, dst, status, stream);
+}
+
+int wg_gpu_plan_batch(wg_gpu_ctx *ctx, int seal, const wg_packet_desc *descs, uint32_t n,
+                      uint32_t *order, uint32_t *scratch, void *stream) {
+  if (!ctx || (n && (!descs || !order || !scratch)))
+    return fail(WG_RC_INVALID_ARGUMENT, "plan_batch: null argument");
+  if (n == 0) return WG_RC_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t extra = seal ? WG_DATA_OVERHEAD_SZ : 0u;  // rounds follow the datagram size
+  hipLaunchKernelGGL(wg::plan_hist_kernel, dim3(wg::kPlanTiles), dim3(256), 0, s, descs, n, extra,
+                     scratch);
+  hipLaunchKernelGGL(wg::plan_scan_kernel, dim3(1), dim3(1024), 0, s, scratch);
+  hipLaunchKernelGGL(wg::plan_scatter_kernel, dim3(wg::kPlanTiles), dim3(256), 0, s, descs, n,
+                     extra, scratch, order);
+  WG_HIP(hipGetLastError(), "plan_batch: launch");
+  return WG_RC_OK;
 }
 
 static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, uint32_t key_slot,

@@ -102,6 +102,24 @@ class GpuContext:
         check(self._lib.wg_gpu_open_batch(self._h, _ptr(descs), n, _ptr(src), _ptr(dst),
                                           _ptr(status), _stream(stream)), "wg_gpu_open_batch")
 
+    # --- mixed-length scheduling -------------------------------------------
+    PLAN_SCRATCH_BYTES = 262144  # WG_PLAN_SCRATCH_BYTES
+
+    def plan_batch(self, seal: bool, descs, n: int, order, scratch, stream=None) -> None:
+        """Permutation grouping packets by length, longest first (device counting sort)."""
+        check(self._lib.wg_gpu_plan_batch(self._h, 1 if seal else 0, _ptr(descs), n, _ptr(order),
+                                          _ptr(scratch), _stream(stream)), "wg_gpu_plan_batch")
+
+    def seal_batch_ordered(self, descs, order, n: int, src, dst, status, stream=None) -> None:
+        check(self._lib.wg_gpu_seal_batch_ordered(self._h, _ptr(descs), _ptr(order), n, _ptr(src),
+                                                  _ptr(dst), _ptr(status), _stream(stream)),
+              "wg_gpu_seal_batch_ordered")
+
+    def open_batch_ordered(self, descs, order, n: int, src, dst, status, stream=None) -> None:
+        check(self._lib.wg_gpu_open_batch_ordered(self._h, _ptr(descs), _ptr(order), n, _ptr(src),
+                                                  _ptr(dst), _ptr(status), _stream(stream)),
+              "wg_gpu_open_batch_ordered")
+
     # --- uniform single-session batches -------------------------------------
     def seal_strided(self, n: int, length: int, key_slot: int, counter_base: int, src,
                      src_stride: int, dst, dst_stride: int, status=None, stream=None) -> None:

@@ -1,0 +1,113 @@
+"""bench.py's multi-rank path (one process per GPU, gloo control plane) on CPU.
+
+The data path has no collective (packets shard independently);
+what must hold across ranks is the timing contract: barrier + sync around the
+timed steps, MAX of the elapsed time over ranks, SUM of the payload, and a
+failed verification on any rank failing the run.  The GPU workload is replaced
+by a CPU stand-in with the same interface; everything else is bench.run.
+"""
+import json
+import os
+import socket
+import time
+
+import pytest
+import torch.multiprocessing as mp
+
+
+class CpuEvent:
+    def __init__(self):
+        self.t = None
+
+    def record(self, stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+def cpu_device(local):
+    return "cpu", None, (lambda: None), CpuEvent
+
+
+class FakeWorkload:
+    """Same interface as bench.StridedWorkload; rank r sleeps (r+1) ms per step."""
+
+    def __init__(self, args, dev, rank, world):
+        self.rank = rank
+        self.packets = 1000 * (rank + 1)
+        self.payload_bytes = 1350 * self.packets
+        self.launch_bytes = {"seal": 2732 * self.packets, "open": 2732 * self.packets}
+        self.kernels = {"seal": "fake_seal", "open": "fake_open"}
+        self.fail = os.environ.get("FAKE_FAIL_RANK") == str(rank)
+
+    def step(self, stream, evs=None):
+        if evs:
+            evs[0].record()
+        time.sleep(0.001 * (self.rank + 1))
+        if evs:
+            evs[1].record()
+        time.sleep(0.0005)
+        if evs:
+            evs[2].record()
+
+    def verify(self):
+        return not self.fail
+
+    def describe(self, world):
+        return {"workload": "fake", "parallelism": f"{world} shard(s), no collective"}
+
+    def close(self):
+        pass
+
+
+def _worker(rank, world, port, outdir, fail_rank):
+    import contextlib
+    import io
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if fail_rank is not None:
+        os.environ["FAKE_FAIL_RANK"] = str(fail_rank)
+    import bench
+    args = bench.parse(["--steps", "5", "--warmup", "1", "--no-cpu-baseline"])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = bench.run(args, factory=FakeWorkload, device_fn=cpu_device)
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump({"rc": rc, "out": buf.getvalue()}, f)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_ranks(tmp_path, world, fail_rank=None):
+    mp.start_processes(_worker, args=(world, free_port(), str(tmp_path), fail_rank), nprocs=world,
+                       join=True, start_method="spawn")
+    return [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_two_ranks_aggregate_max_time_and_sum_payload(tmp_path, world):
+    res = run_ranks(tmp_path, world)
+    assert all(r["rc"] == 0 for r in res)
+    assert res[1]["out"] == ""  # only rank 0 prints
+    line = json.loads(res[0]["out"])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["packets_per_step"] == 1000 + 2000
+    # the slowest rank (rank 1: >= 2.5 ms per step) sets the time
+    assert line["ms_per_step"] >= 2.5
+    total_payload = 1350 * 3000
+    want = total_payload * 8 / (line["ms_per_step"] * 1e-3) / 1e9
+    assert abs(line["value"] - want) / want < 1e-3
+    assert line["config"]["parallelism"] == "2 shard(s), no collective"
+
+
+def test_failed_verification_on_any_rank_fails_the_run(tmp_path):
+    res = run_ranks(tmp_path, 2, fail_rank=1)
+    assert all(r["rc"] == 1 for r in res)
+    assert "error" in json.loads(res[0]["out"])

@@ -279,3 +279,100 @@ def test_config2_full_size_round_trip(torch_cuda, gpu):
     for r, w, p in zip(rows, wire_rows, pt_rows):
         want = o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, int(r), p[:P].tobytes())
         assert w[:P + 32].tobytes() == want
+
+
+# ---------------------------------------------------------------------------
+# mixed-length scheduling (BASELINE config 3) and per-peer keys (config 4)
+# ---------------------------------------------------------------------------
+def rounds_of(lens):
+    return (lens.astype(np.int64) + 127) // 128
+
+
+def test_plan_batch_is_a_length_sorted_permutation(torch_cuda, gpu):
+    torch = torch_cuda
+    from tools import workloads
+    b = workloads.config3(1000, "cuda", seed=11)
+    gpu.plan_batch(True, b.d_seal, b.n, b.order, b.scratch)
+    torch.cuda.synchronize()
+    order = b.order.cpu().numpy().astype(np.int64)
+    assert np.array_equal(np.sort(order), np.arange(b.n))
+    r = rounds_of(b.sizes[order] + 32)
+    assert (np.diff(r) <= 0).all(), "longest packets first"
+    # inside a bin the permutation keeps index order: deterministic
+    for rr in np.unique(r):
+        assert (np.diff(order[r == rr]) > 0).all()
+    b.order.zero_()
+    gpu.plan_batch(True, b.d_seal, b.n, b.order, b.scratch)
+    torch.cuda.synchronize()
+    assert np.array_equal(b.order.cpu().numpy().astype(np.int64), order)
+
+
+@pytest.mark.parametrize("ordered", [True, False])
+def test_mixed_mtu_batch_matches_oracle(torch_cuda, gpu, ordered):
+    torch = torch_cuda
+    from tools import workloads
+    b = workloads.config3(2000, "cuda", seed=12)
+    keys = synth.keys(1, seed=77)
+    kidx = np.array([0xBEEF], np.uint32)
+    gpu.set_keys(0, keys, kidx)
+    if ordered:
+        gpu.plan_batch(True, b.d_seal, b.n, b.order, b.scratch)
+        gpu.seal_batch_ordered(b.d_seal, b.order, b.n, b.pt, b.wire, b.st_seal)
+        gpu.open_batch_ordered(b.d_open, b.order, b.n, b.wire, b.out, b.st_open)
+    else:
+        gpu.seal_batch(b.d_seal, b.n, b.pt, b.wire, b.st_seal)
+        gpu.open_batch(b.d_open, b.n, b.wire, b.out, b.st_open)
+    torch.cuda.synchronize()
+    assert int((b.st_seal != 0).sum()) == 0 and int((b.st_open != 0).sum()) == 0
+    src = b.pt.cpu().numpy()
+    want = np.zeros_like(src)
+    assert (o.seal_batch(b.seal_host, keys, kidx, src, want) == 0).all()
+    assert np.array_equal(b.wire.cpu().numpy(), want)
+    assert b.round_trip_equal()
+
+
+def test_per_peer_keys_match_oracle(torch_cuda, gpu):
+    """Config 4 shape at reduced size: 512 peers x 32 packets, keys looked up per lane."""
+    torch = torch_cuda
+    from tools import workloads
+    peers, per = 512, 32
+    b = workloads.config4(peers, per, 1350, "cuda", seed=13)
+    keys = synth.keys(peers, seed=99)
+    kidx = (np.arange(peers, dtype=np.uint32) * 2654435761).astype(np.uint32)
+    gpu.set_keys(0, keys, kidx)
+    gpu.seal_batch(b.d_seal, b.n, b.pt, b.wire, b.st_seal)
+    gpu.open_batch(b.d_open, b.n, b.wire, b.out, b.st_open)
+    torch.cuda.synchronize()
+    assert int((b.st_seal != 0).sum()) == 0 and int((b.st_open != 0).sum()) == 0
+    src = b.pt.cpu().numpy()
+    want = np.zeros_like(src)
+    assert (o.seal_batch(b.seal_host, keys, kidx, src, want) == 0).all()
+    assert np.array_equal(b.wire.cpu().numpy(), want)
+    # per-peer counters 0..per-1 made it into the headers
+    w = b.wire.cpu().numpy()
+    ctr = np.array([int.from_bytes(w[x + 8:x + 16].tobytes(), "little") for x in b.offs])
+    peer = b.seal_host["key_slot"]
+    for pr in range(0, peers, 97):
+        assert sorted(ctr[peer == pr]) == list(range(per))
+    assert b.round_trip_equal()
+
+
+def test_config3_full_size_round_trip(torch_cuda, gpu):
+    """BASELINE config 3 at full size (1.31M packets): statuses, round trip, sampled oracle."""
+    torch = torch_cuda
+    from tools import workloads
+    b = workloads.config3(1 << 18, "cuda")
+    keys = synth.keys(1)
+    kidx = np.array([synth.RECEIVER_IDX], np.uint32)
+    gpu.set_keys(0, keys, kidx)
+    gpu.plan_batch(True, b.d_seal, b.n, b.order, b.scratch)
+    gpu.seal_batch_ordered(b.d_seal, b.order, b.n, b.pt, b.wire, b.st_seal)
+    gpu.open_batch_ordered(b.d_open, b.order, b.n, b.wire, b.out, b.st_open)
+    torch.cuda.synchronize()
+    assert int((b.st_seal != 0).sum()) == 0 and int((b.st_open != 0).sum()) == 0
+    assert b.round_trip_equal()
+    for i in range(0, b.n, 4099):
+        off, p = int(b.offs[i]), int(b.sizes[i])
+        pt = b.pt[off + 16:off + 16 + p].cpu().numpy().tobytes()
+        got = b.wire[off:off + p + 32].cpu().numpy().tobytes()
+        assert got == o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, i, pt)
