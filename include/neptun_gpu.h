@@ -16,7 +16,7 @@
  *         16-byte tag right after it; wire length = len + 32.
  *   open: Tunn::parse_incoming_packet (DATA arm, noise/mod.rs:139-199) +
  *         Session::receive_packet_data session.rs:265-302 without the replay
- *         window (host-side, wg_replay_* below): header checked (type 4,
+ *         window (host-side, wg_replay_* in neptun_tunn.h): header checked (type 4,
  *         len >= 32, receiver_idx == the slot's receiving index), tag verified
  *         (ring open_in_place), plaintext written.  On a tag mismatch the
  *         plaintext bytes are zeroed (ring 0.17 open_within) and the status is
@@ -181,6 +181,29 @@ int wg_gpu_seal_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
 int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_slot,
                         const uint8_t *src, uint64_t src_stride, uint8_t *dst,
                         uint64_t dst_stride, int32_t *status, void *stream);
+
+/*
+ * Host-resident batches (the real data path: TUN read buffers in, UDP send
+ * buffers out and vice versa).  A pipe owns `depth` streams and device staging
+ * buffers of `chunk_bytes` each; a call splits the batch into chunks and runs
+ * H2D copy -> kernel -> D2H copy per chunk, chunks round-robin over the
+ * streams so copies in both directions overlap the kernels.  Host buffers
+ * should be pinned (hipHostMalloc / cudaHostRegister-equivalent) for the copies
+ * to overlap.  Only the packet bytes are copied back (2-D copies of `len` or
+ * `len + 32` bytes at `dst_stride`); the calls return when every chunk is done.
+ * Semantics are those of wg_gpu_seal_strided / wg_gpu_open_strided; packet i is
+ * at h_src + i*src_stride / h_dst + i*dst_stride, status (may be NULL) in host
+ * memory.  A pipe is not thread-safe: one pipe per calling thread.
+ */
+typedef struct wg_gpu_pipe wg_gpu_pipe;
+int wg_gpu_pipe_create(wg_gpu_ctx *ctx, uint64_t chunk_bytes, uint32_t depth, wg_gpu_pipe **out);
+int wg_gpu_pipe_destroy(wg_gpu_pipe *pipe);
+int wg_gpu_pipe_seal_strided(wg_gpu_pipe *pipe, uint32_t n, uint32_t len, uint32_t key_slot,
+                             uint64_t counter_base, const uint8_t *h_src, uint64_t src_stride,
+                             uint8_t *h_dst, uint64_t dst_stride, int32_t *h_status);
+int wg_gpu_pipe_open_strided(wg_gpu_pipe *pipe, uint32_t n, uint32_t len, uint32_t key_slot,
+                             const uint8_t *h_src, uint64_t src_stride, uint8_t *h_dst,
+                             uint64_t dst_stride, int32_t *h_status);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,110 @@
+/*
+ * neptun_tunn.h -- batched Tunn data plane over the GPU AEAD (C ABI).
+ *
+ * Mirrors the data-packet part of neptun::noise::Tunn so that one batch call
+ * returns exactly what N sequential Tunn::encapsulate / Tunn::decapsulate
+ * calls would (/root/reference/neptun/src/noise/mod.rs:295-380, 545-569,
+ * 606-670; session.rs:40-302):
+ *   encapsulate: sessions[current % 8] (mod.rs:310), dst capacity check
+ *     (session.rs:210-217: IncorrectPacketLength, no counter consumed), one
+ *     sending-counter reservation per batch (session.rs:219 fetch_add),
+ *     tx_bytes += P + 32 (mod.rs:321) -> WriteToNetwork(P + 32).
+ *   decapsulate: parse_incoming_packet (mod.rs:139-199), session
+ *     sessions[receiver_idx % 8] (mod.rs:550-556, NoCurrentSession),
+ *     receive_packet_data checks in the reference order -- dst capacity
+ *     (DestinationBufferTooSmall), receiver index (WrongIndex), replay quick
+ *     check (InvalidCounter / DuplicateCounter), tag (InvalidAeadTag), replay
+ *     mark -- then validate_decapsulated_packet (mod.rs:606-670: keepalive ->
+ *     Done, IPv4/IPv6 length truncation, InvalidPacket) and rx_bytes.
+ * Handshake / cookie messages are not the data path: such datagrams come back
+ * as WG_TUNN_NOT_DATA for the caller's CPU Tunn.  Timers (timers.rs) are not
+ * mirrored; set_current_session follows the reference minus its timer test.
+ *
+ * The replay window (session.rs:40-157) is exposed on its own (wg_replay_*)
+ * for tests and for embedders that keep their own sessions.
+ */
+#ifndef NEPTUN_TUNN_H
+#define NEPTUN_TUNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "neptun_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WG_N_SESSIONS 8          /* noise/mod.rs:47 */
+#define WG_REPLAY_WORDS 16       /* session.rs:37 N_WORDS (1024-bit window) */
+
+/* ReceivingKeyCounterValidator (session.rs:40-48) */
+typedef struct wg_replay {
+  uint64_t next;
+  uint64_t receive_cnt;
+  uint64_t bitmap[WG_REPLAY_WORDS];
+} wg_replay;
+
+void wg_replay_init(wg_replay *w);
+/* will_accept (session.rs:90-104): 0, WG_STATUS_INVALID_COUNTER or WG_STATUS_DUPLICATE_COUNTER */
+int wg_replay_will_accept(const wg_replay *w, uint64_t counter);
+/* mark_did_receive (session.rs:109-156): 0 or WG_STATUS_INVALID_COUNTER; does not touch receive_cnt */
+int wg_replay_mark_did_receive(wg_replay *w, uint64_t counter);
+
+enum wg_tunn_kind {
+  WG_TUNN_DONE = 0,              /* TunnResult::Done (keepalive) */
+  WG_TUNN_ERR = 1,               /* TunnResult::Err(status) */
+  WG_TUNN_WRITE_TO_NETWORK = 2,  /* datagram of `len` bytes at dst */
+  WG_TUNN_WRITE_TO_TUNNEL = 3,   /* IP packet of `len` bytes at dst, source address src_ip */
+  WG_TUNN_NOT_DATA = 4,          /* handshake / cookie message: hand it to the CPU Tunn */
+};
+
+typedef struct wg_tunn_result {
+  int32_t kind;        /* wg_tunn_kind */
+  int32_t status;      /* wg_status when kind == WG_TUNN_ERR, else 0 */
+  uint32_t len;
+  uint8_t ip_version;  /* 4 or 6 for WG_TUNN_WRITE_TO_TUNNEL */
+  uint8_t src_ip[16];  /* IPv4 in the first 4 bytes */
+  uint8_t pad[3];
+} wg_tunn_result;
+
+typedef struct wg_tunn wg_tunn;
+
+/* A Tunn bound to a GPU context; it uses key slots [first_slot, first_slot + 16). */
+int wg_tunn_create(wg_gpu_ctx *ctx, uint32_t first_slot, wg_tunn **out);
+int wg_tunn_destroy(wg_tunn *t);
+
+/* Session::new(local_index, peer_index, receiving_key, sending_key) stored at
+ * sessions[local_index % 8] (mod.rs:449-452, 477-481); make_current != 0 makes
+ * it the sending session (set_current_session, mod.rs:521-532). */
+int wg_tunn_install_session(wg_tunn *t, uint32_t local_index, uint32_t peer_index,
+                            const uint8_t receiving_key[32], const uint8_t sending_key[32],
+                            int make_current);
+int wg_tunn_stats(const wg_tunn *t, uint64_t *tx_bytes, uint64_t *rx_bytes);
+/* sending counter of the current session / replay state of a ring slot (for tests) */
+int wg_tunn_session_counters(const wg_tunn *t, uint32_t ring_slot, uint64_t *sending_counter,
+                             wg_replay *window);
+
+/* n x Tunn::encapsulate(src[i][..src_len[i]], dst[i][..dst_cap[i]]) with host buffers */
+int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
+                              const uint32_t *src_len, uint8_t *const *dst,
+                              const uint32_t *dst_cap, wg_tunn_result *res);
+/* n x Tunn::decapsulate(None, datagram[i][..len[i]], dst[i][..dst_cap[i]]) */
+int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
+                              const uint32_t *len, uint8_t *const *dst, const uint32_t *dst_cap,
+                              wg_tunn_result *res);
+/* n x Tunn::decrypt(datagram[i], dst[i]) (feature "xray", mod.rs:383-417 ->
+ * Session::decrypt_data_packet session.rs:316-353): the first session whose
+ * receiving OR sending index equals the header's receiver_idx, opened with the
+ * matching direction's key, no replay window, no set_current_session; then
+ * validate_decapsulated_packet (rx_bytes as the reference).  Ok(p) comes back
+ * as WG_TUNN_WRITE_TO_TUNNEL; a keepalive is ERR UnexpectedPacket and a
+ * handshake / cookie message ERR WrongPacketType, like the reference. */
+int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
+                          const uint32_t *len, uint8_t *const *dst, const uint32_t *dst_cap,
+                          wg_tunn_result *res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEPTUN_TUNN_H */

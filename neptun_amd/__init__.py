@@ -4,8 +4,8 @@ The product is ``libneptun_gpu.so`` (C ABI: include/neptun_gpu.h) built from
 ``neptun_amd/csrc``; this package is its Python face (ctypes) plus the batched
 host-side Tunn semantics.  See DESIGN.md.
 """
-from ._native import NeptunGpuError, LIB_PATH, header_functions, load
-from .gpu import DESC_DTYPE, STATUS, GpuContext
+from ._native import NeptunGpuError, HEADER_PATH, LIB_PATH, header_functions, load
+from .gpu import DESC_DTYPE, STATUS, GpuContext, GpuPipe
 
-__all__ = ["NeptunGpuError", "LIB_PATH", "header_functions", "load", "DESC_DTYPE", "STATUS",
-           "GpuContext"]
+__all__ = ["NeptunGpuError", "HEADER_PATH", "LIB_PATH", "header_functions", "load", "DESC_DTYPE", "STATUS",
+           "GpuContext", "GpuPipe"]

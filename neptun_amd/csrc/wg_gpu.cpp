@@ -62,6 +62,10 @@ struct DeviceGuard {
 
 }  // namespace
 
+// shared with wg_pipe.cpp
+int wg_pipe_fail(int rc, const char *what, hipError_t e) { return fail(rc, what, e); }
+int wg_ctx_device(const wg_gpu_ctx *ctx) { return ctx->device; }
+
 extern "C" {
 
 int wg_gpu_abi_version(void) { return WG_GPU_ABI_VERSION; }

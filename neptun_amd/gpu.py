@@ -134,5 +134,44 @@ class GpuContext:
               "wg_gpu_open_strided")
 
 
-__all__ = ["GpuContext", "NeptunGpuError", "DESC_DTYPE", "STATUS", "DATA_OFFSET", "AEAD_SIZE",
+class GpuPipe:
+    """Host-resident batches: chunked H2D -> kernel -> D2H over `depth` streams.
+
+    The end-to-end shape of NepTUN's data path (TUN/UDP buffers live in host
+    memory); pass pinned host tensors for overlapped copies.
+    """
+
+    def __init__(self, ctx: GpuContext, chunk_bytes: int = 64 << 20, depth: int = 3):
+        self._lib = ctx._lib
+        self._ctx = ctx  # keep the context alive
+        h = ctypes.c_void_p()
+        check(self._lib.wg_gpu_pipe_create(ctx._h, chunk_bytes, depth, ctypes.byref(h)),
+              "wg_gpu_pipe_create")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.wg_gpu_pipe_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def seal_strided(self, n, length, key_slot, counter_base, h_src, src_stride, h_dst,
+                     dst_stride, h_status=None) -> None:
+        check(self._lib.wg_gpu_pipe_seal_strided(self._h, n, length, key_slot, counter_base,
+                                                 _ptr(h_src), src_stride, _ptr(h_dst), dst_stride,
+                                                 _ptr(h_status)), "wg_gpu_pipe_seal_strided")
+
+    def open_strided(self, n, length, key_slot, h_src, src_stride, h_dst, dst_stride,
+                     h_status=None) -> None:
+        check(self._lib.wg_gpu_pipe_open_strided(self._h, n, length, key_slot, _ptr(h_src),
+                                                 src_stride, _ptr(h_dst), dst_stride,
+                                                 _ptr(h_status)), "wg_gpu_pipe_open_strided")
+
+
+__all__ = ["GpuPipe", "GpuContext", "NeptunGpuError", "DESC_DTYPE", "STATUS", "DATA_OFFSET", "AEAD_SIZE",
            "DATA_OVERHEAD_SZ"]

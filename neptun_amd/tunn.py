@@ -1,0 +1,132 @@
+"""Batched Tunn data plane (include/neptun_tunn.h) -- Python face.
+
+`Tunn.encapsulate_batch` / `decapsulate_batch` return what N sequential calls
+of neptun's Tunn::encapsulate / Tunn::decapsulate return
+(/root/reference/neptun/src/noise/mod.rs:295-380), with the AEAD of the whole
+batch on the GPU.  Results mirror TunnResult: (kind, status, len, ip_version,
+src_ip); kinds DONE / ERR / WRITE_TO_NETWORK / WRITE_TO_TUNNEL, plus NOT_DATA
+for handshake/cookie messages the CPU Tunn must handle.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._native import check, load
+from .gpu import GpuContext
+
+DONE, ERR, WRITE_TO_NETWORK, WRITE_TO_TUNNEL, NOT_DATA = 0, 1, 2, 3, 4
+N_SESSIONS = 8
+
+
+class Replay(ctypes.Structure):
+    """wg_replay: ReceivingKeyCounterValidator (session.rs:40-48)."""
+    _fields_ = [("next", ctypes.c_uint64), ("receive_cnt", ctypes.c_uint64),
+                ("bitmap", ctypes.c_uint64 * 16)]
+
+
+class TunnResult(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("status", ctypes.c_int32), ("len", ctypes.c_uint32),
+                ("ip_version", ctypes.c_uint8), ("src_ip", ctypes.c_uint8 * 16),
+                ("pad", ctypes.c_uint8 * 3)]
+
+
+def _bind(L):
+    if getattr(L, "_tunn_bound", False):
+        return L
+    c = ctypes
+    vp, u32, u64 = c.c_void_p, c.c_uint32, c.c_uint64
+    L.wg_replay_init.argtypes = [c.POINTER(Replay)]
+    L.wg_replay_init.restype = None
+    L.wg_replay_will_accept.argtypes = [c.POINTER(Replay), u64]
+    L.wg_replay_mark_did_receive.argtypes = [c.POINTER(Replay), u64]
+    L.wg_tunn_create.argtypes = [vp, u32, c.POINTER(vp)]
+    L.wg_tunn_destroy.argtypes = [vp]
+    L.wg_tunn_install_session.argtypes = [vp, u32, u32, c.c_char_p, c.c_char_p, c.c_int]
+    L.wg_tunn_stats.argtypes = [vp, c.POINTER(u64), c.POINTER(u64)]
+    L.wg_tunn_session_counters.argtypes = [vp, u32, c.POINTER(u64), c.POINTER(Replay)]
+    for fn in (L.wg_tunn_encapsulate_batch, L.wg_tunn_decapsulate_batch, L.wg_tunn_decrypt_batch):
+        fn.argtypes = [vp, u32, vp, vp, vp, vp, c.POINTER(TunnResult)]
+    L._tunn_bound = True
+    return L
+
+
+class ReplayWindow:
+    """The C++ replay window on its own (no GPU needed)."""
+
+    def __init__(self):
+        self._lib = _bind(load())
+        self.w = Replay()
+        self._lib.wg_replay_init(ctypes.byref(self.w))
+
+    def will_accept(self, counter: int) -> int:
+        return self._lib.wg_replay_will_accept(ctypes.byref(self.w), counter)
+
+    def mark_did_receive(self, counter: int) -> int:
+        return self._lib.wg_replay_mark_did_receive(ctypes.byref(self.w), counter)
+
+
+class Tunn:
+    """Tunn mirror bound to a GpuContext; uses 16 key slots from `first_slot`."""
+
+    def __init__(self, ctx: GpuContext, first_slot: int = 0):
+        self._lib = _bind(ctx._lib)
+        self._ctx = ctx
+        h = ctypes.c_void_p()
+        check(self._lib.wg_tunn_create(ctx._h, first_slot, ctypes.byref(h)), "wg_tunn_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.wg_tunn_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def install_session(self, local_index, peer_index, recv_key: bytes, send_key: bytes,
+                        make_current: bool = True):
+        check(self._lib.wg_tunn_install_session(self._h, local_index, peer_index, recv_key,
+                                                send_key, 1 if make_current else 0),
+              "wg_tunn_install_session")
+
+    def stats(self):
+        tx, rx = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self._lib.wg_tunn_stats(self._h, ctypes.byref(tx), ctypes.byref(rx)), "wg_tunn_stats")
+        return tx.value, rx.value
+
+    def session_counters(self, ring_slot):
+        c, w = ctypes.c_uint64(), Replay()
+        check(self._lib.wg_tunn_session_counters(self._h, ring_slot, ctypes.byref(c),
+                                                 ctypes.byref(w)), "wg_tunn_session_counters")
+        return c.value, w
+
+    def _batch(self, fn, name, srcs, dsts):
+        n = len(srcs)
+        keep = [ctypes.create_string_buffer(bytes(s), max(len(s), 1)) for s in srcs]
+        src_ptr = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in keep])
+        src_len = (ctypes.c_uint32 * n)(*[len(s) for s in srcs])
+        dbufs = [(ctypes.c_uint8 * max(len(d), 1)).from_buffer(d) if len(d) else
+                 (ctypes.c_uint8 * 1)() for d in dsts]
+        dst_ptr = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in dbufs])
+        dst_cap = (ctypes.c_uint32 * n)(*[len(d) for d in dsts])
+        res = (TunnResult * n)()
+        check(fn(self._h, n, src_ptr, src_len, dst_ptr, dst_cap, res), name)
+        return [(r.kind, r.status, r.len, r.ip_version, bytes(r.src_ip)) for r in res]
+
+    def encapsulate_batch(self, srcs: list[bytes], dsts: list[bytearray]):
+        return self._batch(self._lib.wg_tunn_encapsulate_batch, "wg_tunn_encapsulate_batch",
+                           srcs, dsts)
+
+    def decapsulate_batch(self, datagrams: list[bytes], dsts: list[bytearray]):
+        return self._batch(self._lib.wg_tunn_decapsulate_batch, "wg_tunn_decapsulate_batch",
+                           datagrams, dsts)
+
+    def decrypt_batch(self, datagrams: list[bytes], dsts: list[bytearray]):
+        """xray Tunn::decrypt per datagram (no replay window)."""
+        return self._batch(self._lib.wg_tunn_decrypt_batch, "wg_tunn_decrypt_batch",
+                           datagrams, dsts)

@@ -1,0 +1,228 @@
+"""Sequential model of NepTUN's Tunn data plane -- TEST INFRASTRUCTURE ONLY.
+
+A plain-Python restatement, one packet at a time, of
+  ReceivingKeyCounterValidator   neptun/src/noise/session.rs:40-157
+  Session::format_packet_data    session.rs:205-259  (AEAD via oracle C lib)
+  Session::receive_packet_data   session.rs:265-302
+  Tunn::encapsulate(_in_place)   neptun/src/noise/mod.rs:295-338
+  Tunn::decapsulate -> parse_incoming_packet -> handle_data -> validate_decapsulated_packet
+                                 mod.rs:139-199, 346-380, 545-569, 606-670
+  set_current_session            mod.rs:521-532 (session timer compare -> install order)
+  Tunn::decrypt (xray)           mod.rs:383-417, session.rs:311-353
+used as the checker of the batched C++ mirror (neptun_amd/csrc/wg_tunn.cpp).
+Results use the same codes as include/neptun_tunn.h.
+"""
+from __future__ import annotations
+
+from oracle import pyoracle as o
+
+WORD, N_WORDS = 64, 16
+N_BITS = WORD * N_WORDS
+N_SESSIONS = 8
+
+DONE, ERR, WRITE_TO_NETWORK, WRITE_TO_TUNNEL, NOT_DATA = 0, 1, 2, 3, 4
+INVALID_LENGTH, INCORRECT_PACKET_LENGTH, DEST_TOO_SMALL = 19, 2, 1
+WRONG_INDEX, INVALID_AEAD_TAG, INVALID_COUNTER, DUPLICATE_COUNTER = 5, 10, 11, 12
+INVALID_PACKET, NO_CURRENT_SESSION = 13, 14
+UNEXPECTED_PACKET, WRONG_PACKET_TYPE = 3, 4
+
+
+class Replay:
+    """session.rs:40-157, line by line."""
+
+    def __init__(self):
+        self.next = 0
+        self.receive_cnt = 0
+        self.bitmap = [0] * N_WORDS
+
+    def _loc(self, idx):
+        b = idx % N_BITS
+        return b // WORD, b % WORD
+
+    def set_bit(self, idx):
+        w, b = self._loc(idx)
+        self.bitmap[w] |= 1 << b
+
+    def clear_bit(self, idx):
+        w, b = self._loc(idx)
+        self.bitmap[w] &= ~(1 << b) & ((1 << 64) - 1)
+
+    def clear_word(self, idx):
+        self.bitmap[self._loc(idx)[0]] = 0
+
+    def check_bit(self, idx):
+        w, b = self._loc(idx)
+        return (self.bitmap[w] >> b) & 1 == 1
+
+    def will_accept(self, counter):
+        if counter >= self.next:
+            return 0
+        if counter + N_BITS < self.next:
+            return INVALID_COUNTER
+        return DUPLICATE_COUNTER if self.check_bit(counter) else 0
+
+    def mark_did_receive(self, counter):
+        if counter + N_BITS < self.next:
+            return INVALID_COUNTER
+        if counter == self.next:
+            self.set_bit(counter)
+            self.next += 1
+            return 0
+        if counter < self.next:
+            if self.check_bit(counter):
+                return INVALID_COUNTER
+            self.set_bit(counter)
+            return 0
+        if counter - self.next >= N_BITS:
+            self.bitmap = [0] * N_WORDS
+        else:
+            i = self.next
+            while i % WORD != 0 and i < counter:
+                self.clear_bit(i)
+                i += 1
+            while i + WORD < counter:
+                self.clear_word(i)
+                i = (i + WORD) & ((1 << 64) - WORD)
+            while i < counter:
+                self.clear_bit(i)
+                i += 1
+        self.set_bit(counter)
+        self.next = counter + 1
+        return 0
+
+
+class Session:
+    def __init__(self, local_index, peer_index, recv_key, send_key, established):
+        self.receiving_index = local_index
+        self.sending_index = peer_index
+        self.recv_key, self.send_key = recv_key, send_key
+        self.sending_counter = 0
+        self.window = Replay()
+        self.established = established
+
+
+class Tunn:
+    def __init__(self):
+        self.sessions = [None] * N_SESSIONS
+        self.current = 0
+        self.tx_bytes = 0
+        self.rx_bytes = 0
+        self._seq = 0
+
+    def install_session(self, local_index, peer_index, recv_key, send_key, make_current):
+        self._seq += 1
+        self.sessions[local_index % N_SESSIONS] = Session(local_index, peer_index, recv_key,
+                                                          send_key, self._seq)
+        if make_current:
+            self.set_current_session(local_index)
+
+    def set_current_session(self, new_idx):
+        cur = self.current
+        if cur == new_idx:
+            return
+        c, n = self.sessions[cur % N_SESSIONS], self.sessions[new_idx % N_SESSIONS]
+        if c is None or n.established >= c.established:
+            self.current = new_idx
+
+    def encapsulate(self, src: bytes, dst: bytearray):
+        """-> (kind, status, len); writes dst like the reference."""
+        if len(dst) < len(src) + 16:
+            return ERR, INVALID_LENGTH, 0
+        dst[16:16 + len(src)] = src  # mod.rs:296-299 copies before looking at the session
+        s = self.sessions[self.current % N_SESSIONS]
+        if s is None:
+            return NOT_DATA, NO_CURRENT_SESSION, 0
+        if len(dst) < len(src) + 32:
+            return ERR, INCORRECT_PACKET_LENGTH, 0
+        ctr = s.sending_counter
+        s.sending_counter += 1
+        wire = o.format_packet_data(s.send_key, s.sending_index, ctr, src)
+        dst[:len(wire)] = wire
+        self.tx_bytes += len(wire)
+        return WRITE_TO_NETWORK, 0, len(wire)
+
+    def decapsulate(self, d: bytes, dst: bytearray):
+        """-> (kind, status, len, ip_version, src_ip bytes)."""
+        L = len(d)
+        if L == 0:
+            return NOT_DATA, 0, 0, 0, b""
+        if L < 4:
+            return ERR, INVALID_PACKET, 0, 0, b""
+        typ = int.from_bytes(d[:4], "little")
+        if (typ, L) in ((1, 148), (2, 92), (3, 64)):
+            return NOT_DATA, 0, 0, 0, b""
+        if typ != 4 or L < 32:
+            return ERR, INVALID_PACKET, 0, 0, b""
+        ridx = int.from_bytes(d[4:8], "little")
+        ctr = int.from_bytes(d[8:16], "little")
+        s = self.sessions[ridx % N_SESSIONS]
+        if s is None:
+            return ERR, NO_CURRENT_SESSION, 0, 0, b""
+        ct_len = L - 16
+        if len(dst) < ct_len:
+            return ERR, DEST_TOO_SMALL, 0, 0, b""
+        if ridx != s.receiving_index:
+            return ERR, WRONG_INDEX, 0, 0, b""
+        e = s.window.will_accept(ctr)
+        if e:
+            return ERR, e, 0, 0, b""
+        P = L - 32
+        st, pt = o.receive_packet_data(s.recv_key, s.receiving_index, bytes(d))
+        # session.rs:287-296: ct||tag copied into dst, opened in place; ring zeroes
+        # the plaintext on a tag mismatch, the tag bytes stay behind it
+        dst[:P] = pt if st == 0 else bytes(P)
+        dst[P:P + 16] = d[16 + P:32 + P]
+        if st:
+            return ERR, st, 0, 0, b""
+        e = s.window.mark_did_receive(ctr)
+        if e:
+            return ERR, e, 0, 0, b""
+        s.window.receive_cnt += 1
+        self.set_current_session(ridx)
+        return self.validate(dst, P)
+
+    def validate(self, dst, P):
+        """validate_decapsulated_packet, mod.rs:606-670."""
+        if P == 0:
+            self.rx_bytes += 32
+            return DONE, 0, 0, 0, b""
+        v = dst[0] >> 4
+        if v == 4 and P >= 20:
+            ip_len, src_ip = int.from_bytes(dst[2:4], "big"), bytes(dst[12:16])
+        elif v == 6 and P >= 40:
+            ip_len, src_ip = int.from_bytes(dst[4:6], "big") + 40, bytes(dst[8:24])
+        else:
+            return ERR, INVALID_PACKET, 0, 0, b""
+        if ip_len > P:
+            return ERR, INVALID_PACKET, 0, 0, b""
+        self.rx_bytes += ip_len + 32
+        return WRITE_TO_TUNNEL, 0, ip_len, v, src_ip
+
+    def decrypt(self, d: bytes, dst: bytearray):
+        """xray Tunn::decrypt: Ok(p) -> WRITE_TO_TUNNEL, else (ERR, code)."""
+        L = len(d)
+        if L < 4:
+            return ERR, INVALID_PACKET, 0, 0, b""
+        typ = int.from_bytes(d[:4], "little")
+        if (typ, L) in ((1, 148), (2, 92), (3, 64)):
+            return ERR, WRONG_PACKET_TYPE, 0, 0, b""
+        if typ != 4 or L < 32:
+            return ERR, INVALID_PACKET, 0, 0, b""
+        ridx = int.from_bytes(d[4:8], "little")
+        s = next((x for x in self.sessions
+                  if x is not None and ridx in (x.receiving_index, x.sending_index)), None)
+        if s is None:
+            return ERR, NO_CURRENT_SESSION, 0, 0, b""
+        if len(dst) < L - 16:
+            return ERR, DEST_TOO_SMALL, 0, 0, b""
+        key = s.recv_key if ridx == s.receiving_index else s.send_key
+        P = L - 32
+        st, pt = o.receive_packet_data(key, ridx, bytes(d))
+        dst[:P] = pt if st == 0 else bytes(P)
+        dst[P:P + 16] = d[16 + P:32 + P]
+        if st:
+            return ERR, st, 0, 0, b""
+        r = self.validate(dst, P)
+        if r[0] == DONE:
+            return ERR, UNEXPECTED_PACKET, 0, 0, b""
+        return r

@@ -1,4 +1,4 @@
-"""The C-ABI library loads and exports every symbol include/neptun_gpu.h declares.
+"""The C-ABI library loads and exports every symbol include/*.h declares.
 
 No compute calls here (this runs without a GPU).
 """
@@ -13,13 +13,32 @@ from neptun_amd import gpu as G
 from oracle import pyoracle as o
 
 
-def test_library_exports_header_symbols():
+@pytest.mark.parametrize("header", ["neptun_gpu.h", "neptun_tunn.h"])
+def test_library_exports_header_symbols(header):
+    import os
     lib = neptun_amd.load()
-    names = neptun_amd.header_functions()
-    assert len(names) >= 10
+    path = os.path.join(os.path.dirname(neptun_amd.HEADER_PATH), header)
+    names = neptun_amd.header_functions(path)
+    assert len(names) >= 9
     for name in names:
-        assert hasattr(lib, name), f"{name} declared in include/neptun_gpu.h but not exported"
+        assert hasattr(lib, name), f"{name} declared in include/{header} but not exported"
     assert lib.wg_gpu_abi_version() == 1
+
+
+def test_tunn_layouts_match_header():
+    from neptun_amd.tunn import Replay, TunnResult
+    text = open(neptun_amd.HEADER_PATH.replace("neptun_gpu.h", "neptun_tunn.h")).read()
+    assert "#define WG_REPLAY_WORDS 16" in text and "#define WG_N_SESSIONS 8" in text
+    assert ctypes.sizeof(Replay) == 8 * 18
+    assert ctypes.sizeof(TunnResult) == 32
+
+
+def test_tunn_entry_points_fail_loudly_on_null():
+    from neptun_amd.tunn import _bind
+    lib = _bind(neptun_amd.load())
+    out = ctypes.c_void_p()
+    assert lib.wg_tunn_create(None, 0, ctypes.byref(out)) != 0
+    assert b"tunn_create" in lib.wg_gpu_last_error()
 
 
 def test_library_is_gfx950_code_object():

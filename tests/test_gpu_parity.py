@@ -376,3 +376,41 @@ def test_config3_full_size_round_trip(torch_cuda, gpu):
         pt = b.pt[off + 16:off + 16 + p].cpu().numpy().tobytes()
         got = b.wire[off:off + p + 32].cpu().numpy().tobytes()
         assert got == o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, i, pt)
+
+
+# ---------------------------------------------------------------------------
+# host-resident pipeline (pinned staging + overlapped hipMemcpyAsync)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("depth,chunk", [(3, 1 << 20), (2, 5 << 20)])
+def test_host_pipe_matches_device_path(torch_cuda, gpu, depth, chunk):
+    torch = torch_cuda
+    import neptun_amd
+    n, P = 10007, 1350           # not a multiple of the chunk's packet count
+    S_host = 1392                # a host layout that is not the device slot layout
+    keys = synth.keys(1, seed=5)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    pipe = neptun_amd.GpuPipe(gpu, chunk_bytes=chunk, depth=depth)
+    pt = torch.randint(0, 256, (n * S_host,), dtype=torch.uint8).pin_memory()
+    wire = torch.zeros(n * S_host, dtype=torch.uint8).pin_memory()
+    back = torch.zeros(n * S_host, dtype=torch.uint8).pin_memory()
+    st = torch.full((n,), -1, dtype=torch.int32).pin_memory()
+    pipe.seal_strided(n, P, 0, 1234, pt, S_host, wire, S_host, st)
+    assert int((st != 0).sum()) == 0
+    # reference: oracle on a sample, device strided path on all
+    w = wire.numpy().reshape(n, S_host)
+    p = pt.numpy().reshape(n, S_host)
+    for i in (0, 1, 4095, 4096, n - 1):
+        assert w[i, :P + 32].tobytes() == o.format_packet_data(
+            keys[0].tobytes(), synth.RECEIVER_IDX, 1234 + i, p[i, :P].tobytes())
+    d_pt = pt.cuda()
+    d_wire = torch.zeros(n * S_host, dtype=torch.uint8, device="cuda")
+    gpu.seal_strided(n, P, 0, 1234, d_pt, S_host, d_wire, S_host)
+    torch.cuda.synchronize()
+    dw = d_wire.cpu().numpy().reshape(n, S_host)
+    assert np.array_equal(w[:, :P + 32], dw[:, :P + 32])
+    assert not w[:, P + 32:].any()   # only packet bytes are written back
+    st.fill_(-1)
+    pipe.open_strided(n, P + 32, 0, wire, S_host, back, S_host, st)
+    assert int((st != 0).sum()) == 0
+    assert np.array_equal(back.numpy().reshape(n, S_host)[:, :P], p[:, :P])
+    pipe.close()

@@ -1,0 +1,254 @@
+"""Batched Tunn (neptun_amd/csrc/wg_tunn.cpp, AEAD on the GPU) == N sequential
+calls of the Tunn data plane (oracle/tunn_model.py, restating mod.rs:295-380,
+545-670 and session.rs:40-302): same TunnResult per packet, same bytes in
+every destination buffer, same counters, replay windows and byte stats.
+
+Traffic covers what the reference's tests and code paths distinguish:
+in-order, reordered, duplicated and too-old counters (session.rs:367-414),
+tampered tags, wrong receiver index, unknown session, handshake-shaped and
+malformed datagrams, keepalives, IPv4/IPv6 packets with valid and truncated
+length fields, undersized destination buffers, and a session switch.
+"""
+import random
+import struct
+
+import pytest
+
+from oracle import tunn_model as M
+from oracle import pyoracle as o
+
+pytestmark = pytest.mark.gpu
+
+FIRST_SLOT = 4000  # the session fixture's context has 4096 slots
+
+
+def ipv4(rng, total, claimed=None):
+    b = bytearray(rng.randbytes(total))
+    b[0] = 0x45
+    b[2:4] = struct.pack(">H", total if claimed is None else claimed)
+    return bytes(b)
+
+
+def ipv6(rng, total, claimed=None):
+    b = bytearray(rng.randbytes(total))
+    b[0] = 0x60
+    b[4:6] = struct.pack(">H", (total - 40) if claimed is None else claimed)
+    return bytes(b)
+
+
+def plaintexts(rng, n):
+    out = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.45:
+            out.append(ipv4(rng, rng.choice([20, 64, 576, 1350, rng.randrange(20, 1500)])))
+        elif r < 0.7:
+            out.append(ipv6(rng, rng.choice([40, 96, 1280, rng.randrange(40, 1500)])))
+        elif r < 0.75:
+            out.append(b"")  # keepalive
+        elif r < 0.8:
+            t = rng.randrange(24, 200)
+            out.append(ipv4(rng, t, claimed=t + rng.randrange(1, 50)))  # truncated
+        elif r < 0.85:
+            out.append(ipv6(rng, 60, claimed=100))
+        elif r < 0.9:
+            b = bytearray(rng.randbytes(rng.randrange(1, 60)))
+            b[0] = 0x75  # neither v4 nor v6
+            out.append(bytes(b))
+        elif r < 0.95:
+            out.append(ipv4(rng, 200, claimed=100))  # padded: len = claimed
+        else:
+            out.append(bytes([0x45]) + rng.randbytes(rng.randrange(0, 19)))  # v4 nibble, < 20 B
+    return out
+
+
+def make_pair(gpu, rng):
+    tm, tg = M.Tunn(), None
+    from neptun_amd.tunn import Tunn
+    tg = Tunn(gpu, FIRST_SLOT)
+    sessions = []
+    for local in (3, 12):  # ring slots 3 and 4
+        rk, sk = rng.randbytes(32), rng.randbytes(32)
+        peer = rng.getrandbits(32)
+        tm.install_session(local, peer, rk, sk, True)
+        tg.install_session(local, peer, rk, sk, True)
+        sessions.append((local, peer, rk, sk))
+    return tm, tg, sessions
+
+
+def check_same(res_g, res_m, dst_g, dst_m, what):
+    assert len(res_g) == len(res_m)
+    for i, (g, m) in enumerate(zip(res_g, res_m)):
+        kind, st, ln = m[:3]
+        assert (g[0], g[1], g[2]) == (kind, st, ln), (what, i, g[:3], m[:3])
+        if len(m) > 3 and kind == M.WRITE_TO_TUNNEL:
+            v, ip = m[3], m[4]
+            assert g[3] == v and g[4][:len(ip)] == ip, (what, i)
+        assert bytes(dst_g[i]) == bytes(dst_m[i]), (what, i)
+
+
+def datagrams(rng, sessions, n, ctr_state):
+    """Peer-side traffic for the sessions plus damaged / foreign messages."""
+    out = []
+    pts = plaintexts(rng, n)
+    for j in range(n):
+        local, peer, rk, sk = sessions[rng.randrange(len(sessions))]
+        r = rng.random()
+        c = ctr_state.setdefault(local, 0)
+        if r < 0.55:
+            ctr = c
+            ctr_state[local] = c + 1
+        elif r < 0.7:
+            ctr = max(0, c - rng.randrange(1, 100))  # reorder / duplicate inside the window
+        elif r < 0.73:
+            ctr = max(0, c - rng.randrange(1100, 5000))  # older than the window
+        elif r < 0.76:
+            ctr = c + rng.randrange(2, 2500)  # loss burst / jump past the window
+            ctr_state[local] = ctr + 1
+        else:
+            ctr = c
+            ctr_state[local] = c + 1
+        d = bytearray(o.format_packet_data(rk, local, ctr, pts[j]))
+        r = rng.random()
+        if r < 0.04:
+            d[rng.randrange(16, len(d))] ^= 1 << rng.randrange(8)  # tamper ct or tag
+        elif r < 0.06:
+            d[4:8] = struct.pack("<I", local + 8)  # same ring slot, wrong index
+        elif r < 0.08:
+            d[4:8] = struct.pack("<I", 6)  # ring slot with no session
+        elif r < 0.09:
+            d = bytearray(struct.pack("<I", 1) + rng.randbytes(144))  # handshake init
+        elif r < 0.10:
+            d = bytearray(struct.pack("<I", 2) + rng.randbytes(88))  # handshake response
+        elif r < 0.11:
+            d = bytearray(struct.pack("<I", 3) + rng.randbytes(60))  # cookie reply
+        elif r < 0.12:
+            d = bytearray(rng.randbytes(rng.randrange(0, 4)))  # empty / too short
+        elif r < 0.13:
+            d = d[:rng.randrange(4, 32)]  # truncated data message
+        elif r < 0.14:
+            d[0] = 7  # unknown type
+        out.append(bytes(d))
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_decapsulate_batch_matches_sequential_tunn(gpu, seed):
+    rng = random.Random(seed)
+    tm, tg, sessions = make_pair(gpu, rng)
+    ctr_state = {}
+    for batch in range(4):
+        dgs = datagrams(rng, sessions, 600, ctr_state)
+        caps = []
+        for d in dgs:
+            need = max(len(d) - 16, 0)
+            caps.append(need if rng.random() > 0.03 else max(need - rng.randrange(1, 17), 0))
+        dst_m = [bytearray(b"\xee" * c) for c in caps]
+        dst_g = [bytearray(b"\xee" * c) for c in caps]
+        res_m = [tm.decapsulate(d, dm) for d, dm in zip(dgs, dst_m)]
+        res_g = tg.decapsulate_batch(dgs, dst_g)
+        check_same(res_g, res_m, dst_g, dst_m, f"decap batch {batch}")
+        kinds = {r[0] for r in res_m}
+        assert {M.WRITE_TO_TUNNEL, M.ERR}.issubset(kinds)
+    for local, *_ in sessions:
+        ctr, w = tg.session_counters(local % M.N_SESSIONS)
+        sm = tm.sessions[local % M.N_SESSIONS]
+        assert w.next == sm.window.next and list(w.bitmap) == sm.window.bitmap
+        assert w.receive_cnt == sm.window.receive_cnt
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    tg.close()
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_encapsulate_batch_matches_sequential_tunn(gpu, seed):
+    rng = random.Random(seed)
+    tm, tg, sessions = make_pair(gpu, rng)
+    for batch in range(3):
+        srcs = [rng.randbytes(rng.choice([0, 1, 15, 16, 17, 64, 1350, rng.randrange(0, 9000)]))
+                for _ in range(500)]
+        caps = []
+        for s in srcs:
+            r = rng.random()
+            caps.append(len(s) + 32 + rng.randrange(0, 40) if r > 0.06 else
+                        len(s) + 16 + rng.randrange(0, 16) if r > 0.03 else len(s) + rng.randrange(0, 16))
+        dst_m = [bytearray(b"\xee" * c) for c in caps]
+        dst_g = [bytearray(b"\xee" * c) for c in caps]
+        res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dst_m)]
+        res_g = tg.encapsulate_batch(srcs, dst_g)
+        check_same(res_g, res_m, dst_g, dst_m, f"encap batch {batch}")
+        # the peer receives what we sent: a keepalive / arbitrary payload path through decap
+        if batch == 1:
+            # switch current session: a valid packet on the first session (older install)
+            # must not take over from the newer one (set_current_session, mod.rs:521-532)
+            local, peer, rk, sk = sessions[0]
+            d = o.format_packet_data(rk, local, 0, b"")
+            dm, dg = bytearray(16), bytearray(16)
+            check_same(tg.decapsulate_batch([d], [dg]), [tm.decapsulate(d, dm)], [dg], [dm], "ka")
+            assert tm.current == sessions[1][0]
+    for local, *_ in sessions:
+        ctr, _ = tg.session_counters(local % M.N_SESSIONS)
+        assert ctr == tm.sessions[local % M.N_SESSIONS].sending_counter
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    tg.close()
+
+
+def test_round_trip_between_two_tunns(gpu):
+    """Two GPU Tunns as peers: A encapsulates, B decapsulates to the same IP packets."""
+    from neptun_amd.tunn import Tunn
+    rng = random.Random(9)
+    a, b = Tunn(gpu, FIRST_SLOT), Tunn(gpu, FIRST_SLOT - 16)
+    k1, k2 = rng.randbytes(32), rng.randbytes(32)
+    a.install_session(21, 34, k2, k1, True)  # a sends with k1 to index 34
+    b.install_session(34, 21, k1, k2, True)
+    pkts = [ipv4(rng, rng.randrange(20, 1500)) for _ in range(300)]
+    wires = [bytearray(len(p) + 32) for p in pkts]
+    res = a.encapsulate_batch(pkts, wires)
+    assert all(r[0] == M.WRITE_TO_NETWORK for r in res)
+    outs = [bytearray(len(p) + 16) for p in pkts]
+    res = b.decapsulate_batch([bytes(w) for w in wires], outs)
+    assert all(r[0] == M.WRITE_TO_TUNNEL for r in res)
+    assert all(bytes(o_[:len(p)]) == p for o_, p in zip(outs, pkts))
+    # replaying the whole batch is refused packet by packet
+    res = b.decapsulate_batch([bytes(w) for w in wires], outs)
+    assert all(r[:2] == (M.ERR, M.DUPLICATE_COUNTER) for r in res)
+    a.close()
+    b.close()
+
+
+def test_no_session_and_argument_errors(gpu):
+    """encapsulate without a session -> NOT_DATA (the CPU Tunn handshakes and queues,
+    mod.rs:325-337); the src copy into dst[16..] happens first, like the reference."""
+    from neptun_amd.tunn import Tunn
+    tm, tg = M.Tunn(), Tunn(gpu, FIRST_SLOT)
+    srcs = [b"\x45" * 40, b"", b"abc" * 10]
+    caps = [100, 32, 20]
+    dm = [bytearray(b"\xee" * c) for c in caps]
+    dg = [bytearray(b"\xee" * c) for c in caps]
+    res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dm)]
+    check_same(tg.encapsulate_batch(srcs, dg), res_m, dg, dm, "no session")
+    assert [r[:2] for r in res_m] == [(M.NOT_DATA, M.NO_CURRENT_SESSION)] * 2 + [(M.ERR, M.INVALID_LENGTH)]
+    tg.close()
+
+
+@pytest.mark.parametrize("seed", [7, 8])
+def test_decrypt_batch_matches_xray_decrypt(gpu, seed):
+    """Tunn::decrypt (xray, mod.rs:383-417): either direction's key, no replay window --
+    so duplicates decrypt again; keepalives are UnexpectedPacket."""
+    rng = random.Random(seed)
+    tm, tg, sessions = make_pair(gpu, rng)
+    dgs = datagrams(rng, sessions, 500, {})
+    # our own outbound traffic (receiver_idx = peer index, sending key) and its duplicates
+    for local, peer, rk, sk in sessions:
+        for c, p in enumerate(plaintexts(rng, 60)):
+            dgs.append(o.format_packet_data(sk, peer, c % 40, p))
+    rng.shuffle(dgs)
+    caps = [max(len(d) - 16, 0) if rng.random() > 0.03 else max(len(d) - 20, 0) for d in dgs]
+    dm = [bytearray(b"\xee" * c) for c in caps]
+    dg = [bytearray(b"\xee" * c) for c in caps]
+    res_m = [tm.decrypt(d, x) for d, x in zip(dgs, dm)]
+    check_same(tg.decrypt_batch(dgs, dg), res_m, dg, dm, "decrypt")
+    codes = {r[:2] for r in res_m}
+    assert (M.ERR, M.UNEXPECTED_PACKET) in codes and (M.ERR, M.WRONG_PACKET_TYPE) in codes
+    assert sum(r[0] == M.WRITE_TO_TUNNEL for r in res_m) > 300
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    tg.close()

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Host-resident end-to-end rate (north star: "the end-to-end rate including
+hipMemcpyAsync to/from pinned host staging must also be measured").
+
+1M x 1350 B packets in pinned host memory (NepTUN slot layout, stride 1408),
+sealed and opened through wg_gpu_pipe_* (chunked H2D -> kernel -> D2H over
+several streams).  Prints one JSON line per (chunk, depth) and the raw pinned
+copy bandwidth for reference.  Not the bench.py metric (that one is
+device-resident).
+"""
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+    import torch
+
+    import neptun_amd
+    from tools import synth
+    n, P, S = 1 << 20, 1350, 1408
+    reps = 5
+    ctx = neptun_amd.GpuContext(0, key_slots=1)
+    ctx.set_keys(0, synth.keys(1), np.array([synth.RECEIVER_IDX], np.uint32))
+    pt = synth.device_payloads(n, P, S, "cuda", offset=16).cpu().pin_memory()
+    wire = torch.zeros(n * S, dtype=torch.uint8).pin_memory()
+    back = torch.zeros(n * S, dtype=torch.uint8).pin_memory()
+    st = torch.zeros(n, dtype=torch.int32).pin_memory()
+    # raw pinned copy bandwidth (one direction at a time, one 1.48 GB copy)
+    d = torch.empty(n * S, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    t = time.perf_counter(); d.copy_(pt, non_blocking=True); torch.cuda.synchronize()
+    h2d = n * S / (time.perf_counter() - t) / 1e9
+    t = time.perf_counter(); back.copy_(d, non_blocking=True); torch.cuda.synchronize()
+    d2h = n * S / (time.perf_counter() - t) / 1e9
+    del d
+    print(json.dumps({"pinned_copy_GBps": {"h2d": round(h2d, 2), "d2h": round(d2h, 2)}}), flush=True)
+    best = None
+    for chunk in (16 << 20, 64 << 20, 256 << 20):
+        for depth in (2, 3, 4):
+            pipe = neptun_amd.GpuPipe(ctx, chunk_bytes=chunk, depth=depth)
+            ts, to = [], []
+            for _ in range(reps + 1):
+                t0 = time.perf_counter()
+                pipe.seal_strided(n, P, 0, 0, pt.data_ptr() + 16, S, wire, S, st)
+                t1 = time.perf_counter()
+                pipe.open_strided(n, P + 32, 0, wire, S, back.data_ptr() + 16, S, st)
+                t2 = time.perf_counter()
+                ts.append(t1 - t0); to.append(t2 - t1)
+            ts, to = ts[1:], to[1:]
+            ok = torch.equal(back.view(n, S)[:, 16:16 + P], pt.view(n, S)[:, 16:16 + P])
+            ms, mo = statistics.median(ts), statistics.median(to)
+            line = {"chunk_MiB": chunk >> 20, "depth": depth, "verified": bool(ok),
+                    "seal_ms": round(ms * 1e3, 3), "open_ms": round(mo * 1e3, 3),
+                    "seal_gbps": round(n * P * 8 / ms / 1e9, 1),
+                    "open_gbps": round(n * P * 8 / mo / 1e9, 1),
+                    "roundtrip_gbps": round(n * P * 8 / (ms + mo) / 1e9, 1)}
+            print(json.dumps(line), flush=True)
+            if ok and (best is None or line["roundtrip_gbps"] > best["roundtrip_gbps"]):
+                best = line
+            pipe.close()
+    print(json.dumps({"best": best, "packets": n, "packet_bytes": P,
+                      "note": "host-resident: pinned host in -> GPU -> pinned host out"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
