@@ -59,6 +59,10 @@ constexpr uint32_t kWaves = kBlockThreads / 64;
 #endif
 constexpr uint32_t kBufs = WG_PREFETCH ? 2 : 1;
 
+#ifndef WG_REG_PREFETCH
+#define WG_REG_PREFETCH 0  // 1: uniform path loads round r+1 into VGPRs during round r
+#endif
+
 // LDS of one wave.  Generic geometry: one 8 KiB run buffer + per-packet tables.
 struct WaveStage {
   uint4 run[1][64 * kChunks];  // [buffer][packet][chunk ^ swz(packet)], 8 KiB
@@ -214,20 +218,62 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
     partial |= ok && hi - w < 16u;
   }
   if (partial) {  // the packet's last, partial chunk (last round only)
+    // n = 1..15 bytes as 3 dword + 1 short + 1 byte buffer stores, each masked
+    // per lane by an out-of-range offset: a static instruction count, so the
+    // compiler's vmcnt bookkeeping stays exact across rounds
 #pragma unroll
     for (uint32_t j = 0; j < kChunks; ++j) {
       const uint32_t k = (j & 1u) ? k1 : k0;
       const uint32_t w = kRun * r + 16u * k;
       const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
-      if (!dead && w >= Ranges<kSeal>::out_lo() && w < hi && hi - w < 16u) {
-        const uint4 v = run[64u * j + lane];
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-        store_partial(reinterpret_cast<uint8_t *>(g.out0) + 8u * j * stride + kRun * r +
-                          y * stride + 16u * k,
-                      wv, (int)(hi - w));
-      }
+      const bool mine = !dead && w >= Ranges<kSeal>::out_lo() && w < hi && hi - w < 16u;
+      const uint32_t n = mine ? hi - w : 0u;
+      const uint4 v = run[64u * j + lane];
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t base = y * stride + 16u * k, soff = 8u * j * stride + kRun * r;
+#pragma unroll
+      for (uint32_t d = 0; d < 3; ++d)
+        __builtin_amdgcn_raw_buffer_store_b32(wv[d], rs, 4u * (d + 1u) <= n ? base + 4u * d
+                                                                            : kNoAccess, soff, 0);
+      const uint32_t nd = n >> 2, rem = n & 3u;
+      const uint32_t last = nd == 0 ? wv[0] : nd == 1 ? wv[1] : nd == 2 ? wv[2] : wv[3];
+      __builtin_amdgcn_raw_buffer_store_b16((unsigned short)last, rs,
+                                            rem >= 2u ? base + 4u * nd : kNoAccess, soff, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(last >> (8u * (rem & 2u))), rs,
+                                           (rem & 1u) ? base + 4u * nd + (rem & 2u) : kNoAccess,
+                                           soff, 0);
     }
   }
+}
+
+// Register-prefetch form of the uniform load: the same 8 coalesced loads (8
+// packets x 128 contiguous bytes per wave instruction) into VGPRs, issued one
+// round ahead and written to the LDS stage at the top of the round they feed.
+// Costs 32 VGPRs (3 waves/SIMD instead of 4) but takes the HBM round trip off
+// the critical path of every round.
+template <bool kSeal>
+__device__ __forceinline__ void load_regs(u32x4 (&pre)[kChunks], const UniformGeom &g,
+                                          uint32_t lane, uint32_t r) {
+  const uint32_t stride = (uint32_t)g.in_stride;
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 64u * stride);
+  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
+  const uint32_t hi = Ranges<kSeal>::in_hi(g.W);
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j) {
+    const uint32_t k = (j & 1u) ? k1 : k0;
+    const uint32_t w = kRun * r + 16u * k;
+    const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
+    const bool ok = !dead && w >= Ranges<kSeal>::in_lo() && w < hi;
+    pre[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? y * stride + 16u * k : kNoAccess,
+                                                   8u * j * stride + kRun * r, 0);
+  }
+}
+
+__device__ __forceinline__ void commit_regs(uint4 *run, const u32x4 (&pre)[kChunks],
+                                            uint32_t lane) {
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j)
+    run[64u * j + lane] = make_uint4(pre[j].x, pre[j].y, pre[j].z, pre[j].w);
 }
 
 // One lane's chunk of ciphertext work.  m = plaintext/ciphertext byte index of
@@ -363,13 +409,28 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 
   // double buffering only for the uniform geometry (static vmcnt counts)
   constexpr bool kPrefetch = kUniform && sizeof(S.run) / sizeof(S.run[0]) == 2;
+  constexpr bool kRegPf = kUniform && !kPrefetch && WG_REG_PREFETCH;
+  u32x4 pre[kChunks];
 #if !WG_ABLATE_NO_MEM
   if constexpr (kPrefetch) stage_in<kSeal>(S.run[0], g, lane, 0);
+  if constexpr (kRegPf) {
+    load_regs<kSeal>(pre, g, lane, 0);
+    // 8 no-op stores (out-of-range offsets) give the loop entry the same
+    // "8 loads, then 8 stores" vmcnt shape as the back edge, so the waits the
+    // compiler puts before commit_regs are vmcnt(15..8), not vmcnt(7..0)
+    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, 64u * (uint32_t)g.out_stride);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, rs, kNoAccess, 16u * j, 0);
+  }
 #endif
   for (uint32_t r = 0; r < rounds; ++r) {
     uint4 *run = S.run[kPrefetch ? (r & 1u) : 0u];
 #if !WG_ABLATE_NO_MEM
-    if constexpr (kPrefetch) {
+    if constexpr (kRegPf) {
+      commit_regs(run, pre, lane);
+      if (r + 1u < rounds) load_regs<kSeal>(pre, g, lane, r + 1u);
+    } else if constexpr (kPrefetch) {
       if (r + 1u < rounds) {
         stage_in<kSeal>(S.run[(r + 1u) & 1u], g, lane, r + 1u);
         // everything older than round r+1's 8 loads is done (round r's DMA)

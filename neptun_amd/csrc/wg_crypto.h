@@ -20,10 +20,21 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) {
   return __builtin_amdgcn_alignbit(x, x, 32u - n);  // v_alignbit_b32: 1 VALU op
 }
 
+#ifndef WG_ROT_PERM
+#define WG_ROT_PERM 0  // 1: byte rotations (16, 8) as v_perm_b32
+#endif
+#if WG_ROT_PERM
+__device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x01000302u); }
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x02010003u); }
+#else
+__device__ __forceinline__ uint32_t rotl16(uint32_t x) { return rotl(x, 16); }
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return rotl(x, 8); }
+#endif
+
 #define WG_QR(a, b, c, d)                   \
-  a += b; d ^= a; d = rotl(d, 16);          \
+  a += b; d ^= a; d = rotl16(d);            \
   c += d; b ^= c; b = rotl(b, 12);          \
-  a += b; d ^= a; d = rotl(d, 8);           \
+  a += b; d ^= a; d = rotl8(d);             \
   c += d; b ^= c; b = rotl(b, 7);
 
 constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu, kSigma2 = 0x79622d32u,
@@ -89,6 +100,81 @@ __device__ __forceinline__ uint64_t mad_c(uint32_t a, uint32_t b, uint64_t c) {
 __device__ __forceinline__ uint64_t mad_c(uint32_t a, uint32_t b, uint64_t c) { return mad(a, b, c); }
 #endif
 
+#ifndef WG_POLY_ONE_ASM
+#define WG_POLY_ONE_ASM 1
+#endif
+
+#if WG_POLY_ONE_ASM
+// h = (h + m + 2^128) * r  (partially reduced mod 2^130 - 5).
+// The 21 multiply-accumulates are ONE asm statement: the compiler pads every
+// separate asm statement that writes an SGPR (the mads' carry-out) with an
+// s_nop, which cost 21 issue slots per block.  Inside: the h + m + 2^128 carry
+// chain, four carry-seeded chains d0..d3 (2^130 == 5 folding via s_i = 5 r_i / 4;
+// seed = (d_{j-1} >> 32) by a 64-bit shift), and h4 * r0.  The carry-out goes to
+// a scratch SGPR pair nothing reads.
+__device__ __forceinline__ void poly_block(Poly &p, uint32_t m0, uint32_t m1, uint32_t m2,
+                                           uint32_t m3) {
+  uint32_t a0, a1, a2, a3, a4;  // h + m + 2^128
+  uint64_t d0, d1, d2, d3, e4, seed, sc;
+  asm volatile(
+      "v_add_co_u32 %[a0], vcc, %[h0], %[m0]\n\t"
+      "v_addc_co_u32 %[a1], vcc, %[h1], %[m1], vcc\n\t"
+      "v_addc_co_u32 %[a2], vcc, %[h2], %[m2], vcc\n\t"
+      "v_addc_co_u32 %[a3], vcc, %[h3], %[m3], vcc\n\t"
+      "v_addc_co_u32 %[a4], vcc, 1, %[h4], vcc\n\t"
+      // d0 = h0 r0 + h1 s3 + h2 s2 + h3 s1
+      "v_mad_u64_u32 %[d0], %[sc], %[a0], %[r0], 0\n\t"
+      "v_mad_u64_u32 %[d0], %[sc], %[a1], %[s3], %[d0]\n\t"
+      "v_mad_u64_u32 %[d0], %[sc], %[a2], %[s2], %[d0]\n\t"
+      "v_mad_u64_u32 %[d0], %[sc], %[a3], %[s1], %[d0]\n\t"
+      // d1 = (d0 >> 32) + h0 r1 + h1 r0 + h2 s3 + h3 s2 + h4 s1
+      "v_lshrrev_b64 %[seed], 32, %[d0]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a0], %[r1], %[seed]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a1], %[r0], %[d1]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a2], %[s3], %[d1]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a3], %[s2], %[d1]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a4], %[s1], %[d1]\n\t"
+      // d2 = (d1 >> 32) + h0 r2 + h1 r1 + h2 r0 + h3 s3 + h4 s2
+      "v_lshrrev_b64 %[seed], 32, %[d1]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a0], %[r2], %[seed]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a1], %[r1], %[d2]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a2], %[r0], %[d2]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a3], %[s3], %[d2]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a4], %[s2], %[d2]\n\t"
+      // d3 = (d2 >> 32) + h0 r3 + h1 r2 + h2 r1 + h3 r0 + h4 s3
+      "v_lshrrev_b64 %[seed], 32, %[d2]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a0], %[r3], %[seed]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a1], %[r2], %[d3]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a2], %[r1], %[d3]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a3], %[r0], %[d3]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a4], %[s3], %[d3]\n\t"
+      // h4' = (d3 >> 32) + h4 r0  (< 2^32)
+      "v_lshrrev_b64 %[seed], 32, %[d3]\n\t"
+      "v_mad_u64_u32 %[e4], %[sc], %[a4], %[r0], %[seed]"
+      : [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4),
+        [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2), [d3] "=&v"(d3), [e4] "=&v"(e4),
+        [seed] "=&v"(seed), [sc] "=&s"(sc)
+      : [h0] "v"(p.h0), [h1] "v"(p.h1), [h2] "v"(p.h2), [h3] "v"(p.h3), [h4] "v"(p.h4),
+        [m0] "v"(m0), [m1] "v"(m1), [m2] "v"(m2), [m3] "v"(m3),
+        [r0] "v"(p.r0), [r1] "v"(p.r1), [r2] "v"(p.r2), [r3] "v"(p.r3),
+        [s1] "v"(p.s1), [s2] "v"(p.s2), [s3] "v"(p.s3)
+      : "vcc");
+  // fold bits >= 130: c = 5 * (h4' >> 2), then one carry chain
+  uint32_t h4 = (uint32_t)e4;
+  const uint32_t c = (h4 >> 2) + (h4 & ~3u);
+  h4 &= 3u;
+  asm volatile(
+      "v_add_co_u32 %0, vcc, %5, %6\n\t"
+      "v_addc_co_u32 %1, vcc, 0, %7, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, 0, %8, vcc\n\t"
+      "v_addc_co_u32 %3, vcc, 0, %9, vcc\n\t"
+      "v_addc_co_u32 %4, vcc, 0, %10, vcc"
+      : "=&v"(p.h0), "=&v"(p.h1), "=&v"(p.h2), "=&v"(p.h3), "=&v"(p.h4)
+      : "v"(c), "v"((uint32_t)d0), "v"((uint32_t)d1), "v"((uint32_t)d2), "v"((uint32_t)d3),
+        "v"(h4)
+      : "vcc");
+}
+#else
 // h = (h + m + 2^128) * r  (partially reduced mod 2^130 - 5)
 __device__ __forceinline__ void poly_block(Poly &p, uint32_t m0, uint32_t m1, uint32_t m2,
                                            uint32_t m3) {
@@ -149,6 +235,8 @@ __device__ __forceinline__ void poly_block(Poly &p, uint32_t m0, uint32_t m1, ui
   p.h4 = h4 + (uint32_t)(t2 >> 32);
 #endif
 }
+
+#endif  // WG_POLY_ONE_ASM
 
 // tag = (h mod p) + s mod 2^128; h < 5*2^128 < 2p so one conditional subtract
 __device__ __forceinline__ void poly_finish(const Poly &p, const uint32_t s[4], uint32_t tag[4]) {

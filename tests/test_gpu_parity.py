@@ -414,3 +414,40 @@ def test_host_pipe_matches_device_path(torch_cuda, gpu, depth, chunk):
     assert int((st != 0).sum()) == 0
     assert np.array_equal(back.numpy().reshape(n, S_host)[:, :P], p[:, :P])
     pipe.close()
+
+
+@pytest.mark.parametrize("P", list(range(0, 70)) + [127, 128, 129, 240, 255, 256, 257, 1000, 1349,
+                                                   1350, 1351, 1407, 1500, 8900])
+def test_strided_every_tail_shape(torch_cuda, gpu, P):
+    """Uniform strided kernel (+ its one-wave tail launch) at lengths covering every
+    partial-chunk size 0..15 on both sides: wire bytes equal the oracle's, nothing
+    is written outside each packet (guard bytes), open restores the plaintext."""
+    torch = torch_cuda
+    n = 130  # two full uniform waves + a 2-packet tail wave
+    S = synth.round_up(P + 32 + 16, 128)
+    keys = synth.keys(1, seed=P + 1)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    rng = np.random.default_rng(P)
+    src = rng.integers(0, 256, n * S, dtype=np.uint8)
+    pt = to_dev(torch, src)
+    wire = torch.full((n * S,), 0xAB, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.seal_strided(n, P, 0, 5 + P, pt.data_ptr() + 16, S, wire, S, st)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = np.arange(n) * S + 16
+    descs["dst_off"] = np.arange(n) * S
+    descs["counter"] = 5 + P + np.arange(n, dtype=np.uint64)
+    descs["len"] = P
+    want = np.full(n * S, 0xAB, np.uint8)
+    assert (o.seal_batch(descs, keys, np.array([synth.RECEIVER_IDX], np.uint32), src, want) == 0).all()
+    assert np.array_equal(wire.cpu().numpy(), want)  # includes the guard bytes past P + 32
+    back = torch.full((n * S,), 0xCD, dtype=torch.uint8, device="cuda")
+    st.fill_(-1)
+    gpu.open_strided(n, P + 32, 0, wire, S, back.data_ptr() + 16, S, st)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    got = back.cpu().numpy().reshape(n, S)
+    assert np.array_equal(got[:, 16:16 + P], src.reshape(n, S)[:, 16:16 + P])
+    assert (got[:, :16] == 0xCD).all() and (got[:, 16 + P:] == 0xCD).all()
