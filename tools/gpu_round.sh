@@ -11,6 +11,7 @@ step smoke && timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke(
 && step bench2 && timeout -k 10 400 python bench.py > $OUT/bench2.json 2> $OUT/bench2.err && cat $OUT/bench2.json \
 && step bench3 && timeout -k 10 400 python bench.py --config 3 --steps 20 > $OUT/bench3.json 2> $OUT/bench3.err && cat $OUT/bench3.json \
 && step bench4 && timeout -k 10 600 python bench.py --config 4 --steps 5 --warmup 2 > $OUT/bench4.json 2> $OUT/bench4.err && cat $OUT/bench4.json \
-&& step trace && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/trace.log 2>&1 \
+&& step trace && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/trace_bench.json 2> $OUT/trace.log && cat $OUT/trace_bench.json \
 && grep -E "aead|Name" $OUT/trace/run_kernel_stats.csv \
-&& step pmc && timeout -k 10 900 python tools/pmc_traffic.py $OUT/pmc_traffic.json > $OUT/pmc.log 2>&1 && cat $OUT/pmc_traffic.json
+&& step pmc && timeout -k 10 900 python tools/pmc_traffic.py $OUT/pmc_traffic.json > $OUT/pmc.log 2>&1 && cat $OUT/pmc_traffic.json \
+&& step valu && timeout -k 10 600 python tools/pmc_valu.py $OUT/pmc_valu.json > $OUT/valu.log 2>&1 && cat $OUT/pmc_valu.json

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""VALU-side PMC summary of the bench kernels: effective clock, VALU
+instructions per wave, VALU-active fraction.  One rocprofv3 pass with
+--kernel-trace (durations) and --pmc (never combined with tracing domains).
+
+  clock_GHz        = GRBM_GUI_ACTIVE / 8 (XCDs) / kernel duration
+  valu_per_wave    = SQ_INSTS_VALU / SQ_WAVES
+  valu_issue_frac  = 4 * SQ_ACTIVE_INST_VALU (quad-cycles) / (clock cycles * 1024 SIMDs)
+
+    python tools/pmc_valu.py OUT.json [bench args...]
+"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COUNTERS = ["GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_SALU",
+            "SQ_INSTS_LDS"]
+
+
+def short(name):
+    for tag in ("aead_strided_kernel<true, false>", "aead_strided_kernel<false, false>",
+                "aead_desc_kernel<true>", "aead_desc_kernel<false>"):
+        if tag in name:
+            return tag
+    return None
+
+
+def main():
+    out, bench_args = sys.argv[1], sys.argv[2:]
+    d = os.path.join(ROOT, "gpurun_out", "pmc_valu")
+    cmd = ["rocprofv3", "--kernel-trace", "--pmc", *COUNTERS, "--output-format", "csv", "-d", d,
+           "-o", "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3",
+           "--warmup", "1", "--no-cpu-baseline"] + bench_args
+    subprocess.run(cmd, check=True, env=dict(os.environ, TMPDIR="/tmp"), timeout=600,
+                   stdout=subprocess.DEVNULL)
+    per = defaultdict(lambda: defaultdict(float))  # (kernel, dispatch) -> counter -> value
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            s = short(r["Kernel_Name"])
+            if s:
+                per[(s, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    dur = {}
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            s = short(r["Kernel_Name"])
+            if s:
+                dur[(s, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    agg = defaultdict(list)
+    for key, c in per.items():
+        t = dur.get(key)
+        if not t or not c.get("SQ_WAVES"):
+            continue
+        clk = c["GRBM_GUI_ACTIVE"] / 8 / t
+        agg[key[0]].append({
+            "ms": t * 1e3, "clock_GHz": clk / 1e9,
+            "valu_per_wave": c["SQ_INSTS_VALU"] / c["SQ_WAVES"],
+            "salu_per_wave": c["SQ_INSTS_SALU"] / c["SQ_WAVES"],
+            "lds_per_wave": c["SQ_INSTS_LDS"] / c["SQ_WAVES"],
+            "valu_issue_frac": 4 * c["SQ_ACTIVE_INST_VALU"] / (clk * t * 1024),
+        })
+    res = {"source": "rocprofv3 --kernel-trace --pmc " + " ".join(COUNTERS) + " on bench.py " +
+                     (" ".join(bench_args) or "(config 2)") + " (profiled: clocks read a few % low)",
+           "kernels": {k: {m: round(sum(x[m] for x in v) / len(v), 4) for m in v[0]} | {"dispatches": len(v)}
+                       for k, v in agg.items()}}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
