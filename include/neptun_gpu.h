@@ -183,6 +183,32 @@ int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
                         uint64_t dst_stride, int32_t *status, void *stream);
 
 /*
+ * Inbound routing on the device.  NepTUN routes a DATA
+ * datagram by its receiver index: the device picks the peer by
+ * receiver_idx >> 8 (device/mod.rs:1022-1024) and the peer's Tunn the session
+ * sessions[receiver_idx % 8] (noise/mod.rs:550-556).  Here one HBM table maps
+ * every live receiving index straight to the key slot holding that session's
+ * receiving key, so a batch of raw datagrams needs no host pre-pass:
+ *   wg_gpu_route_set   replaces the table (host arrays; n <= 2^22 entries);
+ *   wg_gpu_route_batch reads each descriptor's datagram header on the device
+ *                      (src + src_off, descs[i].len bytes) and writes
+ *                      descs[i].key_slot: the session's slot, or
+ *                      WG_KEY_SLOT_INVALID_PACKET when parse_incoming_packet
+ *                      would not yield a DATA packet (len < 32 or type != 4,
+ *                      mod.rs:139-199) or WG_KEY_SLOT_NO_SESSION when no
+ *                      session has that receiving index.
+ * The open kernels turn the two sentinels into WG_STATUS_INVALID_PACKET and
+ * WG_STATUS_NO_CURRENT_SESSION (in the reference's check order); the seal
+ * kernels treat them like any out-of-table slot.
+ */
+#define WG_KEY_SLOT_NO_SESSION 0xFFFFFFFFu
+#define WG_KEY_SLOT_INVALID_PACKET 0xFFFFFFFEu
+int wg_gpu_route_set(wg_gpu_ctx *ctx, uint32_t n, const uint32_t *receiver_idx,
+                     const uint32_t *key_slot);
+int wg_gpu_route_batch(wg_gpu_ctx *ctx, wg_packet_desc *descs, uint32_t n, const uint8_t *src,
+                       void *stream);
+
+/*
  * Host-resident batches (the real data path: TUN read buffers in, UDP send
  * buffers out and vice versa).  A pipe owns `depth` streams and device staging
  * buffers of `chunk_bytes` each; a call splits the batch into chunks and runs

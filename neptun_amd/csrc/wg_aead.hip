@@ -600,7 +600,9 @@ __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_desc_ke
     const uint64_t dst = reinterpret_cast<uint64_t>(prm.dst) + d.dst_off;
     job.in_base = kSeal ? src - 16u : src;
     job.out_base = kSeal ? dst : dst - 16u;
-    if (d.key_slot >= prm.key_slots) job.status = WG_STATUS_BAD_KEY_SLOT;
+    if (!kSeal && d.key_slot == WG_KEY_SLOT_INVALID_PACKET) job.status = WG_STATUS_INVALID_PACKET;
+    else if (!kSeal && d.key_slot == WG_KEY_SLOT_NO_SESSION) job.status = WG_STATUS_NO_CURRENT_SESSION;
+    else if (d.key_slot >= prm.key_slots) job.status = WG_STATUS_BAD_KEY_SLOT;
     else if (((d.src_off | d.dst_off) & 15u) != 0u) job.status = WG_STATUS_MISALIGNED;
     else job.status = WG_STATUS_OK;
   }

@@ -43,4 +43,13 @@ __global__ void plan_scan_kernel(uint32_t *table);
 __global__ void plan_scatter_kernel(const wg_packet_desc *descs, uint32_t n, uint32_t extra,
                                     const uint32_t *table, uint32_t *order);
 
+
+// wg_route.hip: receiver_idx -> key slot (linear probing, capacity 2^bits, empty
+// entries carry slot WG_KEY_SLOT_NO_SESSION); the same hash on host and device
+__host__ __device__ inline uint32_t route_hash(uint32_t x, uint32_t bits) {
+  return (x * 0x9E3779B1u) >> (32u - bits);
+}
+__global__ void route_kernel(wg_packet_desc *descs, uint32_t n, const uint8_t *src,
+                             const uint2 *table, uint32_t bits);
+
 }  // namespace wg

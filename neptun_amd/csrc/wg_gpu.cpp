@@ -13,6 +13,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "neptun_gpu.h"
 #include "wg_aead_kernels.h"
@@ -22,7 +23,9 @@ struct wg_gpu_ctx {
   uint32_t key_slots = 0;
   uint8_t *d_keys = nullptr;       // key_slots * 32
   uint32_t *d_key_index = nullptr; // key_slots
-  std::mutex mu;                   // serialises key-table updates
+  uint2 *d_route = nullptr;        // receiver_idx -> key slot (wg_route.hip), 2^route_bits
+  uint32_t route_bits = 0;
+  std::mutex mu;                   // serialises key-table and route-table updates
 };
 
 namespace {
@@ -104,6 +107,7 @@ int wg_gpu_ctx_destroy(wg_gpu_ctx *ctx) {
   (void)hipDeviceSynchronize();
   (void)hipFree(ctx->d_keys);
   (void)hipFree(ctx->d_key_index);
+  (void)hipFree(ctx->d_route);
   delete ctx;
   return WG_RC_OK;
 }
@@ -237,6 +241,55 @@ int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
                         uint64_t dst_stride, int32_t *status, void *stream) {
   return launch_strided(ctx, false, n, len, key_slot, 0, src, src_stride, dst, dst_stride, status,
                         stream);
+}
+
+int wg_gpu_route_set(wg_gpu_ctx *ctx, uint32_t n, const uint32_t *receiver_idx,
+                     const uint32_t *key_slot) {
+  if (!ctx || (n && (!receiver_idx || !key_slot)))
+    return fail(WG_RC_INVALID_ARGUMENT, "route_set: null argument");
+  if (n > (1u << 22)) return fail(WG_RC_INVALID_ARGUMENT, "route_set: more than 2^22 entries");
+  uint32_t bits = 4;
+  while ((1u << bits) < 2u * n) ++bits;  // load factor <= 1/2
+  const uint32_t cap = 1u << bits, mask = cap - 1u;
+  std::vector<uint2> tab(cap, uint2{0u, WG_KEY_SLOT_NO_SESSION});
+  for (uint32_t i = 0; i < n; ++i) {
+    if (key_slot[i] >= ctx->key_slots)
+      return fail(WG_RC_INVALID_ARGUMENT, "route_set: key slot outside the key table");
+    uint32_t pos = wg::route_hash(receiver_idx[i], bits);
+    while (tab[pos].y != WG_KEY_SLOT_NO_SESSION) {
+      if (tab[pos].x == receiver_idx[i])
+        return fail(WG_RC_INVALID_ARGUMENT, "route_set: duplicate receiver index");
+      pos = (pos + 1u) & mask;
+    }
+    tab[pos] = uint2{receiver_idx[i], key_slot[i]};
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard g(ctx->device);
+  uint2 *d = nullptr;
+  WG_HIP(hipMalloc(&d, (size_t)cap * sizeof(uint2)), "route_set: device alloc");
+  hipError_t e = hipMemcpy(d, tab.data(), (size_t)cap * sizeof(uint2), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return fail(WG_RC_HIP_ERROR, "route_set: copy", e);
+  }
+  // launches already queued may still read the old table
+  WG_HIP(hipDeviceSynchronize(), "route_set: sync");
+  (void)hipFree(ctx->d_route);
+  ctx->d_route = d;
+  ctx->route_bits = bits;
+  return WG_RC_OK;
+}
+
+int wg_gpu_route_batch(wg_gpu_ctx *ctx, wg_packet_desc *descs, uint32_t n, const uint8_t *src,
+                       void *stream) {
+  if (!ctx || (n && (!descs || !src))) return fail(WG_RC_INVALID_ARGUMENT, "route_batch: null argument");
+  if (n == 0) return WG_RC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);  // the table pointer is swapped by route_set
+  DeviceGuard g(ctx->device);
+  hipLaunchKernelGGL(wg::route_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), descs, n, src, ctx->d_route, ctx->route_bits);
+  WG_HIP(hipGetLastError(), "route_batch: launch");
+  return WG_RC_OK;
 }
 
 }  // extern "C"

@@ -24,6 +24,9 @@ DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("counter", "<u8"
                        ("len", "<u4"), ("key_slot", "<u4")])
 
 # per-packet status = WireGuardError index + 1 (neptun/src/noise/errors.rs:4-28)
+KEY_SLOT_NO_SESSION = 0xFFFFFFFF       # include/neptun_gpu.h WG_KEY_SLOT_NO_SESSION
+KEY_SLOT_INVALID_PACKET = 0xFFFFFFFE   # WG_KEY_SLOT_INVALID_PACKET
+
 STATUS = {
     0: "Ok", 1: "DestinationBufferTooSmall", 2: "IncorrectPacketLength", 3: "UnexpectedPacket",
     4: "WrongPacketType", 5: "WrongIndex", 6: "WrongKey", 7: "InvalidTai64nTimestamp",
@@ -109,6 +112,20 @@ class GpuContext:
         """Permutation grouping packets by length, longest first (device counting sort)."""
         check(self._lib.wg_gpu_plan_batch(self._h, 1 if seal else 0, _ptr(descs), n, _ptr(order),
                                           _ptr(scratch), _stream(stream)), "wg_gpu_plan_batch")
+
+    def route_set(self, receiver_idx, key_slot) -> None:
+        """Replace the device receiver_idx -> key slot table (host arrays)."""
+        r = np.ascontiguousarray(receiver_idx, np.uint32)
+        k = np.ascontiguousarray(key_slot, np.uint32)
+        if r.shape != k.shape:
+            raise ValueError("receiver_idx and key_slot must have the same length")
+        check(self._lib.wg_gpu_route_set(self._h, len(r), r.ctypes.data, k.ctypes.data),
+              "wg_gpu_route_set")
+
+    def route_batch(self, descs, n: int, src, stream=None) -> None:
+        """Fill descs[i].key_slot from each datagram's receiver index (device)."""
+        check(self._lib.wg_gpu_route_batch(self._h, _ptr(descs), n, _ptr(src), _stream(stream)),
+              "wg_gpu_route_batch")
 
     def seal_batch_ordered(self, descs, order, n: int, src, dst, status, stream=None) -> None:
         check(self._lib.wg_gpu_seal_batch_ordered(self._h, _ptr(descs), _ptr(order), n, _ptr(src),

@@ -451,3 +451,73 @@ def test_strided_every_tail_shape(torch_cuda, gpu, P):
     got = back.cpu().numpy().reshape(n, S)
     assert np.array_equal(got[:, 16:16 + P], src.reshape(n, S)[:, 16:16 + P])
     assert (got[:, :16] == 0xCD).all() and (got[:, 16 + P:] == 0xCD).all()
+
+
+def test_device_routing_then_open_matches_oracle(torch_cuda, gpu):
+    """Raw inbound datagrams -> wg_gpu_route_batch (receiver_idx -> key slot on the device,
+    device/mod.rs:1022-1024 + noise/mod.rs:550-556) -> open: same plaintext and status as
+    the oracle; unknown receivers are NoCurrentSession, non-DATA messages InvalidPacket."""
+    import random
+    from neptun_amd.gpu import KEY_SLOT_INVALID_PACKET, KEY_SLOT_NO_SESSION
+    torch = torch_cuda
+    rng = random.Random(11)
+    n_sess, first = 40, 1000
+    locals_ = rng.sample(range(1, 2**32), n_sess)
+    keys = np.frombuffer(rng.randbytes(32 * n_sess), np.uint8).reshape(n_sess, 32)
+    gpu.set_keys(first, keys, np.array(locals_, np.uint32))
+    gpu.route_set(np.array(locals_, np.uint32), np.arange(first, first + n_sess, dtype=np.uint32))
+    items, want_slot, want = [], [], []
+    for _ in range(600):
+        r = rng.random()
+        j = rng.randrange(n_sess)
+        P = rng.choice([0, 1, 15, 16, 17, 64, 576, 1350, rng.randrange(0, 1500)])
+        pt = rng.randbytes(P)
+        if r < 0.8:
+            d = o.format_packet_data(bytes(keys[j]), locals_[j], rng.getrandbits(64), pt)
+            if rng.random() < 0.05:
+                d = bytearray(d)
+                d[-1] ^= 1
+                d = bytes(d)
+            items.append(d)
+            want_slot.append(first + j)
+            want.append(o.receive_packet_data(bytes(keys[j]), locals_[j], d))
+        elif r < 0.9:
+            unknown = rng.getrandbits(32)
+            while unknown in locals_:
+                unknown = rng.getrandbits(32)
+            items.append(o.format_packet_data(bytes(keys[j]), unknown, 1, pt))
+            want_slot.append(KEY_SLOT_NO_SESSION)
+            want.append((14, b""))
+        else:
+            kind = rng.randrange(3)
+            d = (struct_le(1) + rng.randbytes(144) if kind == 0 else
+                 struct_le(4) + rng.randbytes(rng.randrange(0, 28)) if kind == 1 else
+                 struct_le(7) + rng.randbytes(60))
+            items.append(d)
+            want_slot.append(KEY_SLOT_INVALID_PACKET)
+            want.append((13, b""))
+    src, offs = pack(items)
+    descs = np.zeros(len(items), DESC)
+    descs["src_off"] = offs
+    descs["dst_off"] = np.array(offs) + 16
+    descs["len"] = [len(x) for x in items]
+    descs["key_slot"] = 7  # overwritten by the router
+    d_descs = to_dev(torch, descs.view(np.uint8))
+    d_src = to_dev(torch, src)
+    gpu.route_batch(d_descs, len(items), d_src)
+    torch.cuda.synchronize()
+    routed = d_descs.cpu().numpy().view(DESC)
+    assert list(routed["key_slot"]) == want_slot
+    d_dst = torch.zeros(len(src), dtype=torch.uint8, device="cuda")
+    d_st = torch.full((len(items),), -1, dtype=torch.int32, device="cuda")
+    gpu.open_batch(d_descs, len(items), d_src, d_dst, d_st)
+    torch.cuda.synchronize()
+    st, out = d_st.cpu().numpy(), d_dst.cpu().numpy()
+    for i, (ws, wpt) in enumerate(want):
+        assert st[i] == ws, (i, st[i], ws)
+        if ws == 0:
+            assert out[offs[i] + 16:offs[i] + 16 + len(wpt)].tobytes() == wpt
+
+
+def struct_le(v):
+    return int(v).to_bytes(4, "little")
