@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Host-resident rate of the batched Tunn data plane (include/neptun_tunn.h).
+
+One peer pair: Tunn A encapsulates N IPv4 packets of P bytes (host buffers, one
+call), Tunn B decapsulates the datagrams (replay window, validation, stats).
+This is the drop-in path a NepTUN device would call per batch: host memcpy into
+pinned staging, H2D, AEAD kernel, D2H, host copy-out, sequential replay /
+truncation pass.  Prints one JSON line per batch size.
+
+    python tools/bench_tunn.py [--sizes 4096,65536] [--P 1350] [--reps 9]
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+
+    import neptun_amd
+    from neptun_amd.tunn import TunnResult, _bind
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="1024,16384,65536")
+    ap.add_argument("--P", type=int, default=1350)
+    ap.add_argument("--reps", type=int, default=9)
+    a = ap.parse_args()
+    P = a.P
+    ctx = neptun_amd.GpuContext(0, key_slots=64)
+    lib = _bind(ctx._lib)
+    ta, tb = neptun_amd.Tunn(ctx, 0), neptun_amd.Tunn(ctx, 16)
+    rng = np.random.default_rng(7)
+    k1, k2 = rng.integers(0, 256, 32, np.uint8).tobytes(), rng.integers(0, 256, 32, np.uint8).tobytes()
+    ta.install_session(21, 34, k2, k1, True)
+    tb.install_session(34, 21, k1, k2, True)
+    for n in [int(x) for x in a.sizes.split(",")]:
+        S = (P + 32 + 63) // 64 * 64
+        src = rng.integers(0, 256, n * S, np.uint8)
+        v = src.reshape(n, S)
+        v[:, 0] = 0x45
+        v[:, 2] = P >> 8
+        v[:, 3] = P & 255
+        wire = np.zeros(n * S, np.uint8)
+        back = np.zeros(n * S, np.uint8)
+        offs = np.arange(n, dtype=np.uint64) * S
+        src_p = (src.ctypes.data + offs).astype(np.uint64)
+        wire_p = (wire.ctypes.data + offs).astype(np.uint64)
+        back_p = (back.ctypes.data + offs).astype(np.uint64)
+        lens = np.full(n, P, np.uint32)
+        wlens = np.full(n, P + 32, np.uint32)
+        caps = np.full(n, S, np.uint32)
+        res = (TunnResult * n)()
+        vp = ctypes.c_void_p
+        te, td = [], []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            rc = lib.wg_tunn_encapsulate_batch(ta._h, n, vp(src_p.ctypes.data), vp(lens.ctypes.data),
+                                               vp(wire_p.ctypes.data), vp(caps.ctypes.data), res)
+            t1 = time.perf_counter()
+            assert rc == 0 and res[0].kind == 2 and res[n - 1].len == P + 32
+            rc = lib.wg_tunn_decapsulate_batch(tb._h, n, vp(wire_p.ctypes.data), vp(wlens.ctypes.data),
+                                               vp(back_p.ctypes.data), vp(caps.ctypes.data), res)
+            t2 = time.perf_counter()
+            assert rc == 0 and res[0].kind == 3 and res[n - 1].len == P, (res[0].kind, res[0].status)
+            te.append(t1 - t0)
+            td.append(t2 - t1)
+        ok = bool(np.array_equal(back.reshape(n, S)[:, :P], v[:, :P]))
+        e, d = statistics.median(te), statistics.median(td)
+        print(json.dumps({"packets": n, "P": P, "verified": ok,
+                          "encap_ms": round(e * 1e3, 3), "decap_ms": round(d * 1e3, 3),
+                          "encap_gbps": round(n * P * 8 / e / 1e9, 1),
+                          "decap_gbps": round(n * P * 8 / d / 1e9, 1),
+                          "roundtrip_gbps": round(n * P * 8 / (e + d) / 1e9, 1),
+                          "mpps_roundtrip": round(n / (e + d) / 1e6, 3)}), flush=True)
+    ta.close()
+    tb.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/tunn
+timeout -k 10 600 python tools/bench_tunn.py "$@" > gpurun_out/tunn/bench.jsonl 2> gpurun_out/tunn/bench.err; rc=$?; cat gpurun_out/tunn/bench.jsonl; tail -3 gpurun_out/tunn/bench.err; exit $rc
