@@ -184,6 +184,16 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint3
   const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 64u * stride);
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
   const uint32_t hi = Ranges<kSeal>::in_hi(g.W);
+  if (kRun * r >= Ranges<kSeal>::in_lo() && kRun * r + kRun <= hi && (kSeal || g.dead == 0)) {
+    // interior round (wave-uniform test): every lane moves a full chunk, the
+    // per-lane offsets are round-independent -- no range checks
+    const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16, (j & 1u) ? v1 : v0,
+                                               8u * j * stride + kRun * r, 0, 0);
+    return;
+  }
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
@@ -203,6 +213,17 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, 64u * stride);
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ (lane >> 4), k1 = k0 ^ 4u;
   const uint32_t hi = Ranges<kSeal>::out_hi(g.W);
+  if (kRun * r >= Ranges<kSeal>::out_lo() && kRun * r + kRun <= hi && (kSeal || g.dead == 0)) {
+    // interior round: 8 full-chunk stores at round-independent per-lane offsets
+    const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j) {
+      const uint4 v = run[64u * j + lane];
+      const u32x4 vv = {v.x, v.y, v.z, v.w};
+      __builtin_amdgcn_raw_buffer_store_b128(vv, rs, (j & 1u) ? v1 : v0, 8u * j * stride + kRun * r, 0);
+    }
+    return;
+  }
   bool partial = false;
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
