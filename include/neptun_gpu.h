@@ -141,7 +141,9 @@ uint32_t wg_gpu_ctx_key_slots(const wg_gpu_ctx *ctx);
 int wg_gpu_set_keys(wg_gpu_ctx *ctx, uint32_t first_slot, uint32_t n, const uint8_t *keys,
                     const uint32_t *indices, void *stream);
 
-/* Batch seal / open over device-resident descriptors (see wg_packet_desc). */
+/* Batch seal / open over device-resident descriptors (see wg_packet_desc).
+ * src / dst may be NULL: the descriptor offsets are then absolute device
+ * addresses (e.g. of mapped, registered host memory). */
 int wg_gpu_seal_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
                       const uint8_t *src, uint8_t *dst, int32_t *status, void *stream);
 int wg_gpu_open_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
@@ -181,6 +183,18 @@ int wg_gpu_seal_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
 int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_slot,
                         const uint8_t *src, uint64_t src_stride, uint8_t *dst,
                         uint64_t dst_stride, int32_t *status, void *stream);
+
+/*
+ * Host memory registration (hipHostRegister, mapped) for copy-free batches:
+ * the kernels can then address the caller's buffers directly (absolute
+ * device addresses in descriptors with NULL src / dst bases, or the Tunn
+ * direct path in neptun_tunn.h).  Ranges must not overlap; wg_gpu_ctx_destroy
+ * releases any left.  wg_gpu_unregister_host waits for the device first.
+ */
+int wg_gpu_register_host(wg_gpu_ctx *ctx, void *base, uint64_t bytes);
+int wg_gpu_unregister_host(wg_gpu_ctx *ctx, void *base);
+/* device address of registered host memory [host, host + bytes): 0 on success */
+int wg_gpu_host_device_address(wg_gpu_ctx *ctx, const void *host, uint64_t bytes, uint64_t *dev);
 
 /*
  * Inbound routing on the device.  NepTUN routes a DATA

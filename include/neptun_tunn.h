@@ -81,6 +81,15 @@ int wg_tunn_install_session(wg_tunn *t, uint32_t local_index, uint32_t peer_inde
                             const uint8_t receiving_key[32], const uint8_t sending_key[32],
                             int make_current);
 int wg_tunn_stats(const wg_tunn *t, uint64_t *tx_bytes, uint64_t *rx_bytes);
+
+/* Direct (copy-free) batches: when the caller's buffers are registered with
+ * wg_gpu_register_host (include/neptun_gpu.h) and every packet of an
+ * encapsulate batch has 16-byte-aligned src and dst inside registered ranges,
+ * the AEAD kernel reads the plaintext from and writes the datagram to the
+ * caller's buffers directly over PCIe (no staging copies); decapsulate /
+ * decrypt batches read registered datagrams directly (their plaintext is still
+ * staged: the replay decision that gates the write to dst comes after the
+ * GPU).  Results are identical either way. */
 /* sending counter of the current session / replay state of a ring slot (for tests) */
 int wg_tunn_session_counters(const wg_tunn *t, uint32_t ring_slot, uint64_t *sending_counter,
                              wg_replay *window);

@@ -52,6 +52,9 @@ def load() -> ctypes.CDLL:
     L.wg_gpu_plan_batch.argtypes = [vp, c.c_int, vp, u32, vp, vp, vp]
     for fn in (L.wg_gpu_seal_batch_ordered, L.wg_gpu_open_batch_ordered):
         fn.argtypes = [vp, vp, vp, u32, vp, vp, vp, vp]
+    L.wg_gpu_register_host.argtypes = [vp, vp, u64]
+    L.wg_gpu_unregister_host.argtypes = [vp, vp]
+    L.wg_gpu_host_device_address.argtypes = [vp, vp, u64, c.POINTER(u64)]
     L.wg_gpu_route_set.argtypes = [vp, u32, vp, vp]
     L.wg_gpu_route_batch.argtypes = [vp, vp, u32, vp, vp]
     L.wg_gpu_pipe_create.argtypes = [vp, u64, u32, c.POINTER(vp)]

@@ -25,6 +25,10 @@ struct wg_gpu_ctx {
   uint32_t *d_key_index = nullptr; // key_slots
   uint2 *d_route = nullptr;        // receiver_idx -> key slot (wg_route.hip), 2^route_bits
   uint32_t route_bits = 0;
+  struct Range {
+    uint64_t host, bytes, dev;
+  };
+  std::vector<Range> reg;          // registered host memory, sorted by host address
   std::mutex mu;                   // serialises key-table and route-table updates
 };
 
@@ -65,9 +69,31 @@ struct DeviceGuard {
 
 }  // namespace
 
-// shared with wg_pipe.cpp
+// shared with wg_pipe.cpp / wg_tunn.cpp
 int wg_pipe_fail(int rc, const char *what, hipError_t e) { return fail(rc, what, e); }
 int wg_ctx_device(const wg_gpu_ctx *ctx) { return ctx->device; }
+// snapshot of the registered ranges as (host, bytes, dev) triples, sorted by host
+void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  out.clear();
+  for (const auto &r : ctx->reg) {
+    out.push_back(r.host);
+    out.push_back(r.bytes);
+    out.push_back(r.dev);
+  }
+}
+// device address of host [p, p + n) if it lies inside one registered range
+bool wg_ctx_dev_addr(wg_gpu_ctx *ctx, const void *p, uint64_t n, uint64_t *dev) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  auto it = std::upper_bound(ctx->reg.begin(), ctx->reg.end(), a,
+                             [](uint64_t x, const wg_gpu_ctx::Range &r) { return x < r.host; });
+  if (it == ctx->reg.begin()) return false;
+  --it;
+  if (a + n > it->host + it->bytes) return false;
+  *dev = it->dev + (a - it->host);
+  return true;
+}
 
 extern "C" {
 
@@ -108,6 +134,7 @@ int wg_gpu_ctx_destroy(wg_gpu_ctx *ctx) {
   (void)hipFree(ctx->d_keys);
   (void)hipFree(ctx->d_key_index);
   (void)hipFree(ctx->d_route);
+  for (const auto &r : ctx->reg) (void)hipHostUnregister(reinterpret_cast<void *>(r.host));
   delete ctx;
   return WG_RC_OK;
 }
@@ -137,8 +164,8 @@ int wg_gpu_set_keys(wg_gpu_ctx *ctx, uint32_t first_slot, uint32_t n, const uint
 static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
                        const uint32_t *order, uint32_t n, const uint8_t *src, uint8_t *dst,
                        int32_t *status, void *stream) {
-  if (!ctx || (n && (!descs || !src || !dst || !status)))
-    return fail(WG_RC_INVALID_ARGUMENT, "batch: null argument");
+  // src / dst may be NULL: descriptor offsets are then absolute device addresses
+  if (!ctx || (n && (!descs || !status))) return fail(WG_RC_INVALID_ARGUMENT, "batch: null argument");
   if (n == 0) return WG_RC_OK;
   DeviceGuard g(ctx->device);
   wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, order, src, dst, status, n,
@@ -241,6 +268,52 @@ int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
                         uint64_t dst_stride, int32_t *status, void *stream) {
   return launch_strided(ctx, false, n, len, key_slot, 0, src, src_stride, dst, dst_stride, status,
                         stream);
+}
+
+int wg_gpu_register_host(wg_gpu_ctx *ctx, void *base, uint64_t bytes) {
+  if (!ctx || !base || !bytes) return fail(WG_RC_INVALID_ARGUMENT, "register_host: bad argument");
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  for (const auto &r : ctx->reg)
+    if (a < r.host + r.bytes && r.host < a + bytes)
+      return fail(WG_RC_INVALID_ARGUMENT, "register_host: overlaps a registered range");
+  DeviceGuard g(ctx->device);
+  WG_HIP(hipHostRegister(base, bytes, hipHostRegisterMapped), "register_host: hipHostRegister");
+  void *dev = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&dev, base, 0);
+  if (e != hipSuccess) {
+    (void)hipHostUnregister(base);
+    return fail(WG_RC_HIP_ERROR, "register_host: device pointer", e);
+  }
+  const wg_gpu_ctx::Range r{a, bytes, reinterpret_cast<uint64_t>(dev)};
+  ctx->reg.insert(std::upper_bound(ctx->reg.begin(), ctx->reg.end(), r,
+                                   [](const wg_gpu_ctx::Range &x, const wg_gpu_ctx::Range &y) {
+                                     return x.host < y.host;
+                                   }),
+                  r);
+  return WG_RC_OK;
+}
+
+int wg_gpu_unregister_host(wg_gpu_ctx *ctx, void *base) {
+  if (!ctx || !base) return fail(WG_RC_INVALID_ARGUMENT, "unregister_host: bad argument");
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  for (auto it = ctx->reg.begin(); it != ctx->reg.end(); ++it)
+    if (it->host == a) {
+      DeviceGuard g(ctx->device);
+      WG_HIP(hipDeviceSynchronize(), "unregister_host: sync");  // no batch may still use it
+      WG_HIP(hipHostUnregister(base), "unregister_host: hipHostUnregister");
+      ctx->reg.erase(it);
+      return WG_RC_OK;
+    }
+  return fail(WG_RC_INVALID_ARGUMENT, "unregister_host: not registered");
+}
+
+int wg_gpu_host_device_address(wg_gpu_ctx *ctx, const void *host, uint64_t bytes, uint64_t *dev) {
+  if (!ctx || !host || !dev) return fail(WG_RC_INVALID_ARGUMENT, "host_device_address: null argument");
+  if (!wg_ctx_dev_addr(ctx, host, bytes, dev))
+    return fail(WG_RC_INVALID_ARGUMENT, "host_device_address: not inside a registered range");
+  return WG_RC_OK;
 }
 
 int wg_gpu_route_set(wg_gpu_ctx *ctx, uint32_t n, const uint32_t *receiver_idx,

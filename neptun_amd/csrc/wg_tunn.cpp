@@ -35,6 +35,7 @@
 
 int wg_pipe_fail(int rc, const char *what, hipError_t e);  // wg_gpu.cpp
 int wg_ctx_device(const wg_gpu_ctx *ctx);                   // wg_gpu.cpp
+void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out);  // wg_gpu.cpp
 
 // ---------------------------------------------------------------------------
 // replay window: ReceivingKeyCounterValidator, session.rs:40-157
@@ -280,6 +281,8 @@ struct wg_tunn {
   std::vector<uint32_t> sel, slot;
   std::vector<uint64_t> off;  // staging offset of each selected packet inside its chunk
   std::vector<Chunk> chunks;
+  std::vector<uint64_t> dsrc, ddst;  // per selected packet: device addresses (direct mode)
+  std::vector<uint64_t> reg;         // registered ranges (host, bytes, dev), snapshot per batch
 };
 
 namespace {
@@ -316,15 +319,34 @@ inline void set_err(wg_tunn_result &r, int32_t st) {
   r.status = st;
 }
 
+// device address of [p, p + n) inside memory registered with wg_gpu_register_host
+// (t->reg: the batch's snapshot of the context's ranges)
+bool dev_addr(const wg_tunn *t, const void *p, uint64_t n, uint64_t &dev) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  size_t lo = 0, hi = t->reg.size() / 3;  // first range with host > a
+  while (lo < hi) {
+    const size_t mid = (lo + hi) / 2;
+    if (t->reg[3 * mid] <= a) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo == 0) return false;
+  const uint64_t *r = &t->reg[3 * (lo - 1)];
+  if (a + n > r[0] + r[1]) return false;
+  dev = r[2] + (a - r[0]);
+  return true;
+}
+
+
 // cut the selected packets (staging size `size(k)` each) into pipeline chunks
 template <class SizeFn>
-void make_chunks(wg_tunn *t, SizeFn size) {
+void make_chunks(wg_tunn *t, SizeFn size, size_t limit = 0) {
+  if (!limit) limit = chunk_bytes();
   t->chunks.clear();
   t->off.resize(t->sel.size());
   size_t k0 = 0, bytes = 0;
   for (size_t k = 0; k < t->sel.size(); ++k) {
     const uint64_t b = size(k);
-    if (bytes && bytes + b > chunk_bytes()) {
+    if (bytes && bytes + b > limit) {
       t->chunks.push_back(Chunk{k0, k, bytes});
       k0 = k;
       bytes = 0;
@@ -354,13 +376,23 @@ bool zero_copy() {
   }();
   return v;
 }
+
+// direct mode is possible at all: zero-copy kernels and some registered memory
+bool direct_possible(wg_tunn *t) {
+  if (!zero_copy()) return false;
+  wg_ctx_reg_snapshot(t->ctx, t->reg);
+  return !t->reg.empty();
+}
 bool trace_on() {
   static const bool v = std::getenv("WG_TUNN_TRACE") != nullptr;
   return v;
 }
 
+// abs_src / abs_dst: descriptors carry absolute device addresses of registered
+// caller memory on that side (no staging bytes there)
 template <class Pack, class Unpack>
-int run_chunks(wg_tunn *t, bool seal, Pack pack, Unpack unpack) {
+int run_chunks(wg_tunn *t, bool seal, Pack pack, Unpack unpack, bool abs_src = false,
+               bool abs_dst = false) {
   const size_t nc = t->chunks.size();
   const bool tr = trace_on();
   const double t0 = tr ? now_us() : 0.0;
@@ -385,17 +417,19 @@ int run_chunks(wg_tunn *t, bool seal, Pack pack, Unpack unpack) {
     const Chunk &ch = t->chunks[c];
     const size_t m = ch.k1 - ch.k0;
     const double pa = tr ? now_us() : 0.0;
-    TUNN_HIP(reserve(S, ch.bytes + 128, m), "tunn: staging");
+    TUNN_HIP(reserve(S, (abs_src && abs_dst) ? 128 : ch.bytes + 128, m), "tunn: staging");
     const double pb = tr ? now_us() : 0.0;
     pack(ch, S);
     if (tr)
       std::fprintf(stderr, "tunn %s chunk %zu: %zu B reserve %.0f us, pack %.0f us (t=%.0f)\n",
                    seal ? "seal" : "open", c, ch.bytes, pb - pa, now_us() - pb, now_us() - t0);
     if (zero_copy()) {
-      const int rc = seal ? wg_gpu_seal_batch(t->ctx, S.h_desc, (uint32_t)m, S.h_in, S.h_out,
-                                              S.h_st, S.stream)
-                          : wg_gpu_open_batch(t->ctx, S.h_desc, (uint32_t)m, S.h_in, S.h_out,
-                                              S.h_st, S.stream);
+      const uint8_t *in = abs_src ? nullptr : S.h_in;
+      uint8_t *out = abs_dst ? nullptr : S.h_out;
+      const int rc = seal ? wg_gpu_seal_batch(t->ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
+                                              S.stream)
+                          : wg_gpu_open_batch(t->ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
+                                              S.stream);
       if (rc) return rc;
     } else {
       TUNN_HIP(hipMemcpyAsync(S.d_in, S.h_in, ch.bytes, hipMemcpyHostToDevice, S.stream), "tunn: H2D");
@@ -475,14 +509,27 @@ template <class Decide>
 int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *len,
                   uint8_t *const *dst, Decide decide) {
   make_chunks(t, [&](size_t k) { return round128(len[t->sel[k]]); });
+  // direct input: every datagram 16-byte aligned inside registered memory
+  bool direct = direct_possible(t);
+  t->dsrc.resize(t->sel.size());
+  for (size_t k = 0; direct && k < t->sel.size(); ++k) {
+    const uint32_t i = t->sel[k];
+    direct = (reinterpret_cast<uint64_t>(datagram[i]) & 15u) == 0 &&
+             dev_addr(t, datagram[i], len[i], t->dsrc[k]);
+  }
   std::vector<uint8_t> action;
   auto pack = [&](const Chunk &ch, Staging &S) {
     t->pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
       for (size_t kk = lo; kk < hi; ++kk) {
         const size_t k = ch.k0 + kk;
         const uint32_t i = t->sel[k];
-        std::memcpy(S.h_in + t->off[k], datagram[i], len[i]);
-        S.h_desc[kk] = wg_packet_desc{t->off[k], t->off[k] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
+        if (direct) {
+          // dst is staging: the replay decision comes after the GPU (session.rs:279-300)
+          S.h_desc[kk] = wg_packet_desc{t->dsrc[k], t->off[k] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
+        } else {
+          std::memcpy(S.h_in + t->off[k], datagram[i], len[i]);
+          S.h_desc[kk] = wg_packet_desc{t->off[k], t->off[k] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
+        }
       }
     });
   };
@@ -501,7 +548,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       }
     });
   };
-  return run_chunks(t, false, pack, unpack);
+  return run_chunks(t, false, pack, unpack, direct, false);
 }
 
 }  // namespace
@@ -625,14 +672,31 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   if (t->sel.empty()) return WG_RC_OK;
   const uint64_t ctr0 = s.sending_counter;  // one fetch_add per batch (session.rs:219)
   s.sending_counter += t->sel.size();
-  make_chunks(t, [&](size_t k) { return round128((uint64_t)src_len[t->sel[k]] + WG_DATA_OVERHEAD_SZ); });
+  // direct mode: src and dst of every packet 16-byte aligned inside registered
+  // memory -> the kernel reads the caller's plaintext and writes the caller's
+  // datagram over PCIe, no host copies at all (and, no staging, one launch)
+  bool direct = direct_possible(t);
+  t->dsrc.resize(t->sel.size());
+  t->ddst.resize(t->sel.size());
+  for (size_t k = 0; direct && k < t->sel.size(); ++k) {
+    const uint32_t i = t->sel[k];
+    direct = ((reinterpret_cast<uint64_t>(src[i]) | reinterpret_cast<uint64_t>(dst[i])) & 15u) == 0 &&
+             dev_addr(t, src[i], src_len[i], t->dsrc[k]) &&
+             dev_addr(t, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, t->ddst[k]);
+  }
+  make_chunks(t, [&](size_t k) { return round128((uint64_t)src_len[t->sel[k]] + WG_DATA_OVERHEAD_SZ); },
+              direct ? ~size_t(0) : 0);
   auto pack = [&](const Chunk &ch, Staging &S) {
     t->pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
       for (size_t kk = lo; kk < hi; ++kk) {
         const size_t k = ch.k0 + kk;
         const uint32_t i = t->sel[k];
-        std::memcpy(S.h_in + t->off[k] + WG_DATA_OFFSET, src[i], src_len[i]);  // NepTUN slot layout
-        S.h_desc[kk] = wg_packet_desc{t->off[k] + WG_DATA_OFFSET, t->off[k], ctr0 + k, src_len[i], slot};
+        if (direct) {
+          S.h_desc[kk] = wg_packet_desc{t->dsrc[k], t->ddst[k], ctr0 + k, src_len[i], slot};
+        } else {
+          std::memcpy(S.h_in + t->off[k] + WG_DATA_OFFSET, src[i], src_len[i]);  // NepTUN slot layout
+          S.h_desc[kk] = wg_packet_desc{t->off[k] + WG_DATA_OFFSET, t->off[k], ctr0 + k, src_len[i], slot};
+        }
       }
     });
   };
@@ -646,7 +710,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
           continue;
         }
         // the whole dst[..P+32]: header, ciphertext, tag (dst[16..] held src before)
-        std::memcpy(dst[i], S.h_out + S.h_desc[kk].dst_off, w);
+        if (!direct) std::memcpy(dst[i], S.h_out + S.h_desc[kk].dst_off, w);
         std::memset(&res[i], 0, sizeof res[i]);
         res[i].kind = WG_TUNN_WRITE_TO_NETWORK;
         res[i].len = w;
@@ -655,7 +719,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
     for (size_t kk = 0; kk < ch.k1 - ch.k0; ++kk)  // mod.rs:321
       if (S.h_st[kk] == WG_STATUS_OK) t->tx_bytes += src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
   };
-  return run_chunks(t, true, pack, unpack);
+  return run_chunks(t, true, pack, unpack, direct, direct);
 }
 
 int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,

@@ -113,6 +113,19 @@ class GpuContext:
         check(self._lib.wg_gpu_plan_batch(self._h, 1 if seal else 0, _ptr(descs), n, _ptr(order),
                                           _ptr(scratch), _stream(stream)), "wg_gpu_plan_batch")
 
+    def register_host(self, addr: int, nbytes: int) -> None:
+        """Register caller host memory (address, size) for copy-free batches."""
+        check(self._lib.wg_gpu_register_host(self._h, addr, nbytes), "wg_gpu_register_host")
+
+    def unregister_host(self, addr: int) -> None:
+        check(self._lib.wg_gpu_unregister_host(self._h, addr), "wg_gpu_unregister_host")
+
+    def host_device_address(self, addr: int, nbytes: int) -> int:
+        dev = ctypes.c_uint64()
+        check(self._lib.wg_gpu_host_device_address(self._h, addr, nbytes, ctypes.byref(dev)),
+              "wg_gpu_host_device_address")
+        return dev.value
+
     def route_set(self, receiver_idx, key_slot) -> None:
         """Replace the device receiver_idx -> key slot table (host arrays)."""
         r = np.ascontiguousarray(receiver_idx, np.uint32)

@@ -94,6 +94,27 @@ class Tunn:
                                                 send_key, 1 if make_current else 0),
               "wg_tunn_install_session")
 
+    def _batch_ptrs(self, fn, name, src_ptrs, src_lens, dst_ptrs, dst_caps):
+        """Batch over raw addresses (numpy uint64 / uint32 arrays); returns the results."""
+        n = len(src_ptrs)
+        res = (TunnResult * n)()
+        vp = ctypes.c_void_p
+        check(fn(self._h, n, vp(src_ptrs.ctypes.data), vp(src_lens.ctypes.data),
+                 vp(dst_ptrs.ctypes.data), vp(dst_caps.ctypes.data), res), name)
+        return [(r.kind, r.status, r.len, r.ip_version, bytes(r.src_ip)) for r in res]
+
+    def encapsulate_ptrs(self, src_ptrs, src_lens, dst_ptrs, dst_caps):
+        return self._batch_ptrs(self._lib.wg_tunn_encapsulate_batch, "wg_tunn_encapsulate_batch",
+                                src_ptrs, src_lens, dst_ptrs, dst_caps)
+
+    def decapsulate_ptrs(self, src_ptrs, src_lens, dst_ptrs, dst_caps):
+        return self._batch_ptrs(self._lib.wg_tunn_decapsulate_batch, "wg_tunn_decapsulate_batch",
+                                src_ptrs, src_lens, dst_ptrs, dst_caps)
+
+    def decrypt_ptrs(self, src_ptrs, src_lens, dst_ptrs, dst_caps):
+        return self._batch_ptrs(self._lib.wg_tunn_decrypt_batch, "wg_tunn_decrypt_batch",
+                                src_ptrs, src_lens, dst_ptrs, dst_caps)
+
     def stats(self):
         tx, rx = ctypes.c_uint64(), ctypes.c_uint64()
         check(self._lib.wg_tunn_stats(self._h, ctypes.byref(tx), ctypes.byref(rx)), "wg_tunn_stats")

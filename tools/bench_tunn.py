@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--sizes", default="1024,16384,65536")
     ap.add_argument("--P", type=int, default=1350)
     ap.add_argument("--reps", type=int, default=9)
+    ap.add_argument("--register", action="store_true",
+                    help="register the packet buffers (direct, copy-free batches)")
     a = ap.parse_args()
     P = a.P
     ctx = neptun_amd.GpuContext(0, key_slots=64)
@@ -55,6 +57,9 @@ def main():
         lens = np.full(n, P, np.uint32)
         wlens = np.full(n, P + 32, np.uint32)
         caps = np.full(n, S, np.uint32)
+        if a.register:
+            for arr in (src, wire, back):
+                ctx.register_host(arr.ctypes.data, arr.nbytes)
         res = (TunnResult * n)()
         vp = ctypes.c_void_p
         te, td = [], []
@@ -71,8 +76,11 @@ def main():
             te.append(t1 - t0)
             td.append(t2 - t1)
         ok = bool(np.array_equal(back.reshape(n, S)[:, :P], v[:, :P]))
+        if a.register:
+            for arr in (src, wire, back):
+                ctx.unregister_host(arr.ctypes.data)
         e, d = statistics.median(te), statistics.median(td)
-        print(json.dumps({"packets": n, "P": P, "verified": ok,
+        print(json.dumps({"packets": n, "P": P, "registered": a.register, "verified": ok,
                           "encap_ms": round(e * 1e3, 3), "decap_ms": round(d * 1e3, 3),
                           "encap_gbps": round(n * P * 8 / e / 1e9, 1),
                           "decap_gbps": round(n * P * 8 / d / 1e9, 1),
