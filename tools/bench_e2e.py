@@ -65,6 +65,30 @@ def main():
             if ok and (best is None or line["roundtrip_gbps"] > best["roundtrip_gbps"]):
                 best = line
             pipe.close()
+    # zero-copy: the strided kernels address the pinned host buffers directly
+    # (torch pin_memory = mapped hipHostMalloc memory), reads and writes share PCIe
+    ts, to = [], []
+    for _ in range(reps + 1):
+        back.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.seal_strided(n, P, 0, 0, pt.data_ptr() + 16, S, wire.data_ptr(), S, st.data_ptr())
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ctx.open_strided(n, P + 32, 0, wire.data_ptr(), S, back.data_ptr() + 16, S, st.data_ptr())
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ts.append(t1 - t0); to.append(t2 - t1)
+    ts, to = ts[1:], to[1:]
+    ok = torch.equal(back.view(n, S)[:, 16:16 + P], pt.view(n, S)[:, 16:16 + P]) and int(st.abs().sum()) == 0
+    ms, mo = statistics.median(ts), statistics.median(to)
+    zc = {"mode": "zero-copy (kernel on pinned host memory)", "verified": bool(ok),
+          "seal_ms": round(ms * 1e3, 3), "open_ms": round(mo * 1e3, 3),
+          "seal_gbps": round(n * P * 8 / ms / 1e9, 1), "open_gbps": round(n * P * 8 / mo / 1e9, 1),
+          "roundtrip_gbps": round(n * P * 8 / (ms + mo) / 1e9, 1)}
+    print(json.dumps(zc), flush=True)
+    if ok and zc["roundtrip_gbps"] > best["roundtrip_gbps"]:
+        best = zc
     print(json.dumps({"best": best, "packets": n, "packet_bytes": P,
                       "note": "host-resident: pinned host in -> GPU -> pinned host out"}), flush=True)
 
