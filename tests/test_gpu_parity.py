@@ -521,3 +521,49 @@ def test_device_routing_then_open_matches_oracle(torch_cuda, gpu):
 
 def struct_le(v):
     return int(v).to_bytes(4, "little")
+
+
+def test_jumbo_and_extreme_lengths_match_oracle(torch_cuda, gpu):
+    """Descriptor path at the length extremes: empty, sub-chunk, MTU, jumbo and the
+    largest IPv4 datagram payload (the planner clamps >= 255 rounds into one bin)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(3)
+    sizes = [0, 1, 15, 16, 17, 8900, 9000, 32768, 65503, 65535 - 32]
+    keys = synth.keys(2, seed=4)
+    gpu.set_keys(0, keys, np.array([11, 22], np.uint32))
+    items = [rng.integers(0, 256, s, np.uint8).tobytes() for s in sizes]
+    src, offs = pack(items, pad=48)
+    descs = np.zeros(len(items), DESC)
+    for i, s in enumerate(sizes):
+        descs[i] = (offs[i], offs[i], (1 << 63) + i, s, i & 1)
+    # seal into a separate buffer at the same offsets (+16 B headroom per slot)
+    out, st = run_desc(torch, gpu, True, descs, src, len(src) + 64)
+    assert (st == 0).all()
+    want = np.zeros_like(out)
+    assert (o.seal_batch(descs, keys, np.array([11, 22], np.uint32), src, want) == 0).all()
+    for i, s in enumerate(sizes):
+        assert out[offs[i]:offs[i] + s + 32].tobytes() == want[offs[i]:offs[i] + s + 32].tobytes(), s
+    opn = descs.copy()
+    opn["len"] = np.array(sizes) + 32
+    opn["dst_off"] = np.array(offs) + 16
+    back, st = run_desc(torch, gpu, False, opn, out, len(out) + 64)
+    assert (st == 0).all()
+    for i, s in enumerate(sizes):
+        assert back[offs[i] + 16:offs[i] + 16 + s].tobytes() == items[i]
+
+
+def test_argument_validation_fails_loudly(torch_cuda, gpu):
+    """Bad arguments are rejected by the ABI (no launch) with a message."""
+    import neptun_amd
+    torch = torch_cuda
+    buf = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(neptun_amd.NeptunGpuError, match="16-byte aligned"):
+        gpu.seal_strided(64, 100, 0, 0, buf.data_ptr() + 4, 256, buf, 256)
+    with pytest.raises(neptun_amd.NeptunGpuError, match="bad key slot"):
+        gpu.seal_strided(64, 100, 1 << 20, 0, buf, 256, buf, 256)
+    with pytest.raises(neptun_amd.NeptunGpuError, match="slot range"):
+        gpu.set_keys(4095, synth.keys(2), np.array([1, 2], np.uint32))
+    with pytest.raises(neptun_amd.NeptunGpuError, match="duplicate receiver"):
+        gpu.route_set(np.array([5, 5], np.uint32), np.array([0, 1], np.uint32))
+    with pytest.raises(neptun_amd.NeptunGpuError, match="outside the key table"):
+        gpu.route_set(np.array([5], np.uint32), np.array([1 << 20], np.uint32))
