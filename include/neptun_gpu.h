@@ -185,6 +185,34 @@ int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
                         uint64_t dst_stride, int32_t *status, void *stream);
 
 /*
+ * Handshake-side crypto, batched.  Device pointers,
+ * asynchronous on `stream`.
+ *   wg_gpu_x25519_batch: out[i] = X25519(scalars[i], points[i]) (RFC 7748;
+ *     x25519-dalek's StaticSecret::diffie_hellman / PublicKey::from with the
+ *     base point 9), 32 bytes each, no rejection of all-zero results (neither
+ *     does the reference).
+ *   wg_gpu_handshake_anon_batch: for n handshake initiations (148 bytes each,
+ *     `stride` apart, stride % 4 == 0) the responder-side work before the peer
+ *     is known: the mac1 check of RateLimiter::verify_packet
+ *     (rate_limiter.rs:187-195, when check_mac1 != 0) and parse_handshake_anon
+ *     (noise/handshake.rs:367-412).  out[i] gets the sender index and the
+ *     initiator's static public key (HalfHandshake) or a status:
+ *     WG_STATUS_WRONG_PACKET_TYPE, WG_STATUS_INVALID_MAC, WG_STATUS_INVALID_AEAD_TAG.
+ *     static_private (32 bytes) is HOST memory.
+ */
+typedef struct wg_half_handshake {
+  uint32_t peer_index;
+  int32_t status;
+  uint8_t peer_static_public[32];
+} wg_half_handshake;
+
+int wg_gpu_x25519_batch(wg_gpu_ctx *ctx, uint32_t n, const uint8_t *scalars, const uint8_t *points,
+                        uint8_t *out, void *stream);
+int wg_gpu_handshake_anon_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32], uint32_t n,
+                                const uint8_t *msgs, uint64_t stride, int check_mac1,
+                                wg_half_handshake *out, void *stream);
+
+/*
  * Host memory registration (hipHostRegister, mapped) for copy-free batches:
  * the kernels can then address the caller's buffers directly (absolute
  * device addresses in descriptors with NULL src / dst bases, or the Tunn

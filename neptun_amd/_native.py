@@ -55,6 +55,8 @@ def load() -> ctypes.CDLL:
     L.wg_gpu_register_host.argtypes = [vp, vp, u64]
     L.wg_gpu_unregister_host.argtypes = [vp, vp]
     L.wg_gpu_host_device_address.argtypes = [vp, vp, u64, c.POINTER(u64)]
+    L.wg_gpu_x25519_batch.argtypes = [vp, u32, vp, vp, vp, vp]
+    L.wg_gpu_handshake_anon_batch.argtypes = [vp, c.c_char_p, u32, vp, u64, c.c_int, vp, vp]
     L.wg_gpu_route_set.argtypes = [vp, u32, vp, vp]
     L.wg_gpu_route_batch.argtypes = [vp, vp, u32, vp, vp]
     L.wg_gpu_pipe_create.argtypes = [vp, u64, u32, c.POINTER(vp)]

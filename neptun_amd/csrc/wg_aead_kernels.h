@@ -52,4 +52,19 @@ __host__ __device__ inline uint32_t route_hash(uint32_t x, uint32_t bits) {
 __global__ void route_kernel(wg_packet_desc *descs, uint32_t n, const uint8_t *src,
                              const uint2 *table, uint32_t bits);
 
+
+// wg_handshake.hip
+struct HandshakeAnonParams {
+  const uint8_t *msgs;  // n handshake initiations, 148 bytes each at `stride`
+  uint64_t stride;
+  wg_half_handshake *out;
+  uint32_t n, check_mac1;
+  uint32_t static_private[8];  // responder static key (wave-uniform)
+  uint32_t hash0[8];           // HASH(INITIAL_CHAIN_HASH || static_public)
+  uint32_t mac1_key[8];        // HASH(LABEL_MAC1 || static_public)
+};
+__global__ void x25519_kernel(uint32_t n, const uint8_t *scalars, const uint8_t *points,
+                              uint8_t *out);
+__global__ void handshake_anon_kernel(HandshakeAnonParams prm);
+
 }  // namespace wg

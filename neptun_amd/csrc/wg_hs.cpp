@@ -1,0 +1,97 @@
+// wg_hs.cpp -- C ABI of the batched handshake kernels (include/neptun_gpu.h).
+// The wave-uniform inputs of handshake_anon_kernel are derived here on the
+// host with the same header code the kernel uses.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "neptun_gpu.h"
+#include "wg_aead_kernels.h"
+#include "wg_blake2s.h"
+#include "wg_x25519.h"
+
+int wg_pipe_fail(int rc, const char *what, hipError_t e);  // wg_gpu.cpp
+int wg_ctx_device(const wg_gpu_ctx *ctx);                   // wg_gpu.cpp
+
+namespace {
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// INITIAL_CHAIN_HASH = HASH(HASH(CONSTRUCTION) || IDENTIFIER) (handshake.rs:29-39)
+void initial_chain_hash(uint32_t out[8]) {
+  static const char kConstruction[] = "Noise_IKpsk2_25519_ChaChaPoly_BLAKE2s";  // 37 bytes
+  static const char kIdentifier[] = "WireGuard v1 zx2c4 Jason@zx2c4.com";       // 34 bytes
+  uint32_t m[16] = {0}, ck[8];
+  std::memcpy(m, kConstruction, 37);
+  wg::b2s::hash_block(ck, m, 37);
+  // 66 bytes: ck || IDENTIFIER[0..32) as one block, IDENTIFIER[32..34) as the last
+  std::memcpy(m, ck, 32);
+  std::memcpy(reinterpret_cast<uint8_t *>(m) + 32, kIdentifier, 32);
+  wg::b2s::init(out, 32, 0);
+  wg::b2s::compress(out, m, 64, false);
+  std::memset(m, 0, sizeof m);
+  std::memcpy(m, kIdentifier + 32, 2);
+  wg::b2s::compress(out, m, 66, true);
+}
+}  // namespace
+
+extern "C" {
+
+int wg_gpu_x25519_batch(wg_gpu_ctx *ctx, uint32_t n, const uint8_t *scalars, const uint8_t *points,
+                        uint8_t *out, void *stream) {
+  if (!ctx || (n && (!scalars || !points || !out)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "x25519_batch: null argument", hipSuccess);
+  if (((uintptr_t)scalars | (uintptr_t)points | (uintptr_t)out) & 15u)
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "x25519_batch: pointers must be 16-byte aligned",
+                        hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::x25519_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, scalars, points, out);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK : wg_pipe_fail(WG_RC_HIP_ERROR, "x25519_batch: launch", e);
+}
+
+int wg_gpu_handshake_anon_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32], uint32_t n,
+                                const uint8_t *msgs, uint64_t stride, int check_mac1,
+                                wg_half_handshake *out, void *stream) {
+  if (!ctx || !static_private || (n && (!msgs || !out)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "handshake_anon_batch: null argument", hipSuccess);
+  if (stride < 148 || (stride & 3u) || ((uintptr_t)msgs & 3u))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT,
+                        "handshake_anon_batch: stride >= 148 and 4-byte alignment required", hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  wg::HandshakeAnonParams prm{};
+  prm.msgs = msgs;
+  prm.stride = stride;
+  prm.out = out;
+  prm.n = n;
+  prm.check_mac1 = check_mac1 ? 1u : 0u;
+  std::memcpy(prm.static_private, static_private, 32);
+  // static_public = X25519(static_private, 9); hash0 = HASH(INITIAL_CHAIN_HASH || static_public);
+  // mac1_key = HASH(LABEL_MAC1 || static_public) (rate_limiter.rs:67)
+  uint32_t base[8] = {9, 0, 0, 0, 0, 0, 0, 0}, pub[8], ich[8];
+  wg::x25519::scalarmult(pub, prm.static_private, base);
+  initial_chain_hash(ich);
+  wg::b2s::hash64(prm.hash0, ich, pub);
+  uint32_t m[16] = {0};
+  std::memcpy(m, "mac1----", 8);
+  std::memcpy(reinterpret_cast<uint8_t *>(m) + 8, pub, 32);
+  wg::b2s::hash_block(prm.mac1_key, m, 40);
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::handshake_anon_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), prm);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK
+                         : wg_pipe_fail(WG_RC_HIP_ERROR, "handshake_anon_batch: launch", e);
+}
+
+}  // extern "C"

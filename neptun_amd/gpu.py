@@ -27,6 +27,9 @@ DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("counter", "<u8"
 KEY_SLOT_NO_SESSION = 0xFFFFFFFF       # include/neptun_gpu.h WG_KEY_SLOT_NO_SESSION
 KEY_SLOT_INVALID_PACKET = 0xFFFFFFFE   # WG_KEY_SLOT_INVALID_PACKET
 
+HALF_HANDSHAKE_DTYPE = np.dtype([("peer_index", "<u4"), ("status", "<i4"),
+                                 ("peer_static_public", "u1", (32,))])  # wg_half_handshake
+
 STATUS = {
     0: "Ok", 1: "DestinationBufferTooSmall", 2: "IncorrectPacketLength", 3: "UnexpectedPacket",
     4: "WrongPacketType", 5: "WrongIndex", 6: "WrongKey", 7: "InvalidTai64nTimestamp",
@@ -125,6 +128,19 @@ class GpuContext:
         check(self._lib.wg_gpu_host_device_address(self._h, addr, nbytes, ctypes.byref(dev)),
               "wg_gpu_host_device_address")
         return dev.value
+
+    def x25519_batch(self, n: int, scalars, points, out, stream=None) -> None:
+        """out[i] = X25519(scalars[i], points[i]), 32-byte rows on the device."""
+        check(self._lib.wg_gpu_x25519_batch(self._h, n, _ptr(scalars), _ptr(points), _ptr(out),
+                                            _stream(stream)), "wg_gpu_x25519_batch")
+
+    def handshake_anon_batch(self, static_private: bytes, n: int, msgs, stride: int, out,
+                             check_mac1: bool = True, stream=None) -> None:
+        """mac1 check + parse_handshake_anon for n initiations (device); out: HALF_HANDSHAKE_DTYPE."""
+        check(self._lib.wg_gpu_handshake_anon_batch(self._h, bytes(static_private), n, _ptr(msgs),
+                                                    stride, 1 if check_mac1 else 0, _ptr(out),
+                                                    _stream(stream)),
+              "wg_gpu_handshake_anon_batch")
 
     def route_set(self, receiver_idx, key_slot) -> None:
         """Replace the device receiver_idx -> key slot table (host arrays)."""

@@ -72,3 +72,41 @@ int ossl_receive_packet_data(const uint8_t key[32], const uint8_t *datagram, int
   int p = len - 32;
   return ossl_aead_open(key, nonce, NULL, 0, datagram + 16, p, datagram + 16 + p, out);
 }
+
+/* Per-thread X25519 context for the CPU baseline: the private key and the
+ * peer key object are created once, the peer's raw public value is replaced per
+ * call (EVP_PKEY_new_raw_* per call serialises threads on provider locks). */
+typedef struct {
+  EVP_PKEY *priv, *peer;
+  EVP_PKEY_CTX *ctx;
+} x25519_thread;
+static __thread x25519_thread t_x;
+
+int ossl_x25519_fast(uint8_t out[32], const uint8_t scalar[32], const uint8_t point[32]) {
+  if (!t_x.priv) {
+    t_x.priv = EVP_PKEY_new_raw_private_key(EVP_PKEY_X25519, NULL, scalar, 32);
+    t_x.peer = EVP_PKEY_new_raw_public_key(EVP_PKEY_X25519, NULL, point, 32);
+    t_x.ctx = t_x.priv ? EVP_PKEY_CTX_new(t_x.priv, NULL) : NULL;
+    if (!t_x.ctx || EVP_PKEY_derive_init(t_x.ctx) <= 0) return -1;
+  }
+  if (EVP_PKEY_set1_encoded_public_key(t_x.peer, point, 32) <= 0) return -1;
+  size_t len = 32;
+  if (EVP_PKEY_derive_set_peer(t_x.ctx, t_x.peer) <= 0) return -1;
+  return EVP_PKEY_derive(t_x.ctx, out, &len) > 0 && len == 32 ? 0 : -1;
+}
+
+/* X25519 (RFC 7748) through OpenSSL's EVP_PKEY -- an independent check of
+ * oracle/handshake_model.py and the CPU baseline of the handshake kernels.
+ * Returns 0, or -1 when OpenSSL refuses (it rejects an all-zero shared secret). */
+int ossl_x25519(uint8_t out[32], const uint8_t scalar[32], const uint8_t point[32]) {
+  EVP_PKEY *priv = EVP_PKEY_new_raw_private_key(EVP_PKEY_X25519, NULL, scalar, 32);
+  EVP_PKEY *peer = EVP_PKEY_new_raw_public_key(EVP_PKEY_X25519, NULL, point, 32);
+  EVP_PKEY_CTX *c = priv ? EVP_PKEY_CTX_new(priv, NULL) : NULL;
+  size_t len = 32;
+  int ok = c && peer && EVP_PKEY_derive_init(c) > 0 && EVP_PKEY_derive_set_peer(c, peer) > 0 &&
+           EVP_PKEY_derive(c, out, &len) > 0 && len == 32;
+  EVP_PKEY_CTX_free(c);
+  EVP_PKEY_free(peer);
+  EVP_PKEY_free(priv);
+  return ok ? 0 : -1;
+}

@@ -77,6 +77,7 @@ def openssl() -> ctypes.CDLL:
         L.ossl_aead_open.argtypes = [u8p, u8p, u8p, c.c_int, u8p, c.c_int, u8p, c.c_void_p]
         L.ossl_format_packet_data.argtypes = [u8p, c.c_uint32, c.c_uint64, u8p, c.c_int, c.c_void_p]
         L.ossl_receive_packet_data.argtypes = [u8p, u8p, c.c_int, c.c_void_p]
+        L.ossl_x25519.argtypes = [c.c_void_p, u8p, u8p]
         _ossl = L
     return _ossl
 
@@ -150,3 +151,9 @@ def open_batch(descs: np.ndarray, keys: np.ndarray, key_index: np.ndarray, src: 
                                    key_index.ctypes.data, src.ctypes.data, dst.ctypes.data,
                                    status.ctypes.data)
     return status
+
+
+def openssl_x25519(scalar: bytes, point: bytes) -> bytes | None:
+    """X25519 through OpenSSL (None when OpenSSL rejects an all-zero result)."""
+    out = ctypes.create_string_buffer(32)
+    return None if openssl().ossl_x25519(out, scalar, point) else out.raw
