@@ -229,6 +229,20 @@ def load_traffic(kernel: str, config: int) -> dict | None:
     return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
 
 
+def load_valu(kernel: str, config: int) -> dict | None:
+    """VALU-side PMC summary (tools/pmc_valu.py) of the same kernel: the bound that
+    actually limits it."""
+    path = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if config != 2 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        k = json.load(f).get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    return {"valu_busy_frac": k["valu_issue_frac"], "valu_instr_per_wave": k["valu_per_wave"],
+            "clock_GHz_profiled": k["clock_GHz"], "source": "profiles/pmc_valu.json"}
+
+
 def run(args, factory=None, device_fn=None):
     """Bench body.  `factory`/`device_fn` are injection points for the CPU tests
     of the multi-rank path (tests/test_bench_dist.py); production uses HIP."""
@@ -290,6 +304,7 @@ def run(args, factory=None, device_fn=None):
         dom = "seal" if avg["seal"] >= avg["open"] else "open"
         achieved = wl.launch_bytes[dom] / (avg[dom] * 1e-3) / 1e9
         tr = load_traffic(wl.kernels[dom], args.config)
+        valu = load_valu(wl.kernels[dom], args.config)
         line = {
             "metric": METRIC if args.config == 2 else
             f"Gbit/s device-resident ChaCha20-Poly1305 seal+open, BASELINE config {args.config}",
@@ -315,6 +330,8 @@ def run(args, factory=None, device_fn=None):
                 "traffic": tr["bytes_per_launch"] if tr else None,
                 "traffic_source": tr["source"] if tr else None,
                 "algorithmic_bytes_per_launch": wl.launch_bytes[dom],
+                # what limits the kernel: VALU issue (96 % busy), not HBM -- DESIGN.md 3
+                "compute": valu,
             },
             "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
             "seal_gbps": round(wl.payload_bytes * 8 / (avg["seal"] * 1e-3) / 1e9, 1),
