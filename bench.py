@@ -255,6 +255,8 @@ def run(args, factory=None, device_fn=None):
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     if device_fn is None:
+        # one rank per GPU; more ranks than GPUs (a rehearsal on a smaller box) share them
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         stream = torch.cuda.current_stream(dev)
