@@ -40,7 +40,7 @@ namespace wg {
 
 constexpr uint32_t kRun = 128;    // bytes of one packet per round (one cache line)
 constexpr uint32_t kChunks = 8;   // 16-byte chunks per run
-constexpr uint32_t kWaves = kBlockThreads / 64;
+constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 
 // timing-only ablations (wrong outputs): skip the HBM traffic / skip the crypto
 #ifndef WG_ABLATE_NO_MEM
@@ -63,6 +63,25 @@ constexpr uint32_t kBufs = WG_PREFETCH ? 2 : 1;
 #define WG_REG_PREFETCH 0  // 1: uniform path loads round r+1 into VGPRs during round r
 #endif
 
+// Diagnostic build only (-DWG_STAMP=1): s_memtime at the phase boundaries of
+// the phase-locked loop, wave 0 of every workgroup, read back with
+// wg_gpu_debug_stamps() (tools/stamps.py).  Never part of the product build.
+#ifndef WG_STAMP
+#define WG_STAMP 0
+#endif
+#if WG_STAMP
+constexpr int kStampBlocks = 4096, kStampRounds = 16, kStampPhases = 6;
+__device__ uint64_t g_stamps[2][kStampBlocks][kStampRounds][kStampPhases];
+#define WG_STAMP_AT(seal, r, ph)                                                              \
+  do {                                                                                      \
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0 && lane == 0 &&                \
+        blockIdx.x < kStampBlocks && (r) < kStampRounds)                                    \
+      g_stamps[seal][blockIdx.x][r][ph] = __builtin_amdgcn_s_memtime();                     \
+  } while (0)
+#else
+#define WG_STAMP_AT(seal, r, ph) do {} while (0)
+#endif
+
 // LDS of one wave.  Generic geometry: one 8 KiB run buffer + per-packet tables.
 struct WaveStage {
   uint4 run[1][64 * kChunks];  // [buffer][packet][chunk ^ swz(packet)], 8 KiB
@@ -70,10 +89,12 @@ struct WaveStage {
   uint64_t out_base[64];       // wire-coordinate origin of the output side
   uint32_t wlen[64];           // W = datagram length (P + 32)
   uint32_t nruns[64];          // rounds this packet takes part in; 0 = none
+  uint4 park[64];              // per-packet Poly1305 "s" half of the one-time key
 };
 // Uniform geometry: kBufs run buffers, no tables (addresses are arithmetic).
 struct WaveStageUniform {
   uint4 run[kBufs][64 * kChunks];
+  uint4 park[64];  // per-packet Poly1305 "s" (parked here: VGPRs are the scarce resource)
 };
 
 // XOR swizzle of a packet's 8 chunk slots: lane L reading chunk k of its own
@@ -355,6 +376,41 @@ __device__ __forceinline__ void crypt_round(uint4 *run, uint32_t lane, uint32_t 
   }
 }
 
+// The same round with both keystream blocks computed beforehand
+// (chacha20_block2_sync(ka, kb, key, 2r + 1, ...)): chunk 0 (keystream saved
+// from the previous round), then chunks 1-7.
+template <bool kSeal>
+__device__ __forceinline__ void apply_chunk0(uint4 *run, uint32_t lane, uint32_t r, uint32_t P,
+                                             Poly &p, const uint32_t ks_save[4]) {
+  const int m0 = (int)(kRun * r) - 16;
+  if (r > 0 && m0 < (int)P)
+    crypt_chunk<kSeal>(run[8u * lane + (0u ^ swz(lane))], p, m0, P, ks_save[0], ks_save[1],
+                       ks_save[2], ks_save[3]);
+}
+
+template <bool kSeal>
+__device__ __forceinline__ void apply_blocks(uint4 *run, uint32_t lane, uint32_t r, uint32_t P,
+                                             const uint32_t (&ka)[16], const uint32_t (&kb)[16],
+                                             Poly &p, uint32_t ks_save[4]) {
+  const int m0 = (int)(kRun * r) - 16;
+  const uint32_t row = 8u * lane, sw = swz(lane);
+#pragma unroll
+  for (int k = 1; k <= 4; ++k) {
+    const int m = m0 + 16 * k;
+    if (m < (int)P)
+      crypt_chunk<kSeal>(run[row + ((uint32_t)k ^ sw)], p, m, P, ka[4 * k - 4], ka[4 * k - 3],
+                         ka[4 * k - 2], ka[4 * k - 1]);
+  }
+#pragma unroll
+  for (int k = 5; k <= 7; ++k) {
+    const int m = m0 + 16 * k;
+    if (m < (int)P)
+      crypt_chunk<kSeal>(run[row + ((uint32_t)k ^ sw)], p, m, P, kb[4 * k - 20], kb[4 * k - 19],
+                         kb[4 * k - 18], kb[4 * k - 17]);
+  }
+  ks_save[0] = kb[12]; ks_save[1] = kb[13]; ks_save[2] = kb[14]; ks_save[3] = kb[15];
+}
+
 // 32 bytes starting at the tail chunk: k ciphertext bytes then the 16-byte tag
 __device__ __forceinline__ void tail_words(const uint32_t (&ct)[4], const uint32_t (&tag)[4], int q,
                                            uint32_t out[8]) {
@@ -374,10 +430,11 @@ struct PacketJob {
 // The owner lane's side of a packet: everything but the cooperative memory
 // moves.  kUniform = every lane of the wave is live with the same length
 // (strided batches); then P, W and the round count are wave-uniform.
-template <bool kSeal, bool kUniform, class Stage, class Geom>
+template <bool kSeal, bool kUniform, bool kSync, class Stage, class Geom>
 __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
                                          int32_t *status_out) {
+  static_assert(!kSync || kUniform, "phase-locked steps need workgroup-uniform control flow");
   // ---- per-packet setup (owner lane) ------------------------------------
   uint32_t W = 0, P = 0;
   if (kUniform || job.status == WG_STATUS_OK) {
@@ -413,18 +470,18 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   }
 
   Poly poly;
-  uint32_t s[4] = {0, 0, 0, 0}, ks_save[4] = {0, 0, 0, 0};
+  uint32_t ks_save[4] = {0, 0, 0, 0};
   uint32_t n1 = (uint32_t)job.counter, n2 = (uint32_t)(job.counter >> 32);
   const uint32_t q = P & 15u;                    // bytes in the partial ciphertext chunk
   const uint32_t wt = 16u + (P & ~15u);          // wire offset of the tail chunk
   uint32_t tailB[4] = {0, 0, 0, 0};              // seal: chunk after the tail chunk (tag rest)
-  uint32_t rx[8] = {0, 0, 0, 0, 0, 0, 0, 0};     // open: raw bytes [wt, wt + 32)
+  uint32_t tg[4] = {0, 0, 0, 0};                 // open: the received tag, bytes [W - 16, W)
 
   auto one_time_key = [&]() {
     uint32_t ks[16];
     chacha20_block(ks, key, 0u, n1, n2);  // RFC 8439 2.6: block 0 -> r | s
     poly_init(poly, ks);
-    s[0] = ks[4]; s[1] = ks[5]; s[2] = ks[6]; s[3] = ks[7];
+    S.park[lane] = make_uint4(ks[4], ks[5], ks[6], ks[7]);  // s, read back for the tag
   };
   if (kSeal && my_runs) one_time_key();  // overlaps the first DMA
 
@@ -445,101 +502,175 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     for (uint32_t j = 0; j < kChunks; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, rs, kNoAccess, 16u * j, 0);
   }
 #endif
-  for (uint32_t r = 0; r < rounds; ++r) {
-    uint4 *run = S.run[kPrefetch ? (r & 1u) : 0u];
+  // open, round 0: the datagram header (noise/mod.rs:170-180) decides the
+  // packet's fate and supplies the nonce counter
+  auto open_header = [&](const uint4 h) {
+    if (h.x != WG_MSG_DATA) job.status = WG_STATUS_INVALID_PACKET;
+    else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
+    if (job.status != WG_STATUS_OK) {
+      my_runs = 0;  // nothing of this packet is stored
+      if constexpr (!kUniform) S.nruns[lane] = 0;
+    } else {
+      n1 = h.z;
+      n2 = h.w;
+      one_time_key();
+    }
+    if constexpr (kUniform) g.dead = __ballot(job.status != WG_STATUS_OK);
+  };
+  // open: collect the received tag before the slots are decrypted in place.
+  // It is bytes [q, q + 16) of the 32 raw bytes [wt, wt + 32), which sit in
+  // two chunks (possibly two rounds); each chunk contributes its bytes (the
+  // other half read as zero) and the parts are OR-ed together.
+  auto open_keep_tail = [&](uint4 *run, uint32_t r) {
+    const uint32_t row = 8u * lane, sw = swz(lane);
+    const uint32_t ra = wt >> 7, rb = (wt + 16u) >> 7;
+    if (ra == r) {
+      const uint4 v = run[row + (((wt >> 4) & 7u) ^ sw)];
+      const uint32_t w[8] = {v.x, v.y, v.z, v.w, 0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tg[j] |= bytes_at(w, (int)q + 4 * j);
+    }
+    if (q && rb == r) {
+      const uint4 v = run[row + ((((wt + 16u) >> 4) & 7u) ^ sw)];
+      const uint32_t w[8] = {0u, 0u, 0u, 0u, v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tg[j] |= bytes_at(w, (int)q + 4 * j);
+    }
+  };
+  // seal: place the tag (and the tag bytes that spill into the next round)
+  auto seal_tail = [&](uint4 *run, uint32_t r) {
+    const uint32_t row = 8u * lane, sw = swz(lane);
+    if (r > 0 && ((wt + 16u) >> 7) == r && (wt >> 7) == r - 1u && q) {
+      // tag remainder spilled into this round's first chunk
+      run[row + (0u ^ sw)] = make_uint4(tailB[0], tailB[1], tailB[2], tailB[3]);
+    }
+    if ((wt >> 7) == r) {
+      // all ciphertext is MACed: LE64(aad_len=0) | LE64(ct_len), then the tag
+      poly_block(poly, 0u, 0u, P, 0u);
+      uint32_t tag[4];
+      const uint4 sp = S.park[lane];
+      const uint32_t s[4] = {sp.x, sp.y, sp.z, sp.w};
+      poly_finish(poly, s, tag);
+      const uint32_t ka = (wt >> 4) & 7u;
+      uint32_t ct[4] = {0, 0, 0, 0};
+      if (q) {
+        const uint4 v = run[row + (ka ^ sw)];
+        ct[0] = v.x; ct[1] = v.y; ct[2] = v.z; ct[3] = v.w;
+      }
+      uint32_t w8[8];
+      tail_words(ct, tag, (int)q, w8);
+      run[row + (ka ^ sw)] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
+      tailB[0] = w8[4]; tailB[1] = w8[5]; tailB[2] = w8[6]; tailB[3] = w8[7];
+      if (q && ka < 7u) run[row + ((ka + 1u) ^ sw)] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
+    }
+  };
+
+  if constexpr (kSync) {
+    // Phase-locked path (workgroup-uniform control flow, one LDS stage per
+    // wave): the round's DMA is issued first and its two keystream blocks are
+    // computed while it is in flight -- the keystream does not depend on the
+    // data.  Only open's round 0 has to wait first: the nonce is in the header.
+    uint4 *run = S.run[0];
+    // open: each lane fetches its own header ahead of round 0's DMA, so the
+    // round-0 keystream waits for 16 bytes, not for the whole stage
+    // (round 0's DMA is issued before the loop so the header is consumed, and
+    // its registers freed, before the loop body)
+    if (rounds) {
+      uint4 hdr = make_uint4(0u, 0u, 0u, 0u);
+      if (!kSeal) hdr = ld16(reinterpret_cast<const uint8_t *>(job.in_base));
 #if !WG_ABLATE_NO_MEM
-    if constexpr (kRegPf) {
-      commit_regs(run, pre, lane);
-      if (r + 1u < rounds) load_regs<kSeal>(pre, g, lane, r + 1u);
-    } else if constexpr (kPrefetch) {
-      if (r + 1u < rounds) {
-        stage_in<kSeal>(S.run[(r + 1u) & 1u], g, lane, r + 1u);
-        // everything older than round r+1's 8 loads is done (round r's DMA)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      stage_in<kSeal>(run, g, lane, 0);
+#endif
+      if (!kSeal && my_runs) open_header(hdr);
+    }
+    for (uint32_t r = 0; r < rounds; ++r) {
+      WG_STAMP_AT(kSeal, r, 0);
+#if !WG_ABLATE_NO_MEM
+      if (r > 0) stage_in<kSeal>(run, g, lane, r);
+#endif
+      WG_STAMP_AT(kSeal, r, 1);
+      auto landed = [&]() {
+        lds_wait_dma();
+        WG_STAMP_AT(kSeal, r, 3);
+        if (!kSeal && my_runs) open_keep_tail(run, r);
+        if (kSeal && r == 0)  // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
+          run[8u * lane + (0u ^ swz(lane))] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
+      };
+      if ((int)(kRun * r) < (int)P && !WG_ABLATE_NO_CRYPT) {  // workgroup-uniform
+        // the keystream lives only inside this branch (kept out of phis, the
+        // compiler would otherwise carry it as a register tuple and spill it)
+        uint32_t ka[16], kb[16];
+        chacha20_block2_sync(ka, kb, key, 2u * r + 1u, n1, n2);
+        WG_STAMP_AT(kSeal, r, 2);
+        landed();
+        if (my_runs) {
+          apply_chunk0<kSeal>(run, lane, r, P, poly, ks_save);
+          apply_blocks<kSeal>(run, lane, r, P, ka, kb, poly, ks_save);
+          if (kSeal) seal_tail(run, r);
+        }
       } else {
+        landed();
+        if (my_runs && !WG_ABLATE_NO_CRYPT) {
+          apply_chunk0<kSeal>(run, lane, r, P, poly, ks_save);
+          if (kSeal) seal_tail(run, r);
+        }
+      }
+      WG_STAMP_AT(kSeal, r, 4);
+#if !WG_ABLATE_NO_MEM
+      stage_out<kSeal>(run, g, lane, r);
+#endif
+      WG_STAMP_AT(kSeal, r, 5);
+    }
+  } else {
+    for (uint32_t r = 0; r < rounds; ++r) {
+      uint4 *run = S.run[kPrefetch ? (r & 1u) : 0u];
+#if !WG_ABLATE_NO_MEM
+      if constexpr (kRegPf) {
+        commit_regs(run, pre, lane);
+        if (r + 1u < rounds) load_regs<kSeal>(pre, g, lane, r + 1u);
+      } else if constexpr (kPrefetch) {
+        if (r + 1u < rounds) {
+          stage_in<kSeal>(S.run[(r + 1u) & 1u], g, lane, r + 1u);
+          // everything older than round r+1's 8 loads is done (round r's DMA)
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+          lds_wait_dma();
+        }
+      } else {
+        stage_in<kSeal>(run, g, lane, r);
         lds_wait_dma();
       }
-    } else {
-      stage_in<kSeal>(run, g, lane, r);
-      lds_wait_dma();
-    }
 #else
-    lds_wait_dma();
+      lds_wait_dma();
 #endif
-    if (r < my_runs) {
-      const uint32_t row = 8u * lane, sw = swz(lane);
-      if (!kSeal) {
-        if (r == 0) {
-          // header: LE32 type | LE32 receiver_idx | LE64 counter (noise/mod.rs:170-180)
-          const uint4 h = run[row + (0u ^ sw)];
-          if (h.x != WG_MSG_DATA) job.status = WG_STATUS_INVALID_PACKET;
-          else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
-          if (job.status != WG_STATUS_OK) {
-            my_runs = 0;  // nothing of this packet is stored
-            if constexpr (!kUniform) S.nruns[lane] = 0;
-          } else {
-            n1 = h.z;
-            n2 = h.w;
-            one_time_key();
-          }
-          if constexpr (kUniform) g.dead = __ballot(job.status != WG_STATUS_OK);
+      if (r < my_runs) {
+        if (!kSeal) {
+          if (r == 0) open_header(run[8u * lane + (0u ^ swz(lane))]);
+          if (my_runs) open_keep_tail(run, r);
+        } else if (r == 0) {
+          // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
+          run[8u * lane + (0u ^ swz(lane))] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
         }
-        // keep the raw tail bytes before the slots are decrypted in place
-        if (my_runs) {
-          const uint32_t ra = wt >> 7, rb = (wt + 16u) >> 7;
-          if (ra == r) {
-            const uint4 v = run[row + (((wt >> 4) & 7u) ^ sw)];
-            rx[0] = v.x; rx[1] = v.y; rx[2] = v.z; rx[3] = v.w;
-          }
-          if (q && rb == r) {
-            const uint4 v = run[row + ((((wt + 16u) >> 4) & 7u) ^ sw)];
-            rx[4] = v.x; rx[5] = v.y; rx[6] = v.z; rx[7] = v.w;
-          }
-        }
-      } else if (r == 0) {
-        // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
-        run[row + (0u ^ sw)] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
-      }
-      if (my_runs && !WG_ABLATE_NO_CRYPT) {
-        crypt_round<kSeal>(run, lane, r, P, key, n1, n2, poly, ks_save);
-        if (kSeal) {
-          if (r > 0 && ((wt + 16u) >> 7) == r && (wt >> 7) == r - 1u && q) {
-            // tag remainder spilled into this round's first chunk
-            run[row + (0u ^ sw)] = make_uint4(tailB[0], tailB[1], tailB[2], tailB[3]);
-          }
-          if ((wt >> 7) == r) {
-            // all ciphertext is MACed: LE64(aad_len=0) | LE64(ct_len), then the tag
-            poly_block(poly, 0u, 0u, P, 0u);
-            uint32_t tag[4];
-            poly_finish(poly, s, tag);
-            const uint32_t ka = (wt >> 4) & 7u;
-            uint32_t ct[4] = {0, 0, 0, 0};
-            if (q) {
-              const uint4 v = run[row + (ka ^ sw)];
-              ct[0] = v.x; ct[1] = v.y; ct[2] = v.z; ct[3] = v.w;
-            }
-            uint32_t w8[8];
-            tail_words(ct, tag, (int)q, w8);
-            run[row + (ka ^ sw)] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
-            tailB[0] = w8[4]; tailB[1] = w8[5]; tailB[2] = w8[6]; tailB[3] = w8[7];
-            if (q && ka < 7u)
-              run[row + ((ka + 1u) ^ sw)] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
-          }
+        if (my_runs && !WG_ABLATE_NO_CRYPT) {
+          crypt_round<kSeal>(run, lane, r, P, key, n1, n2, poly, ks_save);
+          if (kSeal) seal_tail(run, r);
         }
       }
-    }
 #if !WG_ABLATE_NO_MEM
-    stage_out<kSeal>(run, g, lane, r);
+      stage_out<kSeal>(run, g, lane, r);
 #endif
+    }
   }
 
   if (!kSeal && job.status == WG_STATUS_OK) {
     poly_block(poly, 0u, 0u, P, 0u);
     uint32_t tag[4];
+    const uint4 sp = S.park[lane];
+    const uint32_t s[4] = {sp.x, sp.y, sp.z, sp.w};
     poly_finish(poly, s, tag);
     uint32_t diff = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) diff |= bytes_at(rx, (int)q + 4 * j) ^ tag[j];
+    for (int j = 0; j < 4; ++j) diff |= tg[j] ^ tag[j];
     if (diff) {
       // tag mismatch: never expose unauthenticated plaintext (ring open_within
       // zeroes it); the streamed stores of this wave land first (same wave, in order)
@@ -562,15 +693,10 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 // Strided batches: kTail = false covers the whole waves [0, n & ~63) with the
 // uniform geometry; kTail = true is a one-wave launch for the n % 64 packets
 // left over (generic geometry), so the hot kernel carries no generic path.
-template <bool kSeal, bool kTail>
-__global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_strided_kernel(
-    StridedParams prm) {
-  using Stage = typename std::conditional<kTail, WaveStage, WaveStageUniform>::type;
-  __shared__ Stage stage[kWaves];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform
-  const uint32_t pkt0 = kTail ? (prm.n & ~63u) : (blockIdx.x * kWaves + wave) * 64u;
-  if (kTail ? wave != 0 : pkt0 + 64u > prm.n) return;  // wave-uniform
+// one wave's 64 packets [pkt0, pkt0 + 64) of a strided batch
+template <bool kSeal, bool kTail, class Stage>
+__device__ __forceinline__ void strided_group(Stage &stage, const StridedParams &prm,
+                                              uint32_t pkt0, uint32_t lane) {
   const uint32_t i = pkt0 + lane;
   PacketJob job;
   job.slot = prm.key_slot;
@@ -588,11 +714,37 @@ __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_strided
     const uint32_t W = kSeal ? prm.len + WG_DATA_OVERHEAD_SZ : prm.len;
     UniformGeom g{in0, out0, prm.src_stride, prm.dst_stride, 0ull, W,
                   (kSeal || prm.len >= WG_DATA_OVERHEAD_SZ) ? (W + kRun - 1) / kRun : 0u};
-    run_wave<kSeal, true>(stage[wave], g, lane, job, prm.keys, prm.key_index, st);
+    run_wave<kSeal, true, WG_SYNC != 0>(stage, g, lane, job, prm.keys, prm.key_index, st);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
-    LdsGeom g{stage[wave]};
-    run_wave<kSeal, false>(stage[wave], g, lane, job, prm.keys, prm.key_index, st);
+    LdsGeom g{stage};
+    run_wave<kSeal, false, false>(stage, g, lane, job, prm.keys, prm.key_index, st);
+  }
+}
+
+template <bool kSeal, bool kTail>
+__global__ __launch_bounds__(kTail ? kBlockThreads : kStridedThreads,
+                             kTail ? WG_WAVES_PER_SIMD : kStridedMinWaves) void
+aead_strided_kernel(StridedParams prm) {
+  using Stage = typename std::conditional<kTail, WaveStage, WaveStageUniform>::type;
+  constexpr uint32_t kWaves = (kTail ? kBlockThreads : kStridedThreads) / 64u;
+  __shared__ Stage stage[kWaves];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform
+  if constexpr (kTail) {
+    if (wave == 0) strided_group<kSeal, true>(stage[wave], prm, prm.n & ~63u, lane);
+  } else {
+    // persistent walk over workgroup-sized packet groups: the resident
+    // workgroups stay in their steady, mutually de-phased rhythm (one DMA
+    // in flight while the other computes) instead of restarting in step
+    const uint32_t groups = (prm.n / 64u + kWaves - 1u) / kWaves;
+    for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+      const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
+      // only the last group can be partial, and it is this workgroup's last
+      // iteration: a wave without packets ends (ended waves leave the barrier)
+      if (pkt0 + 64u > prm.n) return;
+      strided_group<kSeal, false>(stage[wave], prm, pkt0, lane);
+    }
   }
 }
 
@@ -628,7 +780,7 @@ __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_desc_ke
     else job.status = WG_STATUS_OK;
   }
   LdsGeom g{stage[wave]};
-  run_wave<kSeal, false>(stage[wave], g, lane, job, prm.keys, prm.key_index,
+  run_wave<kSeal, false, false>(stage[wave], g, lane, job, prm.keys, prm.key_index,
                          i < prm.n ? prm.status + idx : nullptr);
 }
 
@@ -640,3 +792,9 @@ template __global__ void aead_desc_kernel<true>(DescParams);
 template __global__ void aead_desc_kernel<false>(DescParams);
 
 }  // namespace wg
+
+#if WG_STAMP
+extern "C" int wg_gpu_debug_stamps(void *out, size_t bytes) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(wg::g_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+#endif

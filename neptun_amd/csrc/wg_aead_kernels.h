@@ -6,7 +6,25 @@
 
 namespace wg {
 
-constexpr uint32_t kBlockThreads = 256;  // 4 waves per workgroup
+constexpr uint32_t kBlockThreads = 256;  // 4 waves per workgroup (descriptor / tail kernels)
+
+// Uniform strided kernel: with WG_SYNC the ChaCha20 steps are phase-locked by
+// s_barrier (wg_crypto.h chacha20_block2_sync), which needs waves that share a
+// SIMD to be in one workgroup.  512 threads = 2 waves per SIMD per workgroup,
+// two workgroups per CU (<= 128 VGPRs): while one waits for its DMA the other
+// computes (one 1024-thread workgroup per CU exposes every round's DMA).
+#ifndef WG_SYNC
+#define WG_SYNC 1
+#endif
+#ifndef WG_STRIDED_THREADS
+#define WG_STRIDED_THREADS (WG_SYNC ? 512 : 256)
+#endif
+constexpr uint32_t kStridedThreads = WG_STRIDED_THREADS;
+constexpr uint32_t kStridedMinWaves = 4;  // __launch_bounds__ waves per SIMD: 128-VGPR cap
+#ifndef WG_STRIDED_BLOCKS_PER_CU
+#define WG_STRIDED_BLOCKS_PER_CU (4u * kStridedMinWaves * 64u / kStridedThreads)
+#endif
+constexpr uint32_t kStridedBlocksPerCU = WG_STRIDED_BLOCKS_PER_CU;
 
 struct StridedParams {
   const uint8_t *keys;        // device key table, 32 B per slot

@@ -60,6 +60,80 @@ __device__ __forceinline__ void chacha20_block(uint32_t ks[16], const uint32_t k
 }
 
 // ---------------------------------------------------------------------------
+// Two consecutive keystream blocks in phase-locked steps.
+//
+// gfx950 issues the "simple" VALU ops (v_add_u32, v_xor_b32, ...) of two waves
+// of a SIMD together, i.e. at twice the rate of v_alignbit_b32 -- but only
+// while the waves' streams run in step: once the waves drift apart, every op
+// costs the single-issue rate (tools/microbench_valu6.hip, microbench_chacha2.hip,
+// profiles/r01_microbench_valu6.txt, r01_microbench_chacha2.txt).  So the two
+// blocks' 8 quarter-rounds of a step are issued as 8 adds, 8 xors, 8 rotates,
+// and the workgroup's waves (4 per SIMD) re-align with s_barrier after every
+// step: 2375 SIMD-cycles per wave-block instead of 3840 for the compiler-
+// scheduled block function.
+//
+// Every wave of the workgroup must call this the same number of times (the
+// barriers have to match); callers guarantee that with wave-uniform control flow.
+// ---------------------------------------------------------------------------
+#define WG_STEP8_ASM(SH)                                                                  \
+  "v_add_u32 %0, %0, %16\n\tv_add_u32 %1, %1, %17\n\tv_add_u32 %2, %2, %18\n\t"           \
+  "v_add_u32 %3, %3, %19\n\tv_add_u32 %4, %4, %20\n\tv_add_u32 %5, %5, %21\n\t"           \
+  "v_add_u32 %6, %6, %22\n\tv_add_u32 %7, %7, %23\n\t"                                    \
+  "v_xor_b32 %8, %8, %0\n\tv_xor_b32 %9, %9, %1\n\tv_xor_b32 %10, %10, %2\n\t"            \
+  "v_xor_b32 %11, %11, %3\n\tv_xor_b32 %12, %12, %4\n\tv_xor_b32 %13, %13, %5\n\t"        \
+  "v_xor_b32 %14, %14, %6\n\tv_xor_b32 %15, %15, %7\n\t"                                  \
+  "v_alignbit_b32 %8, %8, %8, " #SH "\n\tv_alignbit_b32 %9, %9, %9, " #SH "\n\t"          \
+  "v_alignbit_b32 %10, %10, %10, " #SH "\n\tv_alignbit_b32 %11, %11, %11, " #SH "\n\t"    \
+  "v_alignbit_b32 %12, %12, %12, " #SH "\n\tv_alignbit_b32 %13, %13, %13, " #SH "\n\t"    \
+  "v_alignbit_b32 %14, %14, %14, " #SH "\n\tv_alignbit_b32 %15, %15, %15, " #SH "\n\t"    \
+  "s_barrier"
+// One column round and one diagonal round of both blocks (p = block blk,
+// q = block blk + 1, 16 named state words each), 4 steps per round.  Named
+// scalars, not arrays: the compiler keeps arrays that are addressed through
+// pointers in register tuples and spills them whole.
+#define WG_COLUMN_ROUND2 \
+  asm volatile(WG_STEP8_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15), "+v"(q12), "+v"(q13), "+v"(q14), "+v"(q15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7), "v"(q4), "v"(q5), "v"(q6), "v"(q7)); \
+  asm volatile(WG_STEP8_ASM(20) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(q8), "+v"(q9), "+v"(q10), "+v"(q11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15), "v"(q12), "v"(q13), "v"(q14), "v"(q15)); \
+  asm volatile(WG_STEP8_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15), "+v"(q12), "+v"(q13), "+v"(q14), "+v"(q15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7), "v"(q4), "v"(q5), "v"(q6), "v"(q7)); \
+  asm volatile(WG_STEP8_ASM(25) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(q8), "+v"(q9), "+v"(q10), "+v"(q11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15), "v"(q12), "v"(q13), "v"(q14), "v"(q15));
+#define WG_DIAGONAL_ROUND2 \
+  asm volatile(WG_STEP8_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(q15), "+v"(q12), "+v"(q13), "+v"(q14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4), "v"(q5), "v"(q6), "v"(q7), "v"(q4)); \
+  asm volatile(WG_STEP8_ASM(20) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14)); \
+  asm volatile(WG_STEP8_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(q15), "+v"(q12), "+v"(q13), "+v"(q14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4), "v"(q5), "v"(q6), "v"(q7), "v"(q4)); \
+  asm volatile(WG_STEP8_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14));
+
+// keystream blocks blk and blk+1 (same key and nonce) into ka, kb
+__device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_t (&kb)[16],
+                                                     const uint32_t k[8], uint32_t blk,
+                                                     uint32_t n1, uint32_t n2) {
+  uint32_t p0 = kSigma0, p1 = kSigma1, p2 = kSigma2, p3 = kSigma3;
+  uint32_t p4 = k[0], p5 = k[1], p6 = k[2], p7 = k[3], p8 = k[4], p9 = k[5], p10 = k[6], p11 = k[7];
+  uint32_t p12 = blk, p13 = 0, p14 = n1, p15 = n2;
+  uint32_t q0 = kSigma0, q1 = kSigma1, q2 = kSigma2, q3 = kSigma3;
+  uint32_t q4 = k[0], q5 = k[1], q6 = k[2], q7 = k[3], q8 = k[4], q9 = k[5], q10 = k[6], q11 = k[7];
+  uint32_t q12 = blk + 1u, q13 = 0, q14 = n1, q15 = n2;
+  // the first column round stays compiler-scheduled: with a wave-uniform key
+  // and counter its wave-uniform columns run on the scalar unit
+  WG_QR(p0, p4, p8, p12) WG_QR(p1, p5, p9, p13) WG_QR(p2, p6, p10, p14) WG_QR(p3, p7, p11, p15)
+  WG_QR(q0, q4, q8, q12) WG_QR(q1, q5, q9, q13) WG_QR(q2, q6, q10, q14) WG_QR(q3, q7, q11, q15)
+  __builtin_amdgcn_s_barrier();
+  WG_DIAGONAL_ROUND2
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    WG_COLUMN_ROUND2
+    WG_DIAGONAL_ROUND2
+  }
+  ka[0] = p0 + kSigma0; ka[1] = p1 + kSigma1; ka[2] = p2 + kSigma2; ka[3] = p3 + kSigma3;
+  ka[4] = p4 + k[0]; ka[5] = p5 + k[1]; ka[6] = p6 + k[2]; ka[7] = p7 + k[3];
+  ka[8] = p8 + k[4]; ka[9] = p9 + k[5]; ka[10] = p10 + k[6]; ka[11] = p11 + k[7];
+  ka[12] = p12 + blk; ka[13] = p13; ka[14] = p14 + n1; ka[15] = p15 + n2;
+  kb[0] = q0 + kSigma0; kb[1] = q1 + kSigma1; kb[2] = q2 + kSigma2; kb[3] = q3 + kSigma3;
+  kb[4] = q4 + k[0]; kb[5] = q5 + k[1]; kb[6] = q6 + k[2]; kb[7] = q7 + k[3];
+  kb[8] = q8 + k[4]; kb[9] = q9 + k[5]; kb[10] = q10 + k[6]; kb[11] = q11 + k[7];
+  kb[12] = q12 + blk + 1u; kb[13] = q13; kb[14] = q14 + n1; kb[15] = q15 + n2;
+}
+
+// ---------------------------------------------------------------------------
 // Poly1305 (RFC 8439 2.5), radix 2^32: h = h0..h3 (32-bit) + h4 (< 8)
 // ---------------------------------------------------------------------------
 struct Poly {

@@ -25,6 +25,7 @@ struct wg_gpu_ctx {
   uint32_t *d_key_index = nullptr; // key_slots
   uint2 *d_route = nullptr;        // receiver_idx -> key slot (wg_route.hip), 2^route_bits
   uint32_t route_bits = 0;
+  uint32_t cus = 0;                // compute units (persistent strided grid)
   struct Range {
     uint64_t host, bytes, dev;
   };
@@ -113,7 +114,10 @@ int wg_gpu_ctx_create(int device, uint32_t key_slots, wg_gpu_ctx **out) {
   ctx->device = device;
   ctx->key_slots = key_slots;
   DeviceGuard g(device);
-  hipError_t e = hipMalloc(&ctx->d_keys, (size_t)key_slots * 32);
+  int cus = 0;
+  hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  ctx->cus = (e == hipSuccess && cus > 0) ? (uint32_t)cus : 256u;
+  e = hipMalloc(&ctx->d_keys, (size_t)key_slots * 32);
   if (e == hipSuccess) e = hipMalloc(&ctx->d_key_index, (size_t)key_slots * 4);
   if (e == hipSuccess) e = hipMemset(ctx->d_keys, 0, (size_t)key_slots * 32);
   if (e == hipSuccess) e = hipMemset(ctx->d_key_index, 0, (size_t)key_slots * 4);
@@ -234,15 +238,18 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
   wg::StridedParams prm{ctx->d_keys, ctx->d_key_index, src, dst, status, src_stride,
                         dst_stride, counter_base, n, len, key_slot};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const uint32_t full_waves = n / 64u, waves_per_block = wg::kBlockThreads / 64u;
+  const uint32_t full_waves = n / 64u, waves_per_block = wg::kStridedThreads / 64u;
   if (full_waves) {
-    const dim3 grid((full_waves + waves_per_block - 1) / waves_per_block);
+    // persistent: kStridedBlocksPerCU resident workgroups per CU walk the
+    // workgroup-sized packet groups (wg_aead.hip aead_strided_kernel)
+    const uint32_t groups = (full_waves + waves_per_block - 1) / waves_per_block;
+    const dim3 grid(std::min(groups, ctx->cus * wg::kStridedBlocksPerCU));
     if (seal)
-      hipLaunchKernelGGL((wg::aead_strided_kernel<true, false>), grid, dim3(wg::kBlockThreads), 0,
-                         s, prm);
+      hipLaunchKernelGGL((wg::aead_strided_kernel<true, false>), grid, dim3(wg::kStridedThreads),
+                         0, s, prm);
     else
-      hipLaunchKernelGGL((wg::aead_strided_kernel<false, false>), grid, dim3(wg::kBlockThreads), 0,
-                         s, prm);
+      hipLaunchKernelGGL((wg::aead_strided_kernel<false, false>), grid, dim3(wg::kStridedThreads),
+                         0, s, prm);
   }
   if (n % 64u) {  // the last, partial wave: generic per-lane geometry
     if (seal)

@@ -8,6 +8,7 @@ instructions per wave, VALU-active fraction.  One rocprofv3 pass with
   valu_issue_frac  = 4 * SQ_ACTIVE_INST_VALU (quad-cycles) / (clock cycles * 1024 SIMDs)
 
     python tools/pmc_valu.py OUT.json [bench args...]
+    python tools/pmc_valu.py OUT.json --cmd python tools/ab.py build/variants/libX.so
 """
 import csv
 import glob
@@ -32,10 +33,14 @@ def short(name):
 
 def main():
     out, bench_args = sys.argv[1], sys.argv[2:]
-    d = os.path.join(ROOT, "gpurun_out", "pmc_valu")
+    d = os.path.join(ROOT, "gpurun_out", "pmc_valu", os.path.splitext(os.path.basename(out))[0])
+    if bench_args[:1] == ["--cmd"]:  # any command, e.g. tools/ab.py on one variant library
+        target = bench_args[1:]
+    else:
+        target = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                  "--no-cpu-baseline"] + bench_args
     cmd = ["rocprofv3", "--kernel-trace", "--pmc", *COUNTERS, "--output-format", "csv", "-d", d,
-           "-o", "pmc", "--", sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3",
-           "--warmup", "1", "--no-cpu-baseline"] + bench_args
+           "-o", "pmc", "--"] + target
     subprocess.run(cmd, check=True, env=dict(os.environ, TMPDIR="/tmp"), timeout=600,
                    stdout=subprocess.DEVNULL)
     per = defaultdict(lambda: defaultdict(float))  # (kernel, dispatch) -> counter -> value
