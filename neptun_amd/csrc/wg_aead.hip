@@ -54,6 +54,10 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
 #endif
 
+#ifndef WG_STAGGER
+#define WG_STAGGER 0  // experiment: 1 odd workgroups, 2 second half of the grid start late
+#endif
+
 #ifndef WG_PREFETCH
 #define WG_PREFETCH 0  // 1: double-buffered LDS stage (round r+1 DMA overlaps round r)
 #endif
@@ -738,6 +742,11 @@ aead_strided_kernel(StridedParams prm) {
     // workgroups stay in their steady, mutually de-phased rhythm (one DMA
     // in flight while the other computes) instead of restarting in step
     const uint32_t groups = (prm.n / 64u + kWaves - 1u) / kWaves;
+#if WG_STAGGER
+    // de-phase the workgroups that share a CU (a guess at the placement)
+    if ((WG_STAGGER == 1 ? blockIdx.x & 1u : blockIdx.x >= gridDim.x / 2u))
+      for (int i = 0; i < 16; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
     for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
       const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
       // only the last group can be partial, and it is this workgroup's last

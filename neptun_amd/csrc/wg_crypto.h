@@ -75,6 +75,9 @@ __device__ __forceinline__ void chacha20_block(uint32_t ks[16], const uint32_t k
 // Every wave of the workgroup must call this the same number of times (the
 // barriers have to match); callers guarantee that with wave-uniform control flow.
 // ---------------------------------------------------------------------------
+#ifndef WG_CHACHA_PRIO
+#define WG_CHACHA_PRIO 3  // wave priority during the phase-locked steps (0: unchanged)
+#endif
 #define WG_STEP8_ASM(SH)                                                                  \
   "v_add_u32 %0, %0, %16\n\tv_add_u32 %1, %1, %17\n\tv_add_u32 %2, %2, %18\n\t"           \
   "v_add_u32 %3, %3, %19\n\tv_add_u32 %4, %4, %20\n\tv_add_u32 %5, %5, %21\n\t"           \
@@ -117,12 +120,18 @@ __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_
   WG_QR(p0, p4, p8, p12) WG_QR(p1, p5, p9, p13) WG_QR(p2, p6, p10, p14) WG_QR(p3, p7, p11, p15)
   WG_QR(q0, q4, q8, q12) WG_QR(q1, q5, q9, q13) WG_QR(q2, q6, q10, q14) WG_QR(q3, q7, q11, q15)
   __builtin_amdgcn_s_barrier();
+#if WG_CHACHA_PRIO
+  __builtin_amdgcn_s_setprio(WG_CHACHA_PRIO);  // the phase-locked steps go first
+#endif
   WG_DIAGONAL_ROUND2
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
     WG_COLUMN_ROUND2
     WG_DIAGONAL_ROUND2
   }
+#if WG_CHACHA_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   ka[0] = p0 + kSigma0; ka[1] = p1 + kSigma1; ka[2] = p2 + kSigma2; ka[3] = p3 + kSigma3;
   ka[4] = p4 + k[0]; ka[5] = p5 + k[1]; ka[6] = p6 + k[2]; ka[7] = p7 + k[3];
   ka[8] = p8 + k[4]; ka[9] = p9 + k[5]; ka[10] = p10 + k[6]; ka[11] = p11 + k[7];
