@@ -202,6 +202,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(uint64_t base, uint3
                                            0x00020000);
 }
 
+// 16-byte buffer store with wait states after it.  The store reads its data
+// VGPRs a few cycles after issue; for a buffer store with an SGPR soffset the
+// compiler does not model that hazard and may overwrite the data registers in
+// the very next VALU instruction -- measured on MI355X: some lanes then store
+// the new values (tools/diff_variants.py found 1 % of packets corrupted in a
+// build whose register allocation did that).  The asm form keeps two wait
+// states between the store and any later write of its data registers.
+__device__ __forceinline__ void store16(u32x4 data, uint64_t base, uint32_t bytes, uint32_t voff,
+                                        uint32_t soff) {
+  const u32x4 rs = {(uint32_t)base, (uint32_t)(base >> 32) & 0xffffu, bytes, 0x00020000u};
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
+               :: "v"(data), "v"(voff), "s"(rs), "s"(soff) : "memory");
+}
+
 template <bool kSeal>
 __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint32_t lane,
                                          uint32_t r) {
@@ -245,7 +259,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
     for (uint32_t j = 0; j < kChunks; ++j) {
       const uint4 v = run[64u * j + lane];
       const u32x4 vv = {v.x, v.y, v.z, v.w};
-      __builtin_amdgcn_raw_buffer_store_b128(vv, rs, (j & 1u) ? v1 : v0, 8u * j * stride + kRun * r, 0);
+      store16(vv, g.out0, 64u * stride, (j & 1u) ? v1 : v0, 8u * j * stride + kRun * r);
     }
     return;
   }
@@ -258,9 +272,8 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
     const bool ok = !dead && w >= Ranges<kSeal>::out_lo() && w < hi;
     const uint4 v = run[64u * j + lane];
     const u32x4 vv = {v.x, v.y, v.z, v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(vv, rs, ok && hi - w >= 16u ? y * stride + 16u * k
-                                                                        : kNoAccess,
-                                           8u * j * stride + kRun * r, 0);
+    store16(vv, g.out0, 64u * stride, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
+            8u * j * stride + kRun * r);
     partial |= ok && hi - w < 16u;
   }
   if (partial) {  // the packet's last, partial chunk (last round only)
