@@ -567,3 +567,59 @@ def test_argument_validation_fails_loudly(torch_cuda, gpu):
         gpu.route_set(np.array([5, 5], np.uint32), np.array([0, 1], np.uint32))
     with pytest.raises(neptun_amd.NeptunGpuError, match="outside the key table"):
         gpu.route_set(np.array([5], np.uint32), np.array([1 << 20], np.uint32))
+
+
+def test_persistent_grid_partial_group_dropped_lanes(torch_cuda, gpu):
+    """Strided batch larger than one pass of the persistent grid (2 workgroups
+    per CU x 512 packets), ending in a partial workgroup group and a tail wave;
+    open with dropped lanes (bad type, wrong index) and forged tags scattered
+    over the waves, so the phase-locked path runs with dead lanes in many
+    workgroups.  Statuses, stored bytes and zeroing follow session.rs:265-302
+    and noise/mod.rs:139-199 (oracle spot checks)."""
+    torch = torch_cuda
+    n, P, S = 512 * 520 + 64 * 3 + 17, 1350, 1408
+    keys = synth.keys(1)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    pt = synth.device_payloads(n, P, S, "cuda", seed=11)
+    wire = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+    back = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    base = 0xFFFF_FF00  # counters cross 2^32 inside the batch
+    gpu.seal_strided(n, P, 0, base, pt, S, wire, S, st)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    rng = np.random.default_rng(5)
+    bad_type = rng.choice(n, 300, replace=False)
+    rest = np.setdiff1d(np.arange(n), bad_type)
+    wrong_idx = rng.choice(rest, 300, replace=False)
+    rest = np.setdiff1d(rest, wrong_idx)
+    forged = rng.choice(rest, 300, replace=False)
+    w = wire.view(n, S)
+    w[torch.from_numpy(bad_type).cuda(), 0] = 2
+    w[torch.from_numpy(wrong_idx).cuda(), 4] ^= 1
+    w[torch.from_numpy(forged).cuda(), P + 20] ^= 0x80   # a tag byte
+    gpu.open_strided(n, P + 32, 0, wire, S, back, S, st)
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    want = np.zeros(n, np.int32)
+    want[bad_type] = 13   # InvalidPacket
+    want[wrong_idx] = 5   # WrongIndex
+    want[forged] = 10     # InvalidAeadTag
+    assert np.array_equal(s, want)
+    b = back.view(n, S)
+    p = pt.view(n, S)
+    ok = torch.from_numpy(np.flatnonzero(want == 0)).cuda()
+    assert torch.equal(b[ok, :P], p[ok, :P])
+    # dropped packets store nothing; forged ones are zeroed (ring open_in_place)
+    assert int(b[torch.from_numpy(bad_type).cuda()].abs().sum()) == 0
+    assert int(b[torch.from_numpy(wrong_idx).cuda()].abs().sum()) == 0
+    assert int(b[torch.from_numpy(forged).cuda(), :P].abs().sum()) == 0
+    # oracle spot checks of the sealed bytes across groups, waves and the tail
+    rows = np.concatenate([np.arange(0, n, 4999), [n - 18, n - 17, n - 1]])
+    wr = w[torch.from_numpy(rows).cuda()].cpu().numpy()
+    pr = p[torch.from_numpy(rows).cuda()].cpu().numpy()
+    for r, wrow, prow in zip(rows, wr, pr):
+        if r in bad_type or r in wrong_idx or r in forged:
+            continue
+        want_w = o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, base + int(r), prow[:P].tobytes())
+        assert wrow[:P + 32].tobytes() == want_w
