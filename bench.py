@@ -141,7 +141,7 @@ class DescWorkload:
         key_bytes = 32 * b.n if self.cfg == 4 else 0  # per-lane key reads
         self.launch_bytes = {"seal": int((2 * P + 32).sum()) + key_bytes,
                              "open": int((2 * P + 32).sum()) + key_bytes}
-        self.kernels = {"seal": "aead_desc_kernel<true>", "open": "aead_desc_kernel<false>"}
+        self.kernels = {"seal": "aead_desc_sync_kernel<true>", "open": "aead_desc_sync_kernel<false>"}
 
     def step(self, stream, evs=None):
         b, ctx = self.b, self.ctx

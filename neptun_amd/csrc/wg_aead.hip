@@ -136,6 +136,51 @@ struct LdsGeom {
   __device__ uint64_t out_base(uint32_t p) const { return S.out_base[p]; }
 };
 
+// Phase-locked descriptor batches: 8 waves x (this + 1 KiB of park) must fit
+// twice in 160 KiB, so the per-packet tables are compact -- stage origins in
+// 16-byte units from base - 16 (64 GiB reach), one length word (0 = no part).
+struct WaveStageDesc {
+  uint4 run[1][64 * kChunks];
+  uint32_t in16[64], out16[64];  // wire-coordinate origins: ref + 16 * (hi:lo)
+  uint8_t in_hi[64], out_hi[64];
+  uint32_t wlen[64];             // W = datagram length; 0 = not staged
+  uint4 park[64];
+};
+
+struct DescGeom {
+  WaveStageDesc &S;
+  uint64_t in_ref, out_ref;      // src - 16, dst - 16
+  uint32_t *wg_rounds;           // [waves] round counts of the workgroup's waves
+  uint32_t wave, alive;          // this wave, waves of the workgroup with packets
+  __device__ bool live(uint32_t p, uint32_t r) const { return kRun * r < S.wlen[p]; }
+  __device__ uint32_t wlen(uint32_t p) const { return S.wlen[p]; }
+  __device__ uint64_t in_base(uint32_t p) const {
+    return in_ref + 16ull * (((uint64_t)S.in_hi[p] << 32) | S.in16[p]);
+  }
+  __device__ uint64_t out_base(uint32_t p) const {
+    return out_ref + 16ull * (((uint64_t)S.out_hi[p] << 32) | S.out16[p]);
+  }
+  // (host side: src and dst are non-null, so offsets stay below 2^44 bytes)
+  __device__ void set(uint32_t lane, uint64_t in_base, uint64_t out_base, uint32_t W, bool ok) {
+    const uint64_t i16 = (in_base - in_ref) >> 4, o16 = (out_base - out_ref) >> 4;
+    S.in16[lane] = (uint32_t)i16;
+    S.in_hi[lane] = (uint8_t)(i16 >> 32);
+    S.out16[lane] = (uint32_t)o16;
+    S.out_hi[lane] = (uint8_t)(o16 >> 32);
+    S.wlen[lane] = ok ? W : 0u;
+  }
+  __device__ void kill(uint32_t lane) { S.wlen[lane] = 0u; }
+  // the workgroup's round count (every wave must run the same barrier steps)
+  __device__ uint32_t wg_max(uint32_t wave_rounds) const {
+    if ((threadIdx.x & 63u) == 0u) wg_rounds[wave] = wave_rounds;
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t w = 0; w < alive; ++w) m = max(m, wg_rounds[w]);
+    __syncthreads();  // the slots are rewritten by the next group
+    return m;
+  }
+};
+
 struct UniformGeom {
   uint64_t in0, out0, in_stride, out_stride;
   uint64_t dead;   // wave mask of packets dropped at the header check (open)
@@ -146,6 +191,59 @@ struct UniformGeom {
   __device__ uint64_t out_base(uint32_t p) const { return out0 + (uint64_t)p * out_stride; }
 };
 
+// Memory instructions of the generic (per-packet address) staging, written so
+// that the compiler inserts no waits of its own between them:
+//  * the LDS-DMA is inline asm -- for the builtin the compiler drains vmcnt
+//    before every later LDS read (here: the per-packet tables read for the
+//    next piece), which serialised the 8 pieces of a round;
+//  * stores go to the global address space -- a flat store may alias LDS, so
+//    the compiler drained every in-flight LDS-DMA before each one;
+//  * asm instructions carry their own wait states (the compiler's hazard
+//    recognizer does not look inside inline asm): five after an SGPR/m0
+//    write before the DMA reads them, two after a 16-byte store before its
+//    data registers may be rewritten.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) uint8_t gbyte;
+typedef __attribute__((address_space(1))) uint16_t gshort;
+typedef __attribute__((address_space(1))) uint32_t gword;
+
+__device__ __forceinline__ uint32_t lds_offset(const uint4 *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint4 *)p;
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma_global(uint32_t lds, const uint8_t *src) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, off"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(src) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ void gstore16(uint8_t *dst, const uint4 v) {
+  const u32x4 vv = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"(dst), "v"(vv) : "memory");
+}
+
+// the first k (1..15) bytes of a chunk, through global-address-space pointers
+__device__ __forceinline__ void gstore_partial(uint8_t *p, const uint32_t w[4], int k) {
+  gbyte *g = (gbyte *)p;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int v = k - 4 * j;
+    if (v >= 4) {
+      *(gword *)(g + 4 * j) = w[j];
+    } else if (v > 0) {
+      gbyte *pb = g + 4 * j;
+      if (v >= 2) {
+        *(gshort *)pb = (uint16_t)w[j];
+        if (v == 3) pb[2] = (uint8_t)(w[j] >> 16);
+      } else {
+        pb[0] = (uint8_t)w[j];
+      }
+    }
+  }
+}
+
 // Cooperative LDS-DMA load of round r: instruction j carries packets 8j..8j+7,
 // lane i moves 16 bytes (chunk (i&7)^swz(p)) of packet p = 8j + i/8.
 template <bool kSeal, class Geom>
@@ -155,10 +253,8 @@ __device__ __forceinline__ void stage_in(uint4 *run, const Geom &g, uint32_t lan
     const uint32_t p = 8u * j + (lane >> 3);
     const uint32_t k = (lane & 7u) ^ swz(p);
     const uint32_t w = kRun * r + 16u * k;
-    if (g.live(p, r) && w >= Ranges<kSeal>::in_lo() && w < Ranges<kSeal>::in_hi(g.wlen(p))) {
-      const uint8_t *src = reinterpret_cast<const uint8_t *>(g.in_base(p)) + w;
-      __builtin_amdgcn_global_load_lds(src, &run[64u * j], 16, 0, 0);
-    }
+    if (g.live(p, r) && w >= Ranges<kSeal>::in_lo() && w < Ranges<kSeal>::in_hi(g.wlen(p)))
+      dma_global(lds_offset(&run[64u * j]), reinterpret_cast<const uint8_t *>(g.in_base(p)) + w);
   }
 }
 
@@ -176,10 +272,10 @@ __device__ __forceinline__ void stage_out(uint4 *run, const Geom &g, uint32_t la
       uint8_t *dst = reinterpret_cast<uint8_t *>(g.out_base(p)) + w;
       const uint32_t n = hi - w;
       if (n >= 16u) {
-        *reinterpret_cast<uint4 *>(dst) = v;
+        gstore16(dst, v);
       } else {
         const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-        store_partial(dst, wv, (int)n);
+        gstore_partial(dst, wv, (int)n);
       }
     }
   }
@@ -194,7 +290,6 @@ __device__ __forceinline__ void stage_out(uint4 *run, const Geom &g, uint32_t la
 // byte to move gets an offset past the resource's num_records, which the
 // buffer range check turns into no memory access.  That keeps vmcnt counts
 // static, which the double-buffered prefetch relies on.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kNoAccess = 0x7ffffff0u;  // >= any num_records used below
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(uint64_t base, uint32_t bytes) {
@@ -451,7 +546,8 @@ template <bool kSeal, bool kUniform, bool kSync, class Stage, class Geom>
 __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
                                          int32_t *status_out) {
-  static_assert(!kSync || kUniform, "phase-locked steps need workgroup-uniform control flow");
+  // phase-locked: every wave of the workgroup runs the same number of rounds
+  // (uniform batches by construction, descriptor batches via DescGeom::wg_max)
   // ---- per-packet setup (owner lane) ------------------------------------
   uint32_t W = 0, P = 0;
   if (kUniform || job.status == WG_STATUS_OK) {
@@ -469,6 +565,9 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   uint32_t rounds;
   if constexpr (kUniform) {
     rounds = my_runs;  // uniform: job.len is a kernel argument
+  } else if constexpr (kSync) {
+    g.set(lane, job.in_base, job.out_base, W, my_runs != 0u);
+    rounds = g.wg_max(wave_max(my_runs));
   } else {
     S.in_base[lane] = job.in_base;
     S.out_base[lane] = job.out_base;
@@ -500,7 +599,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     poly_init(poly, ks);
     S.park[lane] = make_uint4(ks[4], ks[5], ks[6], ks[7]);  // s, read back for the tag
   };
-  if (kSeal && my_runs) one_time_key();  // overlaps the first DMA
+  if (kSeal && !kSync && my_runs) one_time_key();
 
   // double buffering only for the uniform geometry (static vmcnt counts)
   constexpr bool kPrefetch = kUniform && sizeof(S.run) / sizeof(S.run[0]) == 2;
@@ -526,7 +625,8 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
     if (job.status != WG_STATUS_OK) {
       my_runs = 0;  // nothing of this packet is stored
-      if constexpr (!kUniform) S.nruns[lane] = 0;
+      if constexpr (kSync && !kUniform) g.kill(lane);
+      else if constexpr (!kUniform) S.nruns[lane] = 0;
     } else {
       n1 = h.z;
       n2 = h.w;
@@ -594,10 +694,11 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     // its registers freed, before the loop body)
     if (rounds) {
       uint4 hdr = make_uint4(0u, 0u, 0u, 0u);
-      if (!kSeal) hdr = ld16(reinterpret_cast<const uint8_t *>(job.in_base));
+      if (!kSeal && my_runs) hdr = ld16(reinterpret_cast<const uint8_t *>(job.in_base));
 #if !WG_ABLATE_NO_MEM
       stage_in<kSeal>(run, g, lane, 0);
 #endif
+      if (kSeal && my_runs) one_time_key();  // while round 0's DMA is in flight
       if (!kSeal && my_runs) open_header(hdr);
     }
     for (uint32_t r = 0; r < rounds; ++r) {
@@ -613,7 +714,9 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         if (kSeal && r == 0)  // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
           run[8u * lane + (0u ^ swz(lane))] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
       };
-      if ((int)(kRun * r) < (int)P && !WG_ABLATE_NO_CRYPT) {  // workgroup-uniform
+      // workgroup-uniform: P for uniform batches; every round for descriptor
+      // batches (lanes without ciphertext in the round ignore the keystream)
+      if ((!kUniform || (int)(kRun * r) < (int)P) && !WG_ABLATE_NO_CRYPT) {
         // the keystream lives only inside this branch (kept out of phis, the
         // compiler would otherwise carry it as a register tuple and spill it)
         uint32_t ka[16], kb[16];
@@ -806,12 +909,64 @@ __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_desc_ke
                          i < prm.n ? prm.status + idx : nullptr);
 }
 
+// Phase-locked descriptor batches (configs 3/4): persistent 512-thread
+// workgroups like the strided kernel; each group of 512 descriptors runs the
+// workgroup's longest packet's rounds (the length-sorted plan,
+// wg_gpu_plan_batch, keeps a group's packets alike).
+template <bool kSeal>
+__global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_sync_kernel(
+    DescParams prm) {
+  constexpr uint32_t kWaves = kStridedThreads / 64u;
+  __shared__ WaveStageDesc stage[kWaves];
+  __shared__ uint32_t wg_rounds[kWaves];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t groups = (prm.n + 64u * kWaves - 1u) / (64u * kWaves);
+  for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
+    // only the last group can lack waves; it is this workgroup's last iteration
+    if (pkt0 >= prm.n) return;
+    const uint32_t alive = min(kWaves, (prm.n - grp * kWaves * 64u + 63u) / 64u);
+    const uint32_t i = pkt0 + lane;
+    uint32_t idx = i;
+    PacketJob job;
+    job.status = -1;
+    job.in_base = reinterpret_cast<uint64_t>(prm.src);
+    job.out_base = reinterpret_cast<uint64_t>(prm.dst);
+    job.counter = 0;
+    job.len = 0;
+    job.slot = 0;
+    if (i < prm.n) {
+      if (prm.order) idx = prm.order[i];
+      const wg_packet_desc d = prm.descs[idx];
+      job.len = d.len;
+      job.slot = d.key_slot;
+      job.counter = d.counter;
+      const uint64_t src = reinterpret_cast<uint64_t>(prm.src) + d.src_off;
+      const uint64_t dst = reinterpret_cast<uint64_t>(prm.dst) + d.dst_off;
+      job.in_base = kSeal ? src - 16u : src;
+      job.out_base = kSeal ? dst : dst - 16u;
+      if (!kSeal && d.key_slot == WG_KEY_SLOT_INVALID_PACKET) job.status = WG_STATUS_INVALID_PACKET;
+      else if (!kSeal && d.key_slot == WG_KEY_SLOT_NO_SESSION) job.status = WG_STATUS_NO_CURRENT_SESSION;
+      else if (d.key_slot >= prm.key_slots) job.status = WG_STATUS_BAD_KEY_SLOT;
+      else if (((d.src_off | d.dst_off) & 15u) != 0u) job.status = WG_STATUS_MISALIGNED;
+      else job.status = WG_STATUS_OK;
+    }
+    DescGeom g{stage[wave], reinterpret_cast<uint64_t>(prm.src) - 16u,
+               reinterpret_cast<uint64_t>(prm.dst) - 16u, wg_rounds, wave, alive};
+    run_wave<kSeal, false, true>(stage[wave], g, lane, job, prm.keys, prm.key_index,
+                                 i < prm.n ? prm.status + idx : nullptr);
+  }
+}
+
 template __global__ void aead_strided_kernel<true, false>(StridedParams);
 template __global__ void aead_strided_kernel<false, false>(StridedParams);
 template __global__ void aead_strided_kernel<true, true>(StridedParams);
 template __global__ void aead_strided_kernel<false, true>(StridedParams);
 template __global__ void aead_desc_kernel<true>(DescParams);
 template __global__ void aead_desc_kernel<false>(DescParams);
+template __global__ void aead_desc_sync_kernel<true>(DescParams);
+template __global__ void aead_desc_sync_kernel<false>(DescParams);
 
 }  // namespace wg
 

@@ -25,6 +25,9 @@ constexpr uint32_t kStridedMinWaves = 4;  // __launch_bounds__ waves per SIMD: 1
 #define WG_STRIDED_BLOCKS_PER_CU (4u * kStridedMinWaves * 64u / kStridedThreads)
 #endif
 constexpr uint32_t kStridedBlocksPerCU = WG_STRIDED_BLOCKS_PER_CU;
+#ifndef WG_DESC_SYNC
+#define WG_DESC_SYNC 1  // descriptor batches with non-null bases use the phase-locked kernel
+#endif
 
 struct StridedParams {
   const uint8_t *keys;        // device key table, 32 B per slot
@@ -50,6 +53,7 @@ struct DescParams {
 
 template <bool kSeal, bool kTail> __global__ void aead_strided_kernel(StridedParams prm);
 template <bool kSeal> __global__ void aead_desc_kernel(DescParams prm);
+template <bool kSeal> __global__ void aead_desc_sync_kernel(DescParams prm);
 
 // wg_plan.hip: counting sort of a descriptor batch by rounds (longest first)
 constexpr uint32_t kPlanBins = 256;   // rounds 0..254, 255+ share the top bin

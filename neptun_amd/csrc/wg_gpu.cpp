@@ -175,12 +175,22 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
   wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, order, src, dst, status, n,
                      ctx->key_slots};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (seal)
+  if (WG_DESC_SYNC && src && dst) {
+    // phase-locked, persistent (wg_aead.hip aead_desc_sync_kernel); its compact
+    // per-packet tables hold buffer-relative offsets, hence non-null bases
+    const uint32_t groups = (n + wg::kStridedThreads - 1) / wg::kStridedThreads;
+    const dim3 grid(std::min(groups, ctx->cus * wg::kStridedBlocksPerCU));
+    if (seal)
+      hipLaunchKernelGGL(wg::aead_desc_sync_kernel<true>, grid, dim3(wg::kStridedThreads), 0, s, prm);
+    else
+      hipLaunchKernelGGL(wg::aead_desc_sync_kernel<false>, grid, dim3(wg::kStridedThreads), 0, s, prm);
+  } else if (seal) {
     hipLaunchKernelGGL(wg::aead_desc_kernel<true>, dim3(grid_for(n)), dim3(wg::kBlockThreads), 0,
                        s, prm);
-  else
+  } else {
     hipLaunchKernelGGL(wg::aead_desc_kernel<false>, dim3(grid_for(n)), dim3(wg::kBlockThreads), 0,
                        s, prm);
+  }
   WG_HIP(hipGetLastError(), "batch: launch");
   return WG_RC_OK;
 }

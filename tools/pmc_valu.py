@@ -25,7 +25,8 @@ COUNTERS = ["GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU
 
 def short(name):
     for tag in ("aead_strided_kernel<true, false>", "aead_strided_kernel<false, false>",
-                "aead_desc_kernel<true>", "aead_desc_kernel<false>"):
+                "aead_desc_kernel<true>", "aead_desc_kernel<false>",
+                "aead_desc_sync_kernel<true>", "aead_desc_sync_kernel<false>"):
         if tag in name:
             return tag
     return None
