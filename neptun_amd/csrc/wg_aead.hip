@@ -54,6 +54,10 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
 #endif
 
+#ifndef WG_SYNC_KEY_BLOCK
+#define WG_SYNC_KEY_BLOCK 1  // phase-locked Poly1305 key block on the sync paths
+#endif
+
 #ifndef WG_STAGGER
 #define WG_STAGGER 0  // experiment: 1 odd workgroups, 2 second half of the grid start late
 #endif
@@ -595,7 +599,13 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 
   auto one_time_key = [&]() {
     uint32_t ks[16];
-    chacha20_block(ks, key, 0u, n1, n2);  // RFC 8439 2.6: block 0 -> r | s
+    // RFC 8439 2.6: block 0 -> r | s.  Phase-locked for seal on the sync
+    // paths, where every wave calls this once per group right after issuing
+    // round 0's DMA (wave-uniform call site).  Open computes it per lane as
+    // soon as the lane's header has landed: locking it there made every wave
+    // wait for the slowest header (-4 %).
+    if constexpr (kSync && kSeal && WG_SYNC_KEY_BLOCK) chacha20_block_sync(ks, key, 0u, n1, n2);
+    else chacha20_block(ks, key, 0u, n1, n2);
     poly_init(poly, ks);
     S.park[lane] = make_uint4(ks[4], ks[5], ks[6], ks[7]);  // s, read back for the tag
   };
@@ -621,8 +631,10 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   // open, round 0: the datagram header (noise/mod.rs:170-180) decides the
   // packet's fate and supplies the nonce counter
   auto open_header = [&](const uint4 h) {
-    if (h.x != WG_MSG_DATA) job.status = WG_STATUS_INVALID_PACKET;
-    else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
+    if (job.status == WG_STATUS_OK) {  // (lanes already failed keep their status)
+      if (h.x != WG_MSG_DATA) job.status = WG_STATUS_INVALID_PACKET;
+      else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
+    }
     if (job.status != WG_STATUS_OK) {
       my_runs = 0;  // nothing of this packet is stored
       if constexpr (kSync && !kUniform) g.kill(lane);
@@ -698,7 +710,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 #if !WG_ABLATE_NO_MEM
       stage_in<kSeal>(run, g, lane, 0);
 #endif
-      if (kSeal && my_runs) one_time_key();  // while round 0's DMA is in flight
+      if (kSeal) one_time_key();  // while round 0's DMA is in flight (every wave: phase-locked)
       if (!kSeal && my_runs) open_header(hdr);
     }
     for (uint32_t r = 0; r < rounds; ++r) {

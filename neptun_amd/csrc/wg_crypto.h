@@ -90,6 +90,53 @@ __device__ __forceinline__ void chacha20_block(uint32_t ks[16], const uint32_t k
   "v_alignbit_b32 %12, %12, %12, " #SH "\n\tv_alignbit_b32 %13, %13, %13, " #SH "\n\t"    \
   "v_alignbit_b32 %14, %14, %14, " #SH "\n\tv_alignbit_b32 %15, %15, %15, " #SH "\n\t"    \
   "s_barrier"
+// Single-block form of the phase-locked steps (4 quarter-rounds per step:
+// 4 v_add + 4 v_xor + 4 v_alignbit + s_barrier), for the Poly1305 key block.
+#define WG_STEP4_ASM(SH)                                                                  \
+  "v_add_u32 %0, %0, %8\n\tv_add_u32 %1, %1, %9\n\tv_add_u32 %2, %2, %10\n\t"            \
+  "v_add_u32 %3, %3, %11\n\t"                                                            \
+  "v_xor_b32 %4, %4, %0\n\tv_xor_b32 %5, %5, %1\n\tv_xor_b32 %6, %6, %2\n\t"              \
+  "v_xor_b32 %7, %7, %3\n\t"                                                             \
+  "v_alignbit_b32 %4, %4, %4, " #SH "\n\tv_alignbit_b32 %5, %5, %5, " #SH "\n\t"          \
+  "v_alignbit_b32 %6, %6, %6, " #SH "\n\tv_alignbit_b32 %7, %7, %7, " #SH "\n\t"          \
+  "s_barrier"
+#define WG_COLUMN_ROUND1 \
+  asm volatile(WG_STEP4_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7)); \
+  asm volatile(WG_STEP4_ASM(20) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15)); \
+  asm volatile(WG_STEP4_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7)); \
+  asm volatile(WG_STEP4_ASM(25) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15));
+#define WG_DIAGONAL_ROUND1 \
+  asm volatile(WG_STEP4_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4)); \
+  asm volatile(WG_STEP4_ASM(20) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14)); \
+  asm volatile(WG_STEP4_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4)); \
+  asm volatile(WG_STEP4_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14));
+
+// Keystream block blk, phase-locked (same barrier contract as chacha20_block2_sync).
+__device__ __forceinline__ void chacha20_block_sync(uint32_t (&ks)[16], const uint32_t k[8],
+                                                    uint32_t blk, uint32_t n1, uint32_t n2) {
+  uint32_t p0 = kSigma0, p1 = kSigma1, p2 = kSigma2, p3 = kSigma3;
+  uint32_t p4 = k[0], p5 = k[1], p6 = k[2], p7 = k[3], p8 = k[4], p9 = k[5], p10 = k[6], p11 = k[7];
+  uint32_t p12 = blk, p13 = 0, p14 = n1, p15 = n2;
+  WG_QR(p0, p4, p8, p12) WG_QR(p1, p5, p9, p13) WG_QR(p2, p6, p10, p14) WG_QR(p3, p7, p11, p15)
+  __builtin_amdgcn_s_barrier();
+#if WG_CHACHA_PRIO
+  __builtin_amdgcn_s_setprio(WG_CHACHA_PRIO);
+#endif
+  WG_DIAGONAL_ROUND1
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    WG_COLUMN_ROUND1
+    WG_DIAGONAL_ROUND1
+  }
+#if WG_CHACHA_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
+  ks[0] = p0 + kSigma0; ks[1] = p1 + kSigma1; ks[2] = p2 + kSigma2; ks[3] = p3 + kSigma3;
+  ks[4] = p4 + k[0]; ks[5] = p5 + k[1]; ks[6] = p6 + k[2]; ks[7] = p7 + k[3];
+  ks[8] = p8 + k[4]; ks[9] = p9 + k[5]; ks[10] = p10 + k[6]; ks[11] = p11 + k[7];
+  ks[12] = p12 + blk; ks[13] = p13; ks[14] = p14 + n1; ks[15] = p15 + n2;
+}
+
 // One column round and one diagonal round of both blocks (p = block blk,
 // q = block blk + 1, 16 named state words each), 4 steps per round.  Named
 // scalars, not arrays: the compiler keeps arrays that are addressed through
