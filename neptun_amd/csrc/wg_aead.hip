@@ -54,6 +54,10 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
 #endif
 
+#ifndef WG_ABLATE_ZEROING
+#define WG_ABLATE_ZEROING 0  // timing-only: forged packets keep their plaintext
+#endif
+
 #ifndef WG_SYNC_KEY_BLOCK
 #define WG_SYNC_KEY_BLOCK 1  // phase-locked Poly1305 key block on the sync paths
 #endif
@@ -838,13 +842,18 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       // tag mismatch: never expose unauthenticated plaintext (ring open_within
       // zeroes it); the streamed stores of this wave land first (same wave, in order)
       job.status = WG_STATUS_INVALID_AEAD_TAG;
+#if !WG_ABLATE_ZEROING
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (global-address-space stores: a flat store may alias LDS and would
+      // make the compiler drain in-flight LDS-DMA around it)
       uint8_t *pt = reinterpret_cast<uint8_t *>(job.out_base) + 16u;
-      for (uint32_t off = 0; off + 16u <= P; off += 16u) st16(pt + off, 0, 0, 0, 0);
+      const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+      for (uint32_t off = 0; off + 16u <= P; off += 16u) gstore16(pt + off, zero);
       if (q) {
         const uint32_t z[4] = {0, 0, 0, 0};
-        store_partial(pt + (P & ~15u), z, (int)q);
+        gstore_partial(pt + (P & ~15u), z, (int)q);
       }
+#endif
     }
   }
   if (status_out) *status_out = job.status;
