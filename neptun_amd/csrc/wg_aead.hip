@@ -737,7 +737,12 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     // its registers freed, before the loop body)
     if (rounds) {
       uint4 hdr = make_uint4(0u, 0u, 0u, 0u);
-      if (!kSeal && my_runs) hdr = ld16(reinterpret_cast<const uint8_t *>(job.in_base));
+      // (a global-address-space load: a flat one may alias LDS and makes the
+      // compiler drain the LDS-DMA in flight before it)
+      if (!kSeal && my_runs) {
+        const u32x4 h = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(job.in_base);
+        hdr = make_uint4(h.x, h.y, h.z, h.w);
+      }
 #if !WG_ABLATE_NO_MEM
       stage_in<kSeal>(run, g, lane, 0);
 #endif
