@@ -370,24 +370,30 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   const uint32_t hi = Ranges<kSeal>::out_hi(g.W);
   if (kRun * r >= Ranges<kSeal>::out_lo() && kRun * r + kRun <= hi && (kSeal || g.dead == 0)) {
     // interior round: 8 full-chunk stores at round-independent per-lane offsets
+    // (all 8 LDS reads first: the asm stores are memory barriers to the
+    // compiler, which otherwise serialises read -> wait -> store per piece)
     const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
+    uint4 v[kChunks];
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j) v[j] = run[64u * j + lane];
 #pragma unroll
     for (uint32_t j = 0; j < kChunks; ++j) {
-      const uint4 v = run[64u * j + lane];
-      const u32x4 vv = {v.x, v.y, v.z, v.w};
+      const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
       store16(vv, g.out0, 64u * stride, (j & 1u) ? v1 : v0, 8u * j * stride + kRun * r);
     }
     return;
   }
   bool partial = false;
+  uint4 v[kChunks];
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j) v[j] = run[64u * j + lane];
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
     const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
     const bool ok = !dead && w >= Ranges<kSeal>::out_lo() && w < hi;
-    const uint4 v = run[64u * j + lane];
-    const u32x4 vv = {v.x, v.y, v.z, v.w};
+    const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
     store16(vv, g.out0, 64u * stride, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
             8u * j * stride + kRun * r);
     partial |= ok && hi - w < 16u;
