@@ -62,19 +62,6 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_SYNC_KEY_BLOCK 1  // phase-locked Poly1305 key block on the sync paths
 #endif
 
-#ifndef WG_STAGGER
-#define WG_STAGGER 0  // experiment: 1 odd workgroups, 2 second half of the grid start late
-#endif
-
-#ifndef WG_PREFETCH
-#define WG_PREFETCH 0  // 1: double-buffered LDS stage (round r+1 DMA overlaps round r)
-#endif
-constexpr uint32_t kBufs = WG_PREFETCH ? 2 : 1;
-
-#ifndef WG_REG_PREFETCH
-#define WG_REG_PREFETCH 0  // 1: uniform path loads round r+1 into VGPRs during round r
-#endif
-
 // Diagnostic build only (-DWG_STAMP=1): s_memtime at the phase boundaries of
 // the phase-locked loop, wave 0 of every workgroup, read back with
 // wg_gpu_debug_stamps() (tools/stamps.py).  Never part of the product build.
@@ -104,9 +91,9 @@ struct WaveStage {
   uint4 park[64];              // per-packet Poly1305 "s" half of the one-time key
   static constexpr bool kTagPark = false;
 };
-// Uniform geometry: kBufs run buffers, no tables (addresses are arithmetic).
+// Uniform geometry: one run buffer, no tables (addresses are arithmetic).
 struct WaveStageUniform {
-  uint4 run[kBufs][64 * kChunks];
+  uint4 run[1][64 * kChunks];
   uint4 park[64];  // per-packet Poly1305 "s" (parked here: VGPRs are the scarce resource)
   uint4 tagp[64];  // open: the received tag (ditto; 2 x 8 waves x 10 KiB = the whole LDS)
   static constexpr bool kTagPark = true;
@@ -119,12 +106,7 @@ struct WaveStageUniform {
 // 8(L&1) + (k ^ swz)) and ds_write_b128 (8 contiguous lanes, 32 banks: slot
 // k ^ swz).  (L>>1)&7 alone left every write 2-way conflicted (L, L^1 on one
 // slot): PMC SQ_LDS_BANK_CONFLICT was a third of SQ_LDS_IDX_ACTIVE.
-#ifndef WG_SWZ_V1
-#define WG_SWZ_V1 0  // 1: the old (p>>1)&7 swizzle, for A/B
-#endif
-__device__ __forceinline__ uint32_t swz(uint32_t p) {
-  return WG_SWZ_V1 ? ((p >> 1) & 7u) : (((p >> 1) & 7u) ^ ((p & 1u) << 2));
-}
+__device__ __forceinline__ uint32_t swz(uint32_t p) { return ((p >> 1) & 7u) ^ ((p & 1u) << 2); }
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 #pragma unroll
@@ -427,36 +409,6 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   }
 }
 
-// Register-prefetch form of the uniform load: the same 8 coalesced loads (8
-// packets x 128 contiguous bytes per wave instruction) into VGPRs, issued one
-// round ahead and written to the LDS stage at the top of the round they feed.
-// Costs 32 VGPRs (3 waves/SIMD instead of 4) but takes the HBM round trip off
-// the critical path of every round.
-template <bool kSeal>
-__device__ __forceinline__ void load_regs(u32x4 (&pre)[kChunks], const UniformGeom &g,
-                                          uint32_t lane, uint32_t r) {
-  const uint32_t stride = (uint32_t)g.in_stride;
-  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 64u * stride);
-  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
-  const uint32_t hi = Ranges<kSeal>::in_hi(g.W);
-#pragma unroll
-  for (uint32_t j = 0; j < kChunks; ++j) {
-    const uint32_t k = (j & 1u) ? k1 : k0;
-    const uint32_t w = kRun * r + 16u * k;
-    const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
-    const bool ok = !dead && w >= Ranges<kSeal>::in_lo() && w < hi;
-    pre[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? y * stride + 16u * k : kNoAccess,
-                                                   8u * j * stride + kRun * r, 0);
-  }
-}
-
-__device__ __forceinline__ void commit_regs(uint4 *run, const u32x4 (&pre)[kChunks],
-                                            uint32_t lane) {
-#pragma unroll
-  for (uint32_t j = 0; j < kChunks; ++j)
-    run[64u * j + lane] = make_uint4(pre[j].x, pre[j].y, pre[j].z, pre[j].w);
-}
-
 // One lane's chunk of ciphertext work.  m = plaintext/ciphertext byte index of
 // the chunk (wire w - 16); `ks` = its 4 keystream words.  Returns via LDS.
 template <bool kSeal>
@@ -634,23 +586,6 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   };
   if (kSeal && !kSync && my_runs) one_time_key();
 
-  // double buffering only for the uniform geometry (static vmcnt counts)
-  constexpr bool kPrefetch = kUniform && sizeof(S.run) / sizeof(S.run[0]) == 2;
-  constexpr bool kRegPf = kUniform && !kPrefetch && WG_REG_PREFETCH;
-  u32x4 pre[kChunks];
-#if !WG_ABLATE_NO_MEM
-  if constexpr (kPrefetch) stage_in<kSeal>(S.run[0], g, lane, 0);
-  if constexpr (kRegPf) {
-    load_regs<kSeal>(pre, g, lane, 0);
-    // 8 no-op stores (out-of-range offsets) give the loop entry the same
-    // "8 loads, then 8 stores" vmcnt shape as the back edge, so the waits the
-    // compiler puts before commit_regs are vmcnt(15..8), not vmcnt(7..0)
-    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, 64u * (uint32_t)g.out_stride);
-    const u32x4 z = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (uint32_t j = 0; j < kChunks; ++j) __builtin_amdgcn_raw_buffer_store_b128(z, rs, kNoAccess, 16u * j, 0);
-  }
-#endif
   // open, round 0: the datagram header (noise/mod.rs:170-180) decides the
   // packet's fate and supplies the nonce counter
   auto open_header = [&](const uint4 h) {
@@ -796,27 +731,12 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       WG_STAMP_AT(kSeal, r, 5);
     }
   } else {
+    uint4 *run = S.run[0];
     for (uint32_t r = 0; r < rounds; ++r) {
-      uint4 *run = S.run[kPrefetch ? (r & 1u) : 0u];
 #if !WG_ABLATE_NO_MEM
-      if constexpr (kRegPf) {
-        commit_regs(run, pre, lane);
-        if (r + 1u < rounds) load_regs<kSeal>(pre, g, lane, r + 1u);
-      } else if constexpr (kPrefetch) {
-        if (r + 1u < rounds) {
-          stage_in<kSeal>(S.run[(r + 1u) & 1u], g, lane, r + 1u);
-          // everything older than round r+1's 8 loads is done (round r's DMA)
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else {
-          lds_wait_dma();
-        }
-      } else {
-        stage_in<kSeal>(run, g, lane, r);
-        lds_wait_dma();
-      }
-#else
-      lds_wait_dma();
+      stage_in<kSeal>(run, g, lane, r);
 #endif
+      lds_wait_dma();
       if (r < my_runs) {
         if (!kSeal) {
           if (r == 0) open_header(run[8u * lane + (0u ^ swz(lane))]);
@@ -921,11 +841,6 @@ aead_strided_kernel(StridedParams prm) {
     // workgroups stay in their steady, mutually de-phased rhythm (one DMA
     // in flight while the other computes) instead of restarting in step
     const uint32_t groups = (prm.n / 64u + kWaves - 1u) / kWaves;
-#if WG_STAGGER
-    // de-phase the workgroups that share a CU (a guess at the placement)
-    if ((WG_STAGGER == 1 ? blockIdx.x & 1u : blockIdx.x >= gridDim.x / 2u))
-      for (int i = 0; i < 16; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
     for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
       const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
       // only the last group can be partial, and it is this workgroup's last
