@@ -58,6 +58,9 @@ template <bool kSeal> __global__ void aead_desc_sync_kernel(DescParams prm);
 // wg_plan.hip: counting sort of a descriptor batch by rounds (longest first)
 constexpr uint32_t kPlanBins = 256;   // rounds 0..254, 255+ share the top bin
 constexpr uint32_t kPlanTiles = 256;  // contiguous descriptor tiles, one block each
+constexpr uint32_t kPlanThreads = 512, kPlanWaves = kPlanThreads / 64u;  // hist / scatter blocks
+constexpr uint32_t kPlanPer = 8;                            // descriptors per lane per chunk
+constexpr uint32_t kPlanChunk = kPlanThreads * kPlanPer;  // descriptors per chunk
 static_assert(kPlanBins * kPlanTiles * 4 == WG_PLAN_SCRATCH_BYTES, "scratch size");
 __global__ void plan_hist_kernel(const wg_packet_desc *descs, uint32_t n, uint32_t extra,
                                  uint32_t *table);

@@ -227,10 +227,10 @@ int wg_gpu_plan_batch(wg_gpu_ctx *ctx, int seal, const wg_packet_desc *descs, ui
   DeviceGuard g(ctx->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint32_t extra = seal ? WG_DATA_OVERHEAD_SZ : 0u;  // rounds follow the datagram size
-  hipLaunchKernelGGL(wg::plan_hist_kernel, dim3(wg::kPlanTiles), dim3(256), 0, s, descs, n, extra,
+  hipLaunchKernelGGL(wg::plan_hist_kernel, dim3(wg::kPlanTiles), dim3(wg::kPlanThreads), 0, s, descs, n, extra,
                      scratch);
   hipLaunchKernelGGL(wg::plan_scan_kernel, dim3(1), dim3(1024), 0, s, scratch);
-  hipLaunchKernelGGL(wg::plan_scatter_kernel, dim3(wg::kPlanTiles), dim3(256), 0, s, descs, n,
+  hipLaunchKernelGGL(wg::plan_scatter_kernel, dim3(wg::kPlanTiles), dim3(wg::kPlanThreads), 0, s, descs, n,
                      extra, scratch, order);
   WG_HIP(hipGetLastError(), "plan_batch: launch");
   return WG_RC_OK;

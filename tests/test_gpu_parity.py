@@ -307,6 +307,30 @@ def test_plan_batch_is_a_length_sorted_permutation(torch_cuda, gpu):
     assert np.array_equal(b.order.cpu().numpy().astype(np.int64), order)
 
 
+@pytest.mark.parametrize("n", [1, 63, 4097, 256 * 4096 + 12345])
+def test_plan_batch_equals_stable_sort_by_rounds(torch_cuda, gpu, n):
+    """The permutation is exactly a stable sort by round count, longest first
+    (ties keep index order), whatever the tiling: sizes with one partial chunk per
+    tile up to several 4096-descriptor chunks per tile.  Lengths cover the clamp
+    (>= 255 rounds share one bin) and zero."""
+    torch = torch_cuda
+    from neptun_amd.gpu import DESC_DTYPE
+    rng = np.random.default_rng(n)
+    lens = rng.choice(np.array([0, 1, 64, 96, 97, 256, 576, 1350, 8900, 40000, 70000], np.uint32), n)
+    for seal, extra in ((True, 32), (False, 0)):
+        d = np.zeros(n, DESC_DTYPE)
+        d["len"] = lens
+        descs = torch.from_numpy(d.view(np.uint8)).to("cuda")
+        order = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        scratch = torch.empty(256 * 256, dtype=torch.int32, device="cuda")
+        gpu.plan_batch(seal, descs, n, order, scratch)
+        torch.cuda.synchronize()
+        got = order.cpu().numpy().astype(np.int64)
+        rounds = np.minimum((lens.astype(np.int64) + extra + 127) // 128, 255)
+        want = np.argsort(-rounds, kind="stable")
+        assert np.array_equal(got, want), (seal, n)
+
+
 @pytest.mark.parametrize("ordered", [True, False])
 def test_mixed_mtu_batch_matches_oracle(torch_cuda, gpu, ordered):
     torch = torch_cuda
