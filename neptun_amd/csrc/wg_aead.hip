@@ -321,7 +321,9 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint3
   const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 64u * stride);
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   const uint32_t hi = Ranges<kSeal>::in_hi(g.W);
-  if (kRun * r >= Ranges<kSeal>::in_lo() && kRun * r + kRun <= hi && (kSeal || g.dead == 0)) {
+  // (open: packets dropped at the header check are loaded like the others --
+  // harmless, their lanes skip the crypto and stage_out never writes them back)
+  if (kRun * r >= Ranges<kSeal>::in_lo() && kRun * r + kRun <= hi) {
     // interior round (wave-uniform test): every lane moves a full chunk, the
     // per-lane offsets are round-independent -- no range checks
     const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
@@ -335,8 +337,7 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint3
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
-    const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
-    const bool ok = !dead && w >= Ranges<kSeal>::in_lo() && w < hi;
+    const bool ok = w >= Ranges<kSeal>::in_lo() && w < hi;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16,
                                              ok ? y * stride + 16u * k : kNoAccess,
                                              8u * j * stride + kRun * r, 0, 0);
@@ -350,7 +351,12 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, 64u * stride);
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   const uint32_t hi = Ranges<kSeal>::out_hi(g.W);
-  if (kRun * r >= Ranges<kSeal>::out_lo() && kRun * r + kRun <= hi && (kSeal || g.dead == 0)) {
+  // open's drop mask, opaque to the optimiser: otherwise it hoists 8 per-lane
+  // 64-bit masks 1 << (8j + y) out of the round loop, and their spill reloads
+  // drain the DMA in flight
+  uint64_t dead = kSeal ? 0ull : g.dead;
+  if constexpr (!kSeal) asm volatile("" : "+s"(dead));
+  if (kRun * r >= Ranges<kSeal>::out_lo() && kRun * r + kRun <= hi && dead == 0) {
     // interior round: 8 full-chunk stores at round-independent per-lane offsets
     // (all 8 LDS reads first: the asm stores are memory barriers to the
     // compiler, which otherwise serialises read -> wait -> store per piece)
@@ -373,8 +379,8 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
-    const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
-    const bool ok = !dead && w >= Ranges<kSeal>::out_lo() && w < hi;
+    const bool gone = !kSeal && ((((uint32_t)(dead >> (8u * j))) >> y) & 1u);
+    const bool ok = !gone && w >= Ranges<kSeal>::out_lo() && w < hi;
     const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
     store16(vv, g.out0, 64u * stride, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
             8u * j * stride + kRun * r);
@@ -388,8 +394,8 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
     for (uint32_t j = 0; j < kChunks; ++j) {
       const uint32_t k = (j & 1u) ? k1 : k0;
       const uint32_t w = kRun * r + 16u * k;
-      const bool dead = !kSeal && ((g.dead >> (8u * j + y)) & 1u);
-      const bool mine = !dead && w >= Ranges<kSeal>::out_lo() && w < hi && hi - w < 16u;
+      const bool gone = !kSeal && ((((uint32_t)(dead >> (8u * j))) >> y) & 1u);
+      const bool mine = !gone && w >= Ranges<kSeal>::out_lo() && w < hi && hi - w < 16u;
       const uint32_t n = mine ? hi - w : 0u;
       const uint4 v = run[64u * j + lane];
       const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
