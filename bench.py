@@ -44,7 +44,11 @@ def parse(argv=None):
     ap.add_argument("--peers", type=int, default=4096, help="config 4")
     ap.add_argument("--per-peer", type=int, default=4096, help="config 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, affinity)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = one per physical core of this job's CPU share "
+                         "(min of affinity, physical cores, OMP_NUM_THREADS)")
+    ap.add_argument("--evp-sample", type=int, default=257,
+                    help="sealed datagrams compared byte for byte against OpenSSL EVP")
     return ap.parse_args(argv)
 
 
@@ -104,6 +108,21 @@ class StridedWorkload:
         ok = int((self.st_seal != 0).sum()) == 0 and int((self.st_open != 0).sum()) == 0
         return ok and torch.equal(self.back.view(n, S)[:, 16:16 + P], self.pt.view(n, S)[:, 16:16 + P])
 
+    def size_hist(self):
+        return {self.P: self.n}
+
+    def sample(self, k):
+        """k (key, receiver_idx, counter, payload, datagram) tuples spread over the batch."""
+        import numpy as np
+
+        from tools import synth
+        key = synth.keys(1)[0].tobytes()
+        idx = np.unique(np.linspace(0, self.n - 1, min(k, self.n)).astype(np.int64))
+        pt = self.pt.view(self.n, self.S)[idx].cpu().numpy()
+        wire = self.wire.view(self.n, self.S)[idx].cpu().numpy()
+        return [(key, synth.RECEIVER_IDX, self.counter_base + int(i), pt[j, 16:16 + self.P].tobytes(),
+                 wire[j, :self.P + 32].tobytes()) for j, i in enumerate(idx)]
+
     def describe(self, world):
         return {"workload": f"BASELINE config {'2' if world == 1 else '5'}: {self.n} x {self.P} B "
                             "packets per GPU, single session, seal then open, device-resident",
@@ -134,6 +153,7 @@ class DescWorkload:
         keys = synth.keys(nkeys)
         idx = np.full(nkeys, synth.RECEIVER_IDX, np.uint32) + np.arange(nkeys, dtype=np.uint32)
         self.ctx.set_keys(0, keys, idx)
+        self.keys, self.key_index = keys, idx
         b = self.b
         self.packets = b.n
         P = b.sizes.astype(np.int64)
@@ -166,6 +186,14 @@ class DescWorkload:
         ok = int((b.st_seal != 0).sum()) == 0 and int((b.st_open != 0).sum()) == 0
         return ok and b.round_trip_equal()
 
+    def sample(self, k):
+        return self.b.sample(k, self.keys, self.key_index)
+
+    def size_hist(self):
+        import numpy as np
+        u, c = np.unique(self.b.sizes, return_counts=True)
+        return {int(a): int(b) for a, b in zip(u, c)}
+
     def describe(self, world):
         b = self.b
         if self.cfg == 3:
@@ -187,9 +215,35 @@ def make_workload(args, dev, rank, world):
 
 
 # ---------------------------------------------------------------------------
-def cpu_baseline(threads: int) -> dict:
+def host_cpus() -> dict:
+    """The host's CPU model, its physical core count and the CPUs this process
+    may run on (the GPU box grants each job a share of the machine)."""
+    model, phys = "unknown", set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if ":" in line:
+                    k, v = (x.strip() for x in line.split(":", 1))
+                    cur[k] = v
+                    if k == "model name":
+                        model = v
+                elif cur:
+                    phys.add((cur.get("physical id", "0"), cur.get("core id", cur.get("processor"))))
+                    cur = {}
+        if cur:
+            phys.add((cur.get("physical id", "0"), cur.get("core id", cur.get("processor"))))
+    except OSError:
+        pass
+    allowed = len(os.sched_getaffinity(0))
+    return {"model": model, "physical_cores": len(phys) or (os.cpu_count() or 1),
+            "logical_cpus": os.cpu_count() or 1, "allowed_cpus": allowed}
+
+
+def cpu_baseline(threads: int, cpus: dict) -> dict:
     """Config 1 on the host cores: oracle/build/cpu_baseline (NepTUN framing over
-    OpenSSL EVP, the stand-in for ring's asm; see oracle/cpu_baseline.c)."""
+    OpenSSL EVP, the stand-in for ring's asm; see oracle/cpu_baseline.c), one
+    session per thread like packet_workers.rs:113-131 (num_cpus::get_physical())."""
     exe = os.path.join(ROOT, "oracle", "build", "cpu_baseline")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
@@ -208,44 +262,80 @@ def cpu_baseline(threads: int) -> dict:
         "unit": "Gbit/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": cpus["model"],
+        "physical_cores": cpus["physical_cores"],
+        "allowed_cpus": cpus["allowed_cpus"],
         "sample": (f"config 1: 65536 x 1350 B encap+decap round trip, one session per thread, "
                    f"NepTUN framing (session.rs:205-302) over OpenSSL 3 EVP_chacha20_poly1305 "
                    f"(stand-in for ring 0.17 asm; the Rust reference cannot be built here), "
-                   f"median of 21 reps on {threads} threads; 1 thread: {one['gbps']:.3f} Gbit/s"),
+                   f"median of 21 reps on {threads} threads = this job's CPU share "
+                   f"({cpus['allowed_cpus']} CPUs in the affinity mask, {cpus['logical_cpus']} "
+                   f"logical / {cpus['physical_cores']} physical cores on the machine, "
+                   f"{cpus['model']}); "
+                   f"1 thread: {one['gbps']:.3f} Gbit/s"),
         "one_core_gbps": round(one["gbps"], 3),
+        # linear extrapolation of the 1-thread rate, labelled as such (not measured)
+        "all_physical_cores_extrapolated_gbps": round(one["gbps"] * cpus["physical_cores"], 1),
     }
 
 
-def load_traffic(kernel: str, config: int) -> dict | None:
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def evp_check(wl, k: int) -> dict:
+    """Compare k sealed datagrams of the timed batch with OpenSSL EVP (tools/evp_check.py)."""
+    if k <= 0 or not hasattr(wl, "sample"):
+        return {"checked": 0}
+    try:
+        from tools.evp_check import Evp
+        evp = Evp()
+    except OSError as e:  # libcrypto missing: say so, never pass silently
+        return {"checked": 0, "error": f"libcrypto unavailable: {e}"[:120]}
+    bad = 0
+    smp = wl.sample(k)
+    for key, ridx, ctr, pt, wire in smp:
+        bad += evp.seal_datagram(key, ridx, ctr, pt) != wire
+    return {"checked": len(smp), "mismatches": bad}
+
+
+def load_pmc(kind: str, kernel: str, config: int) -> dict | None:
+    """Committed rocprofv3 PMC summary of one bench kernel for this config:
+    kind "traffic" (tools/pmc_traffic.py, HBM bytes per launch) or "valu"
+    (tools/pmc_valu.py, clock + VALU instructions per wave)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{kind}_config{config}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
     k = d.get("kernels", {}).get(kernel)
-    if not k or d.get("config", 2) != config:
-        return None
-    return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": d.get("source", path)}
-
-
-def load_valu(kernel: str, config: int) -> dict | None:
-    """VALU-side PMC summary (tools/pmc_valu.py) of the same kernel: the bound that
-    actually limits it."""
-    path = os.path.join(ROOT, "profiles", "pmc_valu.json")
-    if config != 2 or not os.path.exists(path):
-        return None
-    with open(path) as f:
-        k = json.load(f).get("kernels", {}).get(kernel)
     if not k:
         return None
-    return {"valu_busy_frac": k["valu_issue_frac"], "valu_instr_per_wave": k["valu_per_wave"],
-            "clock_GHz_profiled": k["clock_GHz"], "source": "profiles/pmc_valu.json"}
+    return dict(k, source=os.path.relpath(path, ROOT), how=d.get("source", ""))
 
 
-def run(args, factory=None, device_fn=None):
-    """Bench body.  `factory`/`device_fn` are injection points for the CPU tests
-    of the multi-rank path (tests/test_bench_dist.py); production uses HIP."""
+def compute_roofline(wl, kernel: str, config: int, kernel_ms: float) -> dict:
+    """VALU-issue floor of the launch (tools/compute_roofline.py) at the clock the
+    PMC run measured for this kernel, against the live kernel time."""
+    from tools import compute_roofline as cr
+    if not hasattr(wl, "size_hist"):
+        return None
+    pmc = load_pmc("valu", kernel, config)
+    clock = pmc["clock_GHz"] if pmc else None
+    fl = cr.launch_floor(wl.size_hist(), clock)
+    out = {"bound": "valu-issue", "model": "tools/compute_roofline.py", **fl}
+    if pmc:
+        out.update({
+            "clock_GHz_profiled": pmc["clock_GHz"],
+            "frac": round(fl["floor_ms_at_profiled_clock"] / kernel_ms, 4),
+            "frac_in_profiled_run": round(fl["floor_ms_at_profiled_clock"] / pmc["ms"], 4),
+            "valu_instr_per_64_packets_measured": round(
+                pmc["valu_per_wave"] * pmc.get("waves", 0) * 64 / wl.packets, 1),
+            "pmc_source": pmc["source"],
+        })
+    return out
+
+
+def run(args, factory=None, device_fn=None, device_count=None):
+    """Bench body.  `factory`/`device_fn`/`device_count` are injection points for
+    the CPU tests of the multi-rank path (tests/test_bench_dist.py); production
+    uses HIP."""
     import torch
     import torch.distributed as dist
 
@@ -254,9 +344,18 @@ def run(args, factory=None, device_fn=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    visible = torch.cuda.device_count() if device_count is None else device_count
+    if world > visible:
+        # one process per GPU: an N-GPU line from ranks sharing devices would be
+        # published as scaling it is not -- refuse instead
+        if rank == 0:
+            print(json.dumps({"error": f"{world} ranks but {visible} visible GPU(s): one rank per "
+                                       "GPU is required, refusing to share devices",
+                              "n_gpus": world, "visible_gpus": visible}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 2
     if device_fn is None:
-        # one rank per GPU; more ranks than GPUs (a rehearsal on a smaller box) share them
-        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         stream = torch.cuda.current_stream(dev)
@@ -291,28 +390,32 @@ def run(args, factory=None, device_fn=None):
     open_ms = [e[1].elapsed_time(e[2]) for e in events]
 
     # correctness of what was timed: statuses + round-trip identity (whole batch)
+    # + a sample of sealed datagrams byte for byte against OpenSSL EVP
     ok = bool(wl.verify())
+    evp = evp_check(wl, args.evp_sample)
+    ok = ok and evp.get("mismatches", 0) == 0
     if world > 1:
         f = torch.tensor([0 if ok else 1], dtype=torch.int64)
         dist.all_reduce(f, op=dist.ReduceOp.MAX)
         ok = int(f.item()) == 0
     line = None
     if not ok:
-        line = {"error": "round-trip verification failed", "rank": rank}
+        line = {"error": "verification failed (statuses, round trip or EVP sample)", "rank": rank,
+                "evp_sample": evp}
     elif rank == 0:
         total_payload, total_pkts = float(totals[0]), float(totals[1])
         gbps = total_payload * 8 * args.steps / elapsed / 1e9
         avg = {"seal": sum(seal_ms) / len(seal_ms), "open": sum(open_ms) / len(open_ms)}
         dom = "seal" if avg["seal"] >= avg["open"] else "open"
         achieved = wl.launch_bytes[dom] / (avg[dom] * 1e-3) / 1e9
-        tr = load_traffic(wl.kernels[dom], args.config)
-        valu = load_valu(wl.kernels[dom], args.config)
+        tr = load_pmc("traffic", wl.kernels[dom], args.config)
         line = {
             "metric": METRIC if args.config == 2 else
             f"Gbit/s device-resident ChaCha20-Poly1305 seal+open, BASELINE config {args.config}",
             "value": round(gbps, 2),
             "unit": "Gbit/s",
             "n_gpus": world,
+            "visible_gpus": visible,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -329,11 +432,13 @@ def run(args, factory=None, device_fn=None):
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": tr["bytes_per_launch"] if tr else None,
+                "traffic": tr["hbm_bytes_per_launch"] if tr else None,
+                "traffic_over_algorithmic": round(tr["hbm_bytes_per_launch"] / wl.launch_bytes[dom], 4)
+                if tr else None,
                 "traffic_source": tr["source"] if tr else None,
                 "algorithmic_bytes_per_launch": wl.launch_bytes[dom],
-                # what limits the kernel: VALU issue (96 % busy), not HBM -- DESIGN.md 3
-                "compute": valu,
+                # the bound that actually limits the kernel: VALU issue
+                "compute": compute_roofline(wl, wl.kernels[dom], args.config, avg[dom]),
             },
             "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
             "seal_gbps": round(wl.payload_bytes * 8 / (avg["seal"] * 1e-3) / 1e9, 1),
@@ -341,12 +446,19 @@ def run(args, factory=None, device_fn=None):
             "roundtrip_hbm_frac": round((wl.launch_bytes["seal"] + wl.launch_bytes["open"]) /
                                         ((avg["seal"] + avg["open"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "packets_per_step": int(total_pkts),
-            "verified": "all statuses Ok and open(seal(x)) == x over the whole batch",
+            "verified": "all statuses Ok, open(seal(x)) == x over the whole batch, and "
+                        f"{evp.get('checked', 0)} sealed datagrams spread over the batch equal "
+                        "OpenSSL EVP_chacha20_poly1305 with NepTUN framing",
+            "evp_sample": evp,
         }
         if world == 1 and not args.no_cpu_baseline and args.config == 2:
-            threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+            cpus = host_cpus()
+            # one thread per physical core this job may use: the GPU box grants a
+            # job a CPU share (OMP_NUM_THREADS there) of a larger machine
+            share = int(os.environ.get("OMP_NUM_THREADS") or cpus["allowed_cpus"])
+            threads = args.cpu_threads or max(1, min(cpus["allowed_cpus"], cpus["physical_cores"], share))
             try:
-                line["cpu_baseline"] = cpu_baseline(threads)
+                line["cpu_baseline"] = cpu_baseline(threads, cpus)
             except Exception as e:  # reported, never fatal to the GPU number
                 line["cpu_baseline"] = {"error": str(e)[:200]}
     if line is not None:

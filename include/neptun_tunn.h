@@ -17,8 +17,11 @@
  *     mark -- then validate_decapsulated_packet (mod.rs:606-670: keepalive ->
  *     Done, IPv4/IPv6 length truncation, InvalidPacket) and rx_bytes.
  * Handshake / cookie messages are not the data path: such datagrams come back
- * as WG_TUNN_NOT_DATA for the caller's CPU Tunn.  Timers (timers.rs) are not
- * mirrored; set_current_session follows the reference minus its timer test.
+ * as WG_TUNN_NOT_DATA for the caller's CPU Tunn.  Of the timers (timers.rs)
+ * only what the data plane reads is mirrored: timers[TimeCurrent] (set by the
+ * caller, wg_tunn_set_time) and the per-ring-slot session_timers that
+ * set_current_session compares (mod.rs:528-542); rekey / keepalive / expiry
+ * stay with the caller's CPU Tunn.
  *
  * The replay window (session.rs:40-157) is exposed on its own (wg_replay_*)
  * for tests and for embedders that keep their own sessions.
@@ -75,12 +78,19 @@ int wg_tunn_create(wg_gpu_ctx *ctx, uint32_t first_slot, wg_tunn **out);
 int wg_tunn_destroy(wg_tunn *t);
 
 /* Session::new(local_index, peer_index, receiving_key, sending_key) stored at
- * sessions[local_index % 8] (mod.rs:449-452, 477-481); make_current != 0 makes
- * it the sending session (set_current_session, mod.rs:521-532). */
+ * sessions[local_index % 8] (mod.rs:449-452, 477-481) with session timer =
+ * the Tunn's current time; make_current != 0 then runs set_current_session
+ * (mod.rs:528-542). */
 int wg_tunn_install_session(wg_tunn *t, uint32_t local_index, uint32_t peer_index,
                             const uint8_t receiving_key[32], const uint8_t sending_key[32],
                             int make_current);
 int wg_tunn_stats(const wg_tunn *t, uint64_t *tx_bytes, uint64_t *rx_bytes);
+/* timers[TimeCurrent] = now (update_timers, timers.rs:228-233; any monotonic
+ * unit, e.g. ns since the Tunn was created).  wg_tunn_install_session records
+ * it as the ring slot's session timer (timer_tick_session_established,
+ * timers.rs:173-185); set_current_session switches to a session only if the
+ * current slot is empty or its timer is not newer (mod.rs:528-542).  Default 0. */
+int wg_tunn_set_time(wg_tunn *t, uint64_t now);
 
 /* Direct (copy-free) batches: when the caller's buffers are registered with
  * wg_gpu_register_host (include/neptun_gpu.h) and every packet of an

@@ -293,7 +293,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const Geom &g, uint32_t la
 // byte to move gets an offset past the resource's num_records, which the
 // buffer range check turns into no memory access.  That keeps vmcnt counts
 // static, which the double-buffered prefetch relies on.
-constexpr uint32_t kNoAccess = 0x7ffffff0u;  // >= any num_records used below
+constexpr uint32_t kNoAccess = kNoAccessOffset;  // >= any num_records used below
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(uint64_t base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)bytes,
@@ -318,9 +318,14 @@ template <bool kSeal>
 __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint32_t lane,
                                          uint32_t r) {
   const uint32_t stride = (uint32_t)g.in_stride;
-  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 64u * stride);
-  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   const uint32_t hi = Ranges<kSeal>::in_hi(g.W);
+  // num_records = the end of the wave's last packet's input, rounded up to its
+  // 16-byte chunk: the range check drops a WHOLE 16-byte access that crosses
+  // num_records (the tail chunk reads up to 15 bytes past the packet -- inside
+  // the same 16-byte-aligned, so mapped, granule).  launch_strided bounds
+  // 63 * stride + hi below kNoAccess.
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 63u * stride + ((hi + 15u) & ~15u));
+  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   // (open: packets dropped at the header check are loaded like the others --
   // harmless, their lanes skip the crypto and stage_out never writes them back)
   if (kRun * r >= Ranges<kSeal>::in_lo() && kRun * r + kRun <= hi) {
@@ -348,9 +353,10 @@ template <bool kSeal>
 __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint32_t lane,
                                           uint32_t r) {
   const uint32_t stride = (uint32_t)g.out_stride;
-  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, 64u * stride);
-  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   const uint32_t hi = Ranges<kSeal>::out_hi(g.W);
+  const uint32_t records = 63u * stride + ((hi + 15u) & ~15u);  // (see stage_in)
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, records);
+  const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   // open's drop mask, opaque to the optimiser: otherwise it hoists 8 per-lane
   // 64-bit masks 1 << (8j + y) out of the round loop, and their spill reloads
   // drain the DMA in flight
@@ -367,7 +373,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
 #pragma unroll
     for (uint32_t j = 0; j < kChunks; ++j) {
       const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
-      store16(vv, g.out0, 64u * stride, (j & 1u) ? v1 : v0, 8u * j * stride + kRun * r);
+      store16(vv, g.out0, records, (j & 1u) ? v1 : v0, 8u * j * stride + kRun * r);
     }
     return;
   }
@@ -382,7 +388,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
     const bool gone = !kSeal && ((((uint32_t)(dead >> (8u * j))) >> y) & 1u);
     const bool ok = !gone && w >= Ranges<kSeal>::out_lo() && w < hi;
     const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
-    store16(vv, g.out0, 64u * stride, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
+    store16(vv, g.out0, records, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
             8u * j * stride + kRun * r);
     partial |= ok && hi - w < 16u;
   }

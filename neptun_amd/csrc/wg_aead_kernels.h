@@ -6,7 +6,10 @@
 
 namespace wg {
 
-constexpr uint32_t kBlockThreads = 256;  // 4 waves per workgroup (descriptor / tail kernels)
+constexpr uint32_t kBlockThreads = 256;
+// buffer offset past every num_records the uniform kernels use: a lane given it
+// moves nothing (launch_strided keeps 63 * stride + len below it)
+constexpr uint32_t kNoAccessOffset = 0x7ffffff0u;  // 4 waves per workgroup (descriptor / tail kernels)
 
 // Uniform strided kernel: with WG_SYNC the ChaCha20 steps are phase-locked by
 // s_barrier (wg_crypto.h chacha20_block2_sync), which needs waves that share a

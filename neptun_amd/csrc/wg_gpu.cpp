@@ -243,6 +243,17 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
   if (key_slot >= ctx->key_slots) return fail(WG_RC_INVALID_ARGUMENT, "strided: bad key slot");
   if (((uintptr_t)src | (uintptr_t)dst | src_stride | dst_stride) & 15u)
     return fail(WG_RC_INVALID_ARGUMENT, "strided: pointers and strides must be 16-byte aligned");
+  // packets must not overlap their neighbours: the datagram / plaintext of
+  // packet i lies in [i * stride, i * stride + its length)
+  const uint64_t in_len = len, out_len = seal ? (uint64_t)len + WG_DATA_OVERHEAD_SZ
+                                               : (len >= WG_DATA_OVERHEAD_SZ ? len - WG_DATA_OVERHEAD_SZ : 0);
+  if (in_len > src_stride || out_len > dst_stride)
+    return fail(WG_RC_INVALID_ARGUMENT, "strided: packet length exceeds its stride (slots would overlap)");
+  // the uniform kernels reach a wave's 64 slots through one buffer resource
+  // with 32-bit offsets (num_records = 63 * stride + the last packet's extent)
+  // and mask idle lanes with the out-of-range offset wg::kNoAccessOffset
+  if (63u * std::max(src_stride, dst_stride) + (uint64_t)len + 64u >= wg::kNoAccessOffset)
+    return fail(WG_RC_INVALID_ARGUMENT, "strided: stride too large (63 * stride + len must stay below 2 GiB)");
   if (n == 0) return WG_RC_OK;
   DeviceGuard g(ctx->device);
   wg::StridedParams prm{ctx->d_keys, ctx->d_key_index, src, dst, status, src_stride,

@@ -108,7 +108,6 @@ struct Session {  // session.rs:11-18
   uint32_t receiving_index = 0, sending_index = 0;
   uint64_t sending_counter = 0;  // AtomicUsize sending_key_counter
   wg_replay window{};
-  uint64_t established = 0;      // install sequence: stands in for timers.session_timers
 };
 
 inline uint32_t ld32(const uint8_t *p) {
@@ -123,12 +122,9 @@ inline uint64_t ld64(const uint8_t *p) {
 }
 inline uint64_t round128(uint64_t x) { return (x + 127) / 128 * 128; }
 
-size_t chunk_bytes() {  // staging bytes per pipeline chunk (WG_TUNN_CHUNK_KB overrides)
-  static const size_t v = [] {
-    const char *e = std::getenv("WG_TUNN_CHUNK_KB");
-    return e ? std::max<size_t>(64, (size_t)std::atol(e)) << 10 : size_t(16) << 20;
-  }();
-  return v;
+size_t chunk_bytes() {  // staging bytes per pipeline chunk (WG_TUNN_CHUNK_KB overrides, per call)
+  const char *e = std::getenv("WG_TUNN_CHUNK_KB");
+  return e ? std::max<size_t>(64, (size_t)std::atol(e)) << 10 : size_t(16) << 20;
 }
 constexpr uint32_t kSets = 2;                     // double buffering
 
@@ -274,7 +270,10 @@ struct wg_tunn {
   Session sessions[WG_N_SESSIONS];
   uint64_t current = 0;     // index of the most recently used session (mod.rs:69)
   uint64_t tx_bytes = 0, rx_bytes = 0;
-  uint64_t install_seq = 0;
+  // timers[TimeCurrent] and timers.session_timers (timers.rs:91, :173-185): the
+  // only timer state the data plane reads (set_current_session, mod.rs:530-538)
+  uint64_t time_current = 0;
+  uint64_t session_timers[WG_N_SESSIONS] = {};
   Staging st[kSets];
   Pool *pool = nullptr;
   // per-call scratch (kept to avoid reallocations)
@@ -304,13 +303,14 @@ struct DevGuard {
     if (e_ != hipSuccess) return wg_pipe_fail(WG_RC_HIP_ERROR, what, e_); \
   } while (0)
 
-// set_current_session (mod.rs:521-532); the timer comparison uses install order
+// set_current_session (mod.rs:528-542): switch unless the current slot holds a
+// session established later than the new one (session_timers compare)
 void set_current_session(wg_tunn *t, uint64_t new_idx) {
   const uint64_t cur = t->current;
   if (cur == new_idx) return;
-  const Session &c = t->sessions[cur % WG_N_SESSIONS];
-  const Session &n = t->sessions[new_idx % WG_N_SESSIONS];
-  if (!c.live || n.established >= c.established) t->current = new_idx;
+  if (!t->sessions[cur % WG_N_SESSIONS].live ||
+      t->session_timers[new_idx % WG_N_SESSIONS] >= t->session_timers[cur % WG_N_SESSIONS])
+    t->current = new_idx;
 }
 
 inline void set_err(wg_tunn_result &r, int32_t st) {
@@ -390,9 +390,36 @@ bool trace_on() {
 
 // abs_src / abs_dst: descriptors carry absolute device addresses of registered
 // caller memory on that side (no staging bytes there)
+// Test-only fault injection: WG_TUNN_FAIL_CHUNK=c makes the batch fail with a
+// HIP error right after chunk c has been enqueued (read per call).
+int injected_failure(size_t c) {
+  const char *e = std::getenv("WG_TUNN_FAIL_CHUNK");
+  if (e && (size_t)std::atol(e) == c)
+    return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: injected failure (WG_TUNN_FAIL_CHUNK)", hipSuccess);
+  return WG_RC_OK;
+}
+
+// Every exit from run_chunks -- error paths included -- leaves both staging
+// sets idle: work still queued on a set is waited for (its kernel may still be
+// writing the pinned staging a later reserve() would free) and `busy` cleared,
+// so the next batch starts from a clean pipeline.
+struct PipelineDrain {
+  wg_tunn *t;
+  explicit PipelineDrain(wg_tunn *tt) : t(tt) { drain(); }
+  ~PipelineDrain() { drain(); }
+  void drain() {
+    for (auto &S : t->st)
+      if (S.busy) {
+        (void)hipStreamSynchronize(S.stream);
+        S.busy = false;
+      }
+  }
+};
+
 template <class Pack, class Unpack>
 int run_chunks(wg_tunn *t, bool seal, Pack pack, Unpack unpack, bool abs_src = false,
                bool abs_dst = false) {
+  PipelineDrain drain_guard(t);
   const size_t nc = t->chunks.size();
   const bool tr = trace_on();
   const double t0 = tr ? now_us() : 0.0;
@@ -448,6 +475,7 @@ int run_chunks(wg_tunn *t, bool seal, Pack pack, Unpack unpack, bool abs_src = f
     }
     TUNN_HIP(hipEventRecord(S.done, S.stream), "tunn: event");
     S.busy = true;
+    if (const int rc = injected_failure(c)) return rc;
     if (c >= 1 && t->st[(c - 1) % kSets].busy) {  // overlap: unpack c-1 while c runs
       const int rc2 = wait_unpack(c - 1);
       if (rc2) return rc2;
@@ -616,8 +644,15 @@ int wg_tunn_install_session(wg_tunn *t, uint32_t local_index, uint32_t peer_inde
   s.receiving_index = local_index;
   s.sending_index = peer_index;
   wg_replay_init(&s.window);
-  s.established = ++t->install_seq;
+  // timer_tick_session_established (timers.rs:173-185)
+  t->session_timers[ring] = t->time_current;
   if (make_current) set_current_session(t, local_index);
+  return WG_RC_OK;
+}
+
+int wg_tunn_set_time(wg_tunn *t, uint64_t now) {
+  if (!t) return WG_RC_INVALID_ARGUMENT;
+  t->time_current = now;  // update_timers: timers[TimeCurrent] = now (timers.rs:228-233)
   return WG_RC_OK;
 }
 
@@ -670,6 +705,9 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   // mod.rs:296-299 copies src into dst[16..] before looking at the session
   for (uint32_t i : copy_only) std::memcpy(dst[i] + WG_DATA_OFFSET, src[i], src_len[i]);
   if (t->sel.empty()) return WG_RC_OK;
+  // until its chunk comes back a selected packet reads as failed (a batch that
+  // errors part-way leaves no stale or zeroed results behind)
+  for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);
   const uint64_t ctr0 = s.sending_counter;  // one fetch_add per batch (session.rs:219)
   s.sending_counter += t->sel.size();
   // direct mode: src and dst of every packet 16-byte aligned inside registered
@@ -757,10 +795,12 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
     t->slot.push_back(t->first_slot + 2 * (ridx % WG_N_SESSIONS));
   }
   if (t->sel.empty()) return WG_RC_OK;
+  for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);  // until its chunk returns
   // pass 2 (sequential, packet order, per chunk as it returns): replay window,
   // validation, stats; the byte copies follow on the pool
   return open_selected(t, datagram, len, dst, [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
     const uint32_t i = t->sel[k];
+    std::memset(&res[i], 0, sizeof res[i]);
     const uint8_t *d = datagram[i];
     const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
     const uint32_t ridx = ld32(d + 4);
@@ -813,8 +853,10 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
     t->slot.push_back(t->first_slot + 2 * (uint32_t)ring + (ours ? 0u : 1u));
   }
   if (t->sel.empty()) return WG_RC_OK;
+  for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);  // until its chunk returns
   return open_selected(t, datagram, len, dst, [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
     const uint32_t i = t->sel[k];
+    std::memset(&res[i], 0, sizeof res[i]);
     const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
     const int32_t g_st = S.h_st[kk];
     if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }

@@ -45,6 +45,7 @@ def _bind(L):
     L.wg_tunn_destroy.argtypes = [vp]
     L.wg_tunn_install_session.argtypes = [vp, u32, u32, c.c_char_p, c.c_char_p, c.c_int]
     L.wg_tunn_stats.argtypes = [vp, c.POINTER(u64), c.POINTER(u64)]
+    L.wg_tunn_set_time.argtypes = [vp, u64]
     L.wg_tunn_session_counters.argtypes = [vp, u32, c.POINTER(u64), c.POINTER(Replay)]
     for fn in (L.wg_tunn_encapsulate_batch, L.wg_tunn_decapsulate_batch, L.wg_tunn_decrypt_batch):
         fn.argtypes = [vp, u32, vp, vp, vp, vp, c.POINTER(TunnResult)]
@@ -93,6 +94,10 @@ class Tunn:
         check(self._lib.wg_tunn_install_session(self._h, local_index, peer_index, recv_key,
                                                 send_key, 1 if make_current else 0),
               "wg_tunn_install_session")
+
+    def set_time(self, now: int):
+        """timers[TimeCurrent] (the session timer the next install_session records)."""
+        check(self._lib.wg_tunn_set_time(self._h, now), "wg_tunn_set_time")
 
     def _batch_ptrs(self, fn, name, src_ptrs, src_lens, dst_ptrs, dst_caps):
         """Batch over raw addresses (numpy uint64 / uint32 arrays); returns the results."""

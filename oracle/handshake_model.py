@@ -13,7 +13,7 @@ The checker for the GPU handshake kernels (neptun_amd/csrc/wg_handshake.hip):
                               ephemeral key and timestamp come from the caller)
 Pinned by RFC 7748's test vectors, OpenSSL's X25519 (oracle/openssl_ref.c) and the
 reference's own INITIAL_CHAIN_KEY / INITIAL_CHAIN_HASH constants (handshake.rs:29-39),
-which are BLAKE2s outputs (tests/test_handshake_oracle.py).
+which are BLAKE2s outputs (tests/test_handshake_cpu.py).
 """
 from __future__ import annotations
 

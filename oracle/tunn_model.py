@@ -7,7 +7,9 @@ A plain-Python restatement, one packet at a time, of
   Tunn::encapsulate(_in_place)   neptun/src/noise/mod.rs:295-338
   Tunn::decapsulate -> parse_incoming_packet -> handle_data -> validate_decapsulated_packet
                                  mod.rs:139-199, 346-380, 545-569, 606-670
-  set_current_session            mod.rs:521-532 (session timer compare -> install order)
+  set_current_session            mod.rs:528-542 (timers.session_timers compare; the
+                                 timers are set like timer_tick_session_established,
+                                 timers.rs:173-185, from timers[TimeCurrent])
   Tunn::decrypt (xray)           mod.rs:383-417, session.rs:311-353
 used as the checker of the batched C++ mirror (neptun_amd/csrc/wg_tunn.cpp).
 Results use the same codes as include/neptun_tunn.h.
@@ -92,13 +94,12 @@ class Replay:
 
 
 class Session:
-    def __init__(self, local_index, peer_index, recv_key, send_key, established):
+    def __init__(self, local_index, peer_index, recv_key, send_key):
         self.receiving_index = local_index
         self.sending_index = peer_index
         self.recv_key, self.send_key = recv_key, send_key
         self.sending_counter = 0
         self.window = Replay()
-        self.established = established
 
 
 class Tunn:
@@ -107,21 +108,25 @@ class Tunn:
         self.current = 0
         self.tx_bytes = 0
         self.rx_bytes = 0
-        self._seq = 0
+        self.time_current = 0                   # timers[TimeCurrent]
+        self.session_timers = [0] * N_SESSIONS  # timers.session_timers (timers.rs:91)
+
+    def set_time(self, now):
+        self.time_current = now
 
     def install_session(self, local_index, peer_index, recv_key, send_key, make_current):
-        self._seq += 1
-        self.sessions[local_index % N_SESSIONS] = Session(local_index, peer_index, recv_key,
-                                                          send_key, self._seq)
+        self.sessions[local_index % N_SESSIONS] = Session(local_index, peer_index, recv_key, send_key)
+        self.session_timers[local_index % N_SESSIONS] = self.time_current  # timers.rs:181-182
         if make_current:
             self.set_current_session(local_index)
 
     def set_current_session(self, new_idx):
+        """mod.rs:528-542."""
         cur = self.current
         if cur == new_idx:
             return
-        c, n = self.sessions[cur % N_SESSIONS], self.sessions[new_idx % N_SESSIONS]
-        if c is None or n.established >= c.established:
+        if (self.sessions[cur % N_SESSIONS] is None
+                or self.session_timers[new_idx % N_SESSIONS] >= self.session_timers[cur % N_SESSIONS]):
             self.current = new_idx
 
     def encapsulate(self, src: bytes, dst: bytearray):

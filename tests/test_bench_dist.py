@@ -61,7 +61,7 @@ class FakeWorkload:
         pass
 
 
-def _worker(rank, world, port, outdir, fail_rank):
+def _worker(rank, world, port, outdir, fail_rank, device_count=None):
     import contextlib
     import io
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
@@ -72,7 +72,8 @@ def _worker(rank, world, port, outdir, fail_rank):
     args = bench.parse(["--steps", "5", "--warmup", "1", "--no-cpu-baseline"])
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
-        rc = bench.run(args, factory=FakeWorkload, device_fn=cpu_device)
+        rc = bench.run(args, factory=FakeWorkload, device_fn=cpu_device,
+                       device_count=world if device_count is None else device_count)
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
         json.dump({"rc": rc, "out": buf.getvalue()}, f)
 
@@ -85,9 +86,9 @@ def free_port():
     return p
 
 
-def run_ranks(tmp_path, world, fail_rank=None):
-    mp.start_processes(_worker, args=(world, free_port(), str(tmp_path), fail_rank), nprocs=world,
-                       join=True, start_method="spawn")
+def run_ranks(tmp_path, world, fail_rank=None, device_count=None):
+    mp.start_processes(_worker, args=(world, free_port(), str(tmp_path), fail_rank, device_count),
+                       nprocs=world, join=True, start_method="spawn")
     return [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
 
 
@@ -97,7 +98,7 @@ def test_two_ranks_aggregate_max_time_and_sum_payload(tmp_path, world):
     assert all(r["rc"] == 0 for r in res)
     assert res[1]["out"] == ""  # only rank 0 prints
     line = json.loads(res[0]["out"])
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["n_gpus"] == 2 and line["visible_gpus"] == 2 and line["scaling"] == "weak"
     assert line["packets_per_step"] == 1000 + 2000
     # the slowest rank (rank 1: >= 2.5 ms per step) sets the time
     assert line["ms_per_step"] >= 2.5
@@ -111,3 +112,13 @@ def test_failed_verification_on_any_rank_fails_the_run(tmp_path):
     res = run_ranks(tmp_path, 2, fail_rank=1)
     assert all(r["rc"] == 1 for r in res)
     assert "error" in json.loads(res[0]["out"])
+
+
+def test_more_ranks_than_gpus_is_refused(tmp_path):
+    """An N-rank line must come from N distinct GPUs: 2 ranks on a 1-GPU node exit
+    non-zero with an error line instead of publishing shared-device numbers."""
+    res = run_ranks(tmp_path, 2, device_count=1)
+    assert all(r["rc"] == 2 for r in res)
+    line = json.loads(res[0]["out"])
+    assert "error" in line and line["visible_gpus"] == 1 and line["n_gpus"] == 2
+    assert res[1]["out"] == ""

@@ -203,6 +203,42 @@ def test_strided_matches_oracle_and_counter_carry(torch_cuda, gpu):
     assert torch.equal(back.view(n, S)[:, :P], pt.view(n, S)[:, :P])
 
 
+@pytest.mark.parametrize("P", [1344, 1350, 64])
+def test_strided_tightly_packed_slots(torch_cuda, gpu, P):
+    """Strides equal to the packet extents (plaintexts back to back at stride P,
+    datagrams at stride P + 32, both 16-aligned): the last lane of every wave
+    reads and writes right up to the wave's end -- the buffer resource's range
+    must cover it exactly (wg_aead.hip stage_in / stage_out num_records)."""
+    torch = torch_cuda
+    n = 64 * 37 + 5
+    Sp, Sw = synth.round_up(P, 16), synth.round_up(P + 32, 16)
+    keys = synth.keys(1)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    rng = np.random.default_rng(P)
+    src = rng.integers(0, 256, n * Sp + 64, dtype=np.uint8)
+    pt = to_dev(torch, src)
+    wire = torch.zeros(n * Sw + 64, dtype=torch.uint8, device="cuda")
+    back = torch.zeros(n * Sp + 64, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.seal_strided(n, P, 0, 9, pt, Sp, wire, Sw, st)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = np.arange(n) * Sp
+    descs["dst_off"] = np.arange(n) * Sw
+    descs["counter"] = 9 + np.arange(n, dtype=np.uint64)
+    descs["len"] = P
+    want = np.zeros(n * Sw + 64, np.uint8)
+    assert (o.seal_batch(descs, keys, np.array([synth.RECEIVER_IDX], np.uint32), src, want) == 0).all()
+    assert np.array_equal(wire.cpu().numpy(), want)
+    st.fill_(-1)
+    gpu.open_strided(n, P + 32, 0, wire, Sw, back, Sp, st)
+    torch.cuda.synchronize()
+    assert (st == 0).all()
+    got = back.cpu().numpy()
+    assert np.array_equal(got[:n * Sp].reshape(n, Sp)[:, :P], src[:n * Sp].reshape(n, Sp)[:, :P])
+
+
 def test_open_header_checks(torch_cuda, gpu):
     torch = torch_cuda
     v = golden("data_packets.json")["vectors"][23]  # 1350 bytes
@@ -585,6 +621,14 @@ def test_argument_validation_fails_loudly(torch_cuda, gpu):
         gpu.seal_strided(64, 100, 0, 0, buf.data_ptr() + 4, 256, buf, 256)
     with pytest.raises(neptun_amd.NeptunGpuError, match="bad key slot"):
         gpu.seal_strided(64, 100, 1 << 20, 0, buf, 256, buf, 256)
+    # slots that would overlap their neighbours, and strides past the 32-bit
+    # buffer-offset reach of the uniform kernels
+    with pytest.raises(neptun_amd.NeptunGpuError, match="exceeds its stride"):
+        gpu.seal_strided(64, 240, 0, 0, buf, 256, buf, 256)  # datagram 272 > 256
+    with pytest.raises(neptun_amd.NeptunGpuError, match="exceeds its stride"):
+        gpu.open_strided(64, 300, 0, buf, 256, buf, 512)  # datagram 300 > 256
+    with pytest.raises(neptun_amd.NeptunGpuError, match="stride too large"):
+        gpu.seal_strided(64, 100, 0, 0, buf, 64 << 20, buf, 256)
     with pytest.raises(neptun_amd.NeptunGpuError, match="slot range"):
         gpu.set_keys(4095, synth.keys(2), np.array([1, 2], np.uint32))
     with pytest.raises(neptun_amd.NeptunGpuError, match="duplicate receiver"):

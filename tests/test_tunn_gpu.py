@@ -67,11 +67,12 @@ def make_pair(gpu, rng):
     from neptun_amd.tunn import Tunn
     tg = Tunn(gpu, FIRST_SLOT)
     sessions = []
-    for local in (3, 12):  # ring slots 3 and 4
+    for j, local in enumerate((3, 12)):  # ring slots 3 and 4, established at t = 100, 200
         rk, sk = rng.randbytes(32), rng.randbytes(32)
         peer = rng.getrandbits(32)
-        tm.install_session(local, peer, rk, sk, True)
-        tg.install_session(local, peer, rk, sk, True)
+        for t in (tm, tg):
+            t.set_time(100 * (j + 1))
+            t.install_session(local, peer, rk, sk, True)
         sessions.append((local, peer, rk, sk))
     return tm, tg, sessions
 
@@ -178,8 +179,8 @@ def test_encapsulate_batch_matches_sequential_tunn(gpu, seed):
         check_same(res_g, res_m, dst_g, dst_m, f"encap batch {batch}")
         # the peer receives what we sent: a keepalive / arbitrary payload path through decap
         if batch == 1:
-            # switch current session: a valid packet on the first session (older install)
-            # must not take over from the newer one (set_current_session, mod.rs:521-532)
+            # switch current session: a valid packet on the first session (older session
+            # timer) must not take over from the newer one (set_current_session, mod.rs:528-542)
             local, peer, rk, sk = sessions[0]
             d = o.format_packet_data(rk, local, 0, b"")
             dm, dg = bytearray(16), bytearray(16)
@@ -254,10 +255,11 @@ def test_decrypt_batch_matches_xray_decrypt(gpu, seed):
     tg.close()
 
 
-def test_multi_chunk_pipeline_matches_sequential_tunn(gpu):
+def test_multi_chunk_pipeline_matches_sequential_tunn(gpu, monkeypatch):
     """Batches of ~12 MB run as several 4 MiB chunks through the double-buffered
     staging pipeline; results must not depend on the chunking (counters across
     chunk edges, replay decisions in packet order across chunks)."""
+    monkeypatch.setenv("WG_TUNN_CHUNK_KB", "4096")
     rng = random.Random(77)
     tm, tg, sessions = make_pair(gpu, rng)
     srcs = [ipv4(rng, rng.choice([1350, 1400, rng.randrange(20, 1500)])) for _ in range(9000)]
@@ -272,6 +274,76 @@ def test_multi_chunk_pipeline_matches_sequential_tunn(gpu):
     dg = [bytearray(b"\xee" * c) for c in caps]
     res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
     check_same(tg.decapsulate_batch(dgs, dg), res_m, dg, dm, "decap multi-chunk")
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    tg.close()
+
+
+def test_session_timers_pick_the_current_session(gpu):
+    """set_current_session compares timers.session_timers (mod.rs:528-542), not the
+    install order: a session installed LATER but with an OLDER session timer does
+    not take over, and traffic on it does not switch the sending session."""
+    from neptun_amd.tunn import Tunn
+    rng = random.Random(31)
+    tm, tg = M.Tunn(), Tunn(gpu, FIRST_SLOT)
+    keys = {loc: (rng.randbytes(32), rng.randbytes(32), rng.getrandbits(32)) for loc in (9, 18, 27)}
+    for loc, now in ((9, 200), (18, 100), (27, 300)):
+        rk, sk, peer = keys[loc]
+        for t in (tm, tg):
+            t.set_time(now)
+            t.install_session(loc, peer, rk, sk, True)
+        if loc == 18:  # installed after 9, but its timer is older: 9 stays current
+            assert tm.current == 9
+    assert tm.current == 27
+    # data on the older sessions must not move the sending session off 27
+    for loc in (9, 18):
+        rk, sk, peer = keys[loc]
+        d = o.format_packet_data(rk, loc, 0, b"")
+        dm, dg = bytearray(16), bytearray(16)
+        check_same(tg.decapsulate_batch([d], [dg]), [tm.decapsulate(d, dm)], [dg], [dm], "ka")
+    assert tm.current == 27
+    srcs = [ipv4(rng, 100) for _ in range(3)]
+    dm = [bytearray(132) for _ in srcs]
+    dg = [bytearray(132) for _ in srcs]
+    res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dm)]
+    check_same(tg.encapsulate_batch(srcs, dg), res_m, dg, dm, "encap on the current session")
+    assert all(struct.unpack_from("<I", bytes(d), 4)[0] == keys[27][2] for d in dg)
+    tg.close()
+
+
+def test_failed_batch_leaves_the_pipeline_clean(gpu, monkeypatch):
+    """A batch that fails part-way (injected HIP error after chunk 1 of 5) drains both
+    staging sets; its selected packets read as failed; the next batch runs normally
+    and equals the model (counters the failed batch reserved stay consumed)."""
+    from neptun_amd import NeptunGpuError
+    rng = random.Random(41)
+    tm, tg, sessions = make_pair(gpu, rng)
+    monkeypatch.setenv("WG_TUNN_CHUNK_KB", "1024")
+    srcs = [ipv4(rng, 1350) for _ in range(3500)]  # ~5 MB: 5 chunks of 1 MiB
+    dg = [bytearray(1382) for _ in srcs]
+    monkeypatch.setenv("WG_TUNN_FAIL_CHUNK", "1")
+    with pytest.raises(NeptunGpuError):
+        tg.encapsulate_batch(srcs, dg)
+    monkeypatch.delenv("WG_TUNN_FAIL_CHUNK")
+    tm.sessions[tm.current % M.N_SESSIONS].sending_counter += len(srcs)  # reserved by the failed call
+    for batch in range(2):
+        srcs = [ipv4(rng, rng.choice([64, 1350, rng.randrange(20, 1500)])) for _ in range(3500)]
+        caps = [len(s) + 32 for s in srcs]
+        dm = [bytearray(c) for c in caps]
+        dg = [bytearray(c) for c in caps]
+        res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dm)]
+        check_same(tg.encapsulate_batch(srcs, dg), res_m, dg, dm, f"after failure {batch}")
+    # a decapsulate batch that fails before its first chunk is unpacked leaves the
+    # replay windows untouched; the next batch equals the model
+    dgs = datagrams(rng, sessions, 3500, {})
+    monkeypatch.setenv("WG_TUNN_FAIL_CHUNK", "0")
+    with pytest.raises(NeptunGpuError):
+        tg.decapsulate_batch(dgs, [bytearray(max(len(d) - 16, 0)) for d in dgs])
+    monkeypatch.delenv("WG_TUNN_FAIL_CHUNK")
+    caps = [max(len(d) - 16, 0) for d in dgs]
+    dm = [bytearray(b"\xee" * c) for c in caps]
+    dg = [bytearray(b"\xee" * c) for c in caps]
+    res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+    check_same(tg.decapsulate_batch(dgs, dg), res_m, dg, dm, "decap after failure")
     assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
     tg.close()
 

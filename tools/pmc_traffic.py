@@ -10,11 +10,14 @@ stores, write bytes = 1024 * WRITE_SIZE.  Writes a JSON summary that bench.py
 quotes as roofline.traffic.
 
     python tools/pmc_traffic.py OUT.json [--config N] [bench args...]
+
+bench.py reads profiles/pmc_traffic_config{N}.json.
 """
 import csv
 import glob
 import json
 import os
+import shutil
 import subprocess
 import sys
 from collections import defaultdict
@@ -41,6 +44,7 @@ def pmc_pass(counter, outdir, bench_args):
 
 def short(name):
     for tag in ("aead_strided_kernel<true, false>", "aead_strided_kernel<false, false>",
+                "aead_desc_sync_kernel<true>", "aead_desc_sync_kernel<false>",
                 "aead_desc_kernel<true>", "aead_desc_kernel<false>"):
         if tag in name:
             return tag
@@ -53,7 +57,8 @@ def main():
     config = 2
     if "--config" in bench_args:
         config = int(bench_args[bench_args.index("--config") + 1])
-    work = os.path.join(ROOT, "gpurun_out", "pmc_traffic")
+    work = os.path.join(ROOT, "gpurun_out", "pmc_traffic", os.path.splitext(os.path.basename(out))[0])
+    shutil.rmtree(work, ignore_errors=True)  # no stale CSVs of another config in the globs
     fetch = pmc_pass("FETCH_SIZE", work, bench_args)
     write = pmc_pass("WRITE_SIZE", work, bench_args)
     kernels = {}

@@ -5,7 +5,11 @@ instructions per wave, VALU-active fraction.  One rocprofv3 pass with
 
   clock_GHz        = GRBM_GUI_ACTIVE / 8 (XCDs) / kernel duration
   valu_per_wave    = SQ_INSTS_VALU / SQ_WAVES
-  valu_issue_frac  = 4 * SQ_ACTIVE_INST_VALU (quad-cycles) / (clock cycles * 1024 SIMDs)
+
+(SQ_ACTIVE_INST_VALU is not turned into a "busy fraction": it sums quad-cycles
+over co-resident waves, so its quotient by the SIMD cycles can exceed 1.  The
+VALU bound is tools/compute_roofline.py: issue floor at this clock vs ms.)
+bench.py reads profiles/pmc_valu_config{N}.json.
 
     python tools/pmc_valu.py OUT.json [bench args...]
     python tools/pmc_valu.py OUT.json --cmd python tools/ab.py build/variants/libX.so
@@ -14,13 +18,13 @@ import csv
 import glob
 import json
 import os
+import shutil
 import subprocess
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-COUNTERS = ["GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_SALU",
-            "SQ_INSTS_LDS"]
+COUNTERS = ["GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"]
 
 
 def short(name):
@@ -35,6 +39,7 @@ def short(name):
 def main():
     out, bench_args = sys.argv[1], sys.argv[2:]
     d = os.path.join(ROOT, "gpurun_out", "pmc_valu", os.path.splitext(os.path.basename(out))[0])
+    shutil.rmtree(d, ignore_errors=True)
     if bench_args[:1] == ["--cmd"]:  # any command, e.g. tools/ab.py on one variant library
         target = bench_args[1:]
     else:
@@ -67,7 +72,7 @@ def main():
             "valu_per_wave": c["SQ_INSTS_VALU"] / c["SQ_WAVES"],
             "salu_per_wave": c["SQ_INSTS_SALU"] / c["SQ_WAVES"],
             "lds_per_wave": c["SQ_INSTS_LDS"] / c["SQ_WAVES"],
-            "valu_issue_frac": 4 * c["SQ_ACTIVE_INST_VALU"] / (clk * t * 1024),
+            "waves": c["SQ_WAVES"],
         })
     res = {"source": "rocprofv3 --kernel-trace --pmc " + " ".join(COUNTERS) + " on bench.py " +
                      (" ".join(bench_args) or "(config 2)") + " (profiled: clocks read a few % low)",

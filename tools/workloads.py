@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from oracle.pyoracle import DESC_DTYPE
+from neptun_amd.gpu import DESC_DTYPE
 from tools import synth
 
 MIXED_SIZES = (64, 256, 576, 1350, 8900)  # BASELINE config 3
@@ -70,6 +70,19 @@ class DescBatch:
                 if not torch.equal(self.out[idx], self.pt[idx]):
                     return False
         return True
+
+    def sample(self, k: int, keys: np.ndarray, key_index: np.ndarray) -> list:
+        """k (key, receiver_idx, counter, payload, datagram) tuples spread over the batch."""
+        idx = np.unique(np.linspace(0, self.n - 1, min(k, self.n)).astype(np.int64))
+        out = []
+        for i in idx:
+            d = self.seal_host[i]
+            o, P = int(self.offs[i]), int(self.sizes[i])
+            pt = self.pt[o + 16:o + 16 + P].cpu().numpy().tobytes()
+            wire = self.wire[o:o + P + 32].cpu().numpy().tobytes()
+            slot = int(d["key_slot"])
+            out.append((keys[slot].tobytes(), int(key_index[slot]), int(d["counter"]), pt, wire))
+        return out
 
 
 def config3(per_size: int, device, seed: int = synth.SEED) -> DescBatch:
