@@ -58,6 +58,29 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_ABLATE_ZEROING 0  // timing-only: forged packets keep their plaintext
 #endif
 
+// Cache policy of the streaming traffic (every byte is read once and written
+// once): 0 = default, 1 = non-temporal ("nt": no retention in L2 / MALL).
+// The kernel is power-capped (PPT 1400 W, tools/power_probe.py), so what the
+// memory hierarchy spends per byte is clock the VALU does not get.
+#ifndef WG_LOAD_NT
+#define WG_LOAD_NT 0
+#endif
+#ifndef WG_STORE_NT
+#define WG_STORE_NT 0
+#endif
+#define WG_LOAD_CPOL (WG_LOAD_NT ? 2 : 0)    // LLVM CPol::NT (gfx940+)
+#define WG_STORE_CPOL (WG_STORE_NT ? 2 : 0)
+#if WG_STORE_NT
+#define WG_STORE_NT_ASM " nt"
+#else
+#define WG_STORE_NT_ASM ""
+#endif
+#if WG_LOAD_NT
+#define WG_LOAD_NT_ASM " nt"
+#else
+#define WG_LOAD_NT_ASM ""
+#endif
+
 #ifndef WG_SYNC_KEY_BLOCK
 #define WG_SYNC_KEY_BLOCK 1  // phase-locked Poly1305 key block on the sync paths
 #endif
@@ -217,14 +240,15 @@ __device__ __forceinline__ uint32_t lds_offset(const uint4 *p) {
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void dma_global(uint32_t lds, const uint8_t *src) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, off"
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, off" WG_LOAD_NT_ASM
                :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(src) : "memory", "m0");
 }
 #pragma clang diagnostic pop
 
 __device__ __forceinline__ void gstore16(uint8_t *dst, const uint4 v) {
   const u32x4 vv = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"(dst), "v"(vv) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off" WG_STORE_NT_ASM "\n\ts_nop 1" :: "v"(dst), "v"(vv)
+               : "memory");
 }
 
 // the first k (1..15) bytes of a chunk, through global-address-space pointers
@@ -310,7 +334,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(uint64_t base, uint3
 __device__ __forceinline__ void store16(u32x4 data, uint64_t base, uint32_t bytes, uint32_t voff,
                                         uint32_t soff) {
   const u32x4 rs = {(uint32_t)base, (uint32_t)(base >> 32) & 0xffffu, bytes, 0x00020000u};
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1"
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen" WG_STORE_NT_ASM "\n\ts_nop 1"
                :: "v"(data), "v"(voff), "s"(rs), "s"(soff) : "memory");
 }
 
@@ -335,7 +359,7 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint3
 #pragma unroll
     for (uint32_t j = 0; j < kChunks; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16, (j & 1u) ? v1 : v0,
-                                               8u * j * stride + kRun * r, 0, 0);
+                                               8u * j * stride + kRun * r, 0, WG_LOAD_CPOL);
     return;
   }
 #pragma unroll
@@ -345,7 +369,7 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint3
     const bool ok = w >= Ranges<kSeal>::in_lo() && w < hi;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16,
                                              ok ? y * stride + 16u * k : kNoAccess,
-                                             8u * j * stride + kRun * r, 0, 0);
+                                             8u * j * stride + kRun * r, 0, WG_LOAD_CPOL);
   }
 }
 
@@ -409,14 +433,15 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
 #pragma unroll
       for (uint32_t d = 0; d < 3; ++d)
         __builtin_amdgcn_raw_buffer_store_b32(wv[d], rs, 4u * (d + 1u) <= n ? base + 4u * d
-                                                                            : kNoAccess, soff, 0);
+                                                                            : kNoAccess, soff,
+                                              WG_STORE_CPOL);
       const uint32_t nd = n >> 2, rem = n & 3u;
       const uint32_t last = nd == 0 ? wv[0] : nd == 1 ? wv[1] : nd == 2 ? wv[2] : wv[3];
       __builtin_amdgcn_raw_buffer_store_b16((unsigned short)last, rs,
-                                            rem >= 2u ? base + 4u * nd : kNoAccess, soff, 0);
+                                            rem >= 2u ? base + 4u * nd : kNoAccess, soff, WG_STORE_CPOL);
       __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(last >> (8u * (rem & 2u))), rs,
                                            (rem & 1u) ? base + 4u * nd + (rem & 2u) : kNoAccess,
-                                           soff, 0);
+                                           soff, WG_STORE_CPOL);
     }
   }
 }

@@ -70,11 +70,15 @@ def main():
             ref_wire = w.clone()
         same = torch.equal(w, ref_wire)
         print(f"{name}: round-trip {'ok' if ok else 'FAIL'}, wire {'identical' if same else 'DIFFERS'}", flush=True)
+    # AB_BURST: back-to-back round trips per variant before each timed one.  The
+    # chip is power-capped (tools/power_probe.py): a burst of >= ~0.3 s lets the
+    # clock settle to what THIS variant's energy per packet allows.
+    burst = int(os.environ.get("AB_BURST", 2))
     times = {name: ([], []) for name, _, _ in libs}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     for _ in range(rounds):
         for name, L, h in libs:
-            for _ in range(2):
+            for _ in range(burst):
                 seal(L, h); open_(L, h)
             ev[0].record(); seal(L, h); ev[1].record(); open_(L, h); ev[2].record()
             torch.cuda.synchronize()

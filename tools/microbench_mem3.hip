@@ -17,6 +17,8 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #define CHECK(x)                                                                   \
   do {                                                                             \
@@ -175,8 +177,12 @@ __global__ __launch_bounds__(512) void copy_mix(const uint8_t *__restrict__ src,
   if (kMode == 1 && acc == 0x12345678u) dst[wv] = 1;
 }
 
-int main() {
+int main(int argc, char **argv) {
   const uint32_t n = 1u << 20, waves = n / 64u;
+  // `microbench_mem3 P1|FLAT|K1 SECONDS`: run one variant alone for ~SECONDS (for
+  // tools/power_probe.py: is the strided order more expensive in ENERGY?)
+  const char *only = argc > 2 ? argv[1] : nullptr;
+  const double secs = argc > 2 ? atof(argv[2]) : 0.0;
   uint8_t *src, *dst;
   CHECK(hipMalloc(&src, (size_t)n * kS + 65536));
   CHECK(hipMalloc(&dst, (size_t)n * kS + 65536));
@@ -200,6 +206,26 @@ int main() {
     return 0;
   };
   const dim3 grid((waves + 7) / 8), blk(512);
+  if (only) {
+    const uint64_t tot1 = (uint64_t)n * kLines * 128u;
+    auto launch = [&] {
+      if (!strcmp(only, "P1")) hipLaunchKernelGGL((copy_order<1, false, false>), grid, blk, 0, 0, src, dst, waves);
+      else if (!strcmp(only, "FLAT")) hipLaunchKernelGGL((copy_order<0, false, false>), grid, blk, 0, 0, src, dst, waves);
+      else hipLaunchKernelGGL((copy_k<1, 256>), dim3((uint32_t)(tot1 / 1024 / 4)), dim3(256), 0, 0, src, dst, tot1);
+    };
+    launch();
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    const int reps = (int)(secs / 0.55e-3);
+    for (int r = 0; r < reps; ++r) launch();
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    printf("{\"variant\": \"%s\", \"ms_per_copy\": %.4f, \"GBps\": %.1f}\n", only, ms / reps,
+           bytes / (ms / reps * 1e-3) / 1e9);
+    return 0;
+  }
   char name[128];
   for (uint32_t lds : {0u, 60u * 1024u}) {  // 0: up to 4 WG/CU by VGPRs; 60 KiB: 2 WG/CU (the AEAD kernels)
     const char *occ = lds ? "2WG/CU" : "free  ";
