@@ -77,6 +77,22 @@ typedef struct wg_tunn wg_tunn;
 int wg_tunn_create(wg_gpu_ctx *ctx, uint32_t first_slot, wg_tunn **out);
 int wg_tunn_destroy(wg_tunn *t);
 
+/* A Tunn whose batches are spread over several GPU contexts (normally one per
+ * GPU; several on one GPU are allowed, e.g. for tests).  Session keys are
+ * installed on every context (same key slots).  A batch reserves its sending
+ * counters once (session.rs:219) and is then split into contiguous,
+ * byte-balanced shares, one per context, that run concurrently -- each on its
+ * own host driver thread, copy threads, streams and pinned staging, bound to
+ * the GPU's NUMA node; no data is exchanged between GPUs.  Decapsulate
+ * decisions (replay window, validation, stats) are still taken in packet
+ * order, after the shares are back.  Results equal the single-context Tunn's. */
+#define WG_TUNN_MAX_ENGINES 64
+int wg_tunn_create_multi(wg_gpu_ctx *const *ctxs, uint32_t nctx, uint32_t first_slot,
+                         wg_tunn **out);
+uint32_t wg_tunn_engines(const wg_tunn *t);
+/* the HIP device and NUMA node (-1: unknown / not bound) of engine e */
+int wg_tunn_engine_info(const wg_tunn *t, uint32_t engine, int *device, int *numa_node);
+
 /* Session::new(local_index, peer_index, receiving_key, sending_key) stored at
  * sessions[local_index % 8] (mod.rs:449-452, 477-481) with session timer =
  * the Tunn's current time; make_current != 0 then runs set_current_session

@@ -16,9 +16,21 @@
 // is split over a small persistent worker pool.  Sequential semantics are
 // untouched: counters are reserved and replay/validation decisions are made
 // by one thread in packet order; only the byte copies run in parallel.
+//
+// Several GPUs (wg_tunn_create_multi): the selected packets of a
+// batch are split into contiguous, byte-balanced shares, one per GPU
+// ("engine"), AFTER the one counter reservation of the batch (session.rs:219
+// fetch_add), so the shares carry disjoint counters.  Each engine has its own
+// driver thread, copy threads and pinned staging, bound to the GPU's NUMA node
+// (sysfs numa_node of its PCI device; set_mempolicy + hipHostMallocNumaUser),
+// and its own streams.  No collective: the shares never exchange data.
 #include <hip/hip_runtime.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -128,12 +140,78 @@ size_t chunk_bytes() {  // staging bytes per pipeline chunk (WG_TUNN_CHUNK_KB ov
 }
 constexpr uint32_t kSets = 2;                     // double buffering
 
+// ---------------------------------------------------------------------------
+// NUMA placement of an engine's host side (each GPU gets its own
+// NUMA-local pinned staging and host threads).  Linux sysfs + raw syscalls:
+// the GPU's node from its PCI device, the node's CPUs from its cpulist.
+// ---------------------------------------------------------------------------
+int device_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return -1;
+  for (char *c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+  char path[160];
+  std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE *f = std::fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
+}
+
+std::vector<int> node_cpus(int node) {
+  std::vector<int> cpus;
+  char path[96];
+  std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE *f = std::fopen(path, "r");
+  if (!f) return cpus;
+  char buf[4096] = {0};
+  const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  for (char *tok = std::strtok(buf, ",\n"); tok; tok = std::strtok(nullptr, ",\n")) {
+    int a = 0, b = 0;
+    const int k = std::sscanf(tok, "%d-%d", &a, &b);
+    if (k == 1) b = a;
+    if (k >= 1)
+      for (int c = a; c <= b && c < CPU_SETSIZE; ++c) cpus.push_back(c);
+  }
+  return cpus;
+}
+
+// Pin the calling thread to the node's CPUs (intersected with what the process
+// may use) and make its page allocations prefer that node; pinned staging is
+// then allocated with hipHostMallocNumaUser so it follows this policy.
+void bind_thread_to_node(int node) {
+  if (node < 0) return;
+  cpu_set_t allowed, want;
+  CPU_ZERO(&want);
+  if (sched_getaffinity(0, sizeof allowed, &allowed) == 0) {
+    int hits = 0;
+    for (int c : node_cpus(node))
+      if (CPU_ISSET(c, &allowed)) {
+        CPU_SET(c, &want);
+        ++hits;
+      }
+    if (hits) (void)sched_setaffinity(0, sizeof want, &want);
+  }
+  unsigned long mask[16] = {0};
+  if (node < (int)(sizeof mask * 8)) {
+    mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+    (void)syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, mask, sizeof mask * 8);
+  }
+}
+
 // Persistent worker pool: run(n, fn) calls fn(lo, hi) over a split of [0, n)
 // on the workers and the calling thread, and returns when all are done.
 class Pool {
  public:
-  explicit Pool(unsigned workers) {
-    for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this, i] { loop(i + 1); });
+  Pool(unsigned workers, int node) {
+    for (unsigned i = 0; i < workers; ++i)
+      th_.emplace_back([this, i, node] {
+        bind_thread_to_node(node);
+        loop(i + 1);
+      });
   }
   ~Pool() {
     {
@@ -192,6 +270,61 @@ class Pool {
   bool stop_ = false;
 };
 
+// One persistent driver thread of a multi-device engine (pinned to the GPU's
+// NUMA node): submit() hands it a job, wait() returns the job's result.
+class Driver {
+ public:
+  explicit Driver(int node) : th_([this, node] {
+      bind_thread_to_node(node);
+      loop();
+    }) {}
+  ~Driver() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void submit(std::function<int()> job) {
+    std::lock_guard<std::mutex> lk(mu_);
+    job_ = std::move(job);
+    has_ = true;
+    done_ = false;
+    cv_.notify_all();
+  }
+  int wait() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [this] { return done_; });
+    return rc_;
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<int()> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return stop_ || has_; });
+        if (stop_) return;
+        job = std::move(job_);
+        has_ = false;
+      }
+      const int rc = job();
+      std::lock_guard<std::mutex> lk(mu_);
+      rc_ = rc;
+      done_ = true;
+      cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::function<int()> job_;
+  bool has_ = false, done_ = true, stop_ = false;
+  int rc_ = 0;
+  std::thread th_;  // last: started after the members it uses
+};
+
 // one pinned + device buffer set of the pipeline
 struct Staging {
   uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
@@ -200,7 +333,8 @@ struct Staging {
   size_t bytes = 0, descs = 0;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
-  bool busy = false;  // work enqueued and not yet waited for
+  bool busy = false;      // work enqueued and not yet waited for
+  unsigned host_flags = hipHostMallocDefault;  // + hipHostMallocNumaUser on NUMA-bound engines
 };
 
 void free_buffers(Staging &s) {
@@ -220,6 +354,7 @@ void free_buffers(Staging &s) {
 
 hipError_t reserve(Staging &s, size_t bytes, size_t descs) {
   hipError_t e = hipSuccess;
+  const unsigned fl = s.host_flags;
   if (bytes > s.bytes) {
     (void)hipHostFree(s.h_in);
     (void)hipHostFree(s.h_out);
@@ -227,8 +362,8 @@ hipError_t reserve(Staging &s, size_t bytes, size_t descs) {
     (void)hipFree(s.d_out);
     s.h_in = s.h_out = s.d_in = s.d_out = nullptr;
     s.bytes = 0;
-    if ((e = hipHostMalloc(&s.h_in, bytes)) != hipSuccess) return e;
-    if ((e = hipHostMalloc(&s.h_out, bytes)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&s.h_in, bytes, fl)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&s.h_out, bytes, fl)) != hipSuccess) return e;
     if ((e = hipMalloc(&s.d_in, bytes)) != hipSuccess) return e;
     if ((e = hipMalloc(&s.d_out, bytes)) != hipSuccess) return e;
     s.bytes = bytes;
@@ -241,8 +376,8 @@ hipError_t reserve(Staging &s, size_t bytes, size_t descs) {
     s.h_desc = s.d_desc = nullptr;
     s.h_st = s.d_st = nullptr;
     s.descs = 0;
-    if ((e = hipHostMalloc(&s.h_desc, descs * sizeof(wg_packet_desc))) != hipSuccess) return e;
-    if ((e = hipHostMalloc(&s.h_st, descs * 4)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&s.h_desc, descs * sizeof(wg_packet_desc), fl)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&s.h_st, descs * 4, fl)) != hipSuccess) return e;
     if ((e = hipMalloc(&s.d_desc, descs * sizeof(wg_packet_desc))) != hipSuccess) return e;
     if ((e = hipMalloc(&s.d_st, descs * 4)) != hipSuccess) return e;
     s.descs = descs;
@@ -255,17 +390,33 @@ struct Chunk {
   size_t k0, k1, bytes;
 };
 
-unsigned pool_workers() {
+unsigned pool_workers(unsigned engines) {
   if (const char *e = std::getenv("WG_TUNN_THREADS")) return (unsigned)std::max(1, std::atoi(e)) - 1;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  return std::min(8u, hw) - 1;  // copy threads incl. the caller
+  return std::max(1u, std::min(8u, hw / std::max(1u, engines))) - 1;  // copy threads incl. the driver
 }
+
+// The device side of a Tunn: one GPU context with its staging sets, streams
+// and host copy threads.  A Tunn has one engine per GPU it spreads batches
+// over (wg_tunn_create_multi); each engine works on a contiguous range
+// [k0, k1) of the batch's selected packets.
+struct Engine {
+  wg_gpu_ctx *ctx = nullptr;
+  int device = 0, numa = -1;
+  Staging st[kSets];
+  Pool *pool = nullptr;
+  Driver *driver = nullptr;   // multi-engine Tunns only (the single engine runs on the caller)
+  size_t k0 = 0, k1 = 0;      // this batch's share of the selected packets
+  std::vector<Chunk> chunks;
+  std::vector<uint64_t> off;  // staging offset of selected packet k0 + j inside its chunk
+  std::vector<uint64_t> dsrc, ddst;  // per selected packet: device addresses (direct mode)
+  std::vector<uint64_t> reg;         // registered ranges (host, bytes, dev), snapshot per batch
+  uint64_t tx = 0;                   // per-call tx_bytes share (summed by the caller)
+};
 
 }  // namespace
 
 struct wg_tunn {
-  wg_gpu_ctx *ctx = nullptr;
-  int device = 0;
   uint32_t first_slot = 0;  // ring slot i: receiving key first_slot + 2i, sending first_slot + 2i + 1
   Session sessions[WG_N_SESSIONS];
   uint64_t current = 0;     // index of the most recently used session (mod.rs:69)
@@ -274,14 +425,9 @@ struct wg_tunn {
   // only timer state the data plane reads (set_current_session, mod.rs:530-538)
   uint64_t time_current = 0;
   uint64_t session_timers[WG_N_SESSIONS] = {};
-  Staging st[kSets];
-  Pool *pool = nullptr;
+  std::vector<Engine *> eng;
   // per-call scratch (kept to avoid reallocations)
   std::vector<uint32_t> sel, slot;
-  std::vector<uint64_t> off;  // staging offset of each selected packet inside its chunk
-  std::vector<Chunk> chunks;
-  std::vector<uint64_t> dsrc, ddst;  // per selected packet: device addresses (direct mode)
-  std::vector<uint64_t> reg;         // registered ranges (host, bytes, dev), snapshot per batch
 };
 
 namespace {
@@ -320,46 +466,82 @@ inline void set_err(wg_tunn_result &r, int32_t st) {
 }
 
 // device address of [p, p + n) inside memory registered with wg_gpu_register_host
-// (t->reg: the batch's snapshot of the context's ranges)
-bool dev_addr(const wg_tunn *t, const void *p, uint64_t n, uint64_t &dev) {
+// on this engine's context (E.reg: the batch's snapshot of its ranges)
+bool dev_addr(const Engine &E, const void *p, uint64_t n, uint64_t &dev) {
   const uint64_t a = reinterpret_cast<uint64_t>(p);
-  size_t lo = 0, hi = t->reg.size() / 3;  // first range with host > a
+  size_t lo = 0, hi = E.reg.size() / 3;  // first range with host > a
   while (lo < hi) {
     const size_t mid = (lo + hi) / 2;
-    if (t->reg[3 * mid] <= a) lo = mid + 1;
+    if (E.reg[3 * mid] <= a) lo = mid + 1;
     else hi = mid;
   }
   if (lo == 0) return false;
-  const uint64_t *r = &t->reg[3 * (lo - 1)];
+  const uint64_t *r = &E.reg[3 * (lo - 1)];
   if (a + n > r[0] + r[1]) return false;
   dev = r[2] + (a - r[0]);
   return true;
 }
 
-
-// cut the selected packets (staging size `size(k)` each) into pipeline chunks
+// cut the engine's selected packets (staging size `size(k)` each) into pipeline chunks
 template <class SizeFn>
-void make_chunks(wg_tunn *t, SizeFn size, size_t limit = 0) {
+void make_chunks(Engine &E, SizeFn size, size_t limit = 0) {
   if (!limit) limit = chunk_bytes();
-  t->chunks.clear();
-  t->off.resize(t->sel.size());
-  size_t k0 = 0, bytes = 0;
-  for (size_t k = 0; k < t->sel.size(); ++k) {
+  E.chunks.clear();
+  E.off.resize(E.k1 - E.k0);
+  size_t k0 = E.k0, bytes = 0;
+  for (size_t k = E.k0; k < E.k1; ++k) {
     const uint64_t b = size(k);
     if (bytes && bytes + b > limit) {
-      t->chunks.push_back(Chunk{k0, k, bytes});
+      E.chunks.push_back(Chunk{k0, k, bytes});
       k0 = k;
       bytes = 0;
     }
-    t->off[k] = bytes;
+    E.off[k - E.k0] = bytes;
     bytes += b;
   }
-  if (k0 < t->sel.size()) t->chunks.push_back(Chunk{k0, t->sel.size(), bytes});
+  if (k0 < E.k1) E.chunks.push_back(Chunk{k0, E.k1, bytes});
 }
 
-// Pipeline driver: pack(c, S) fills set S for chunk c (descs + bytes), the
-// GPU runs chunk c on S's stream, unpack(c, S) consumes the results.  Chunks
-// are unpacked strictly in order.
+// Split the selected packets [0, n) into contiguous engine ranges of about
+// equal staging bytes (size(k) per packet).
+template <class SizeFn>
+void split(wg_tunn *t, SizeFn size) {
+  const size_t n = t->sel.size(), E = t->eng.size();
+  uint64_t total = 0;
+  for (size_t k = 0; k < n; ++k) total += size(k);
+  size_t k = 0;
+  uint64_t acc = 0;
+  for (size_t e = 0; e < E; ++e) {
+    t->eng[e]->k0 = k;
+    const uint64_t goal = total * (e + 1) / E;
+    while (k < n && (e + 1 == E || acc + size(k) / 2 < goal)) acc += size(k++);
+    t->eng[e]->k1 = k;
+    t->eng[e]->tx = 0;
+  }
+}
+
+// Run job(E) for every engine: on the caller when there is one engine, else
+// concurrently on the engines' NUMA-bound driver threads.  First error wins.
+int for_engines(wg_tunn *t, const std::function<int(Engine &)> &job) {
+  if (t->eng.size() == 1) {
+    DevGuard g(t->eng[0]->device);  // staging is allocated on the current device
+    return job(*t->eng[0]);
+  }
+  for (Engine *E : t->eng) {
+    Engine *e = E;
+    e->driver->submit([e, &job] {
+      DevGuard g(e->device);
+      return job(*e);
+    });
+  }
+  int rc = WG_RC_OK;
+  for (Engine *E : t->eng) {
+    const int r = E->driver->wait();
+    if (r && !rc) rc = r;
+  }
+  return rc;
+}
+
 inline double now_us() {
   return std::chrono::duration<double, std::micro>(
              std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -378,18 +560,16 @@ bool zero_copy() {
 }
 
 // direct mode is possible at all: zero-copy kernels and some registered memory
-bool direct_possible(wg_tunn *t) {
+bool direct_possible(Engine &E) {
   if (!zero_copy()) return false;
-  wg_ctx_reg_snapshot(t->ctx, t->reg);
-  return !t->reg.empty();
+  wg_ctx_reg_snapshot(E.ctx, E.reg);
+  return !E.reg.empty();
 }
 bool trace_on() {
   static const bool v = std::getenv("WG_TUNN_TRACE") != nullptr;
   return v;
 }
 
-// abs_src / abs_dst: descriptors carry absolute device addresses of registered
-// caller memory on that side (no staging bytes there)
 // Test-only fault injection: WG_TUNN_FAIL_CHUNK=c makes the batch fail with a
 // HIP error right after chunk c has been enqueued (read per call).
 int injected_failure(size_t c) {
@@ -404,11 +584,11 @@ int injected_failure(size_t c) {
 // writing the pinned staging a later reserve() would free) and `busy` cleared,
 // so the next batch starts from a clean pipeline.
 struct PipelineDrain {
-  wg_tunn *t;
-  explicit PipelineDrain(wg_tunn *tt) : t(tt) { drain(); }
+  Engine &E;
+  explicit PipelineDrain(Engine &e) : E(e) { drain(); }
   ~PipelineDrain() { drain(); }
   void drain() {
-    for (auto &S : t->st)
+    for (auto &S : E.st)
       if (S.busy) {
         (void)hipStreamSynchronize(S.stream);
         S.busy = false;
@@ -416,46 +596,51 @@ struct PipelineDrain {
   }
 };
 
+// Pipeline driver over one engine: pack(c, S) fills set S for chunk c (descs +
+// bytes), the GPU runs chunk c on S's stream, unpack(c, S) consumes the
+// results.  Chunks are unpacked strictly in order.  abs_src / abs_dst:
+// descriptors carry absolute device addresses of registered caller memory on
+// that side (no staging bytes there).
 template <class Pack, class Unpack>
-int run_chunks(wg_tunn *t, bool seal, Pack pack, Unpack unpack, bool abs_src = false,
+int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = false,
                bool abs_dst = false) {
-  PipelineDrain drain_guard(t);
-  const size_t nc = t->chunks.size();
+  PipelineDrain drain_guard(E);
+  const size_t nc = E.chunks.size();
   const bool tr = trace_on();
   const double t0 = tr ? now_us() : 0.0;
   auto wait_unpack = [&](size_t c) -> int {
-    Staging &S = t->st[c % kSets];
+    Staging &S = E.st[c % kSets];
     const double a = tr ? now_us() : 0.0;
     TUNN_HIP(hipEventSynchronize(S.done), "tunn: chunk wait");
     const double b = tr ? now_us() : 0.0;
     S.busy = false;
-    unpack(t->chunks[c], S);
+    unpack(E.chunks[c], S);
     if (tr)
-      std::fprintf(stderr, "tunn %s chunk %zu: wait %.0f us, unpack %.0f us (t=%.0f)\n",
-                   seal ? "seal" : "open", c, b - a, now_us() - b, now_us() - t0);
+      std::fprintf(stderr, "tunn dev %d %s chunk %zu: wait %.0f us, unpack %.0f us (t=%.0f)\n",
+                   E.device, seal ? "seal" : "open", c, b - a, now_us() - b, now_us() - t0);
     return WG_RC_OK;
   };
   for (size_t c = 0; c < nc; ++c) {
-    Staging &S = t->st[c % kSets];
+    Staging &S = E.st[c % kSets];
     if (S.busy) {  // chunk c - kSets still owns this set
       const int rc = wait_unpack(c - kSets);
       if (rc) return rc;
     }
-    const Chunk &ch = t->chunks[c];
+    const Chunk &ch = E.chunks[c];
     const size_t m = ch.k1 - ch.k0;
     const double pa = tr ? now_us() : 0.0;
     TUNN_HIP(reserve(S, (abs_src && abs_dst) ? 128 : ch.bytes + 128, m), "tunn: staging");
     const double pb = tr ? now_us() : 0.0;
     pack(ch, S);
     if (tr)
-      std::fprintf(stderr, "tunn %s chunk %zu: %zu B reserve %.0f us, pack %.0f us (t=%.0f)\n",
-                   seal ? "seal" : "open", c, ch.bytes, pb - pa, now_us() - pb, now_us() - t0);
+      std::fprintf(stderr, "tunn dev %d %s chunk %zu: %zu B reserve %.0f us, pack %.0f us (t=%.0f)\n",
+                   E.device, seal ? "seal" : "open", c, ch.bytes, pb - pa, now_us() - pb, now_us() - t0);
     if (zero_copy()) {
       const uint8_t *in = abs_src ? nullptr : S.h_in;
       uint8_t *out = abs_dst ? nullptr : S.h_out;
-      const int rc = seal ? wg_gpu_seal_batch(t->ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
+      const int rc = seal ? wg_gpu_seal_batch(E.ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
                                               S.stream)
-                          : wg_gpu_open_batch(t->ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
+                          : wg_gpu_open_batch(E.ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
                                               S.stream);
       if (rc) return rc;
     } else {
@@ -463,9 +648,9 @@ int run_chunks(wg_tunn *t, bool seal, Pack pack, Unpack unpack, bool abs_src = f
       TUNN_HIP(hipMemcpyAsync(S.d_desc, S.h_desc, m * sizeof(wg_packet_desc),
                               hipMemcpyHostToDevice, S.stream),
                "tunn: descs H2D");
-      const int rc = seal ? wg_gpu_seal_batch(t->ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out,
+      const int rc = seal ? wg_gpu_seal_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out,
                                               S.d_st, S.stream)
-                          : wg_gpu_open_batch(t->ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out,
+                          : wg_gpu_open_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out,
                                               S.d_st, S.stream);
       if (rc) return rc;
       TUNN_HIP(hipMemcpyAsync(S.h_out, S.d_out, ch.bytes, hipMemcpyDeviceToHost, S.stream),
@@ -476,13 +661,13 @@ int run_chunks(wg_tunn *t, bool seal, Pack pack, Unpack unpack, bool abs_src = f
     TUNN_HIP(hipEventRecord(S.done, S.stream), "tunn: event");
     S.busy = true;
     if (const int rc = injected_failure(c)) return rc;
-    if (c >= 1 && t->st[(c - 1) % kSets].busy) {  // overlap: unpack c-1 while c runs
+    if (c >= 1 && E.st[(c - 1) % kSets].busy) {  // overlap: unpack c-1 while c runs
       const int rc2 = wait_unpack(c - 1);
       if (rc2) return rc2;
     }
   }
   for (size_t c = nc >= kSets ? nc - kSets : 0; c < nc; ++c)
-    if (t->st[c % kSets].busy) {
+    if (E.st[c % kSets].busy) {
       const int rc = wait_unpack(c);
       if (rc) return rc;
     }
@@ -528,99 +713,176 @@ void validate(wg_tunn *t, const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
   r.len = ip_len;
 }
 
-// Open the selected datagrams through the pipeline.  decide(k, S, kk) runs in
-// packet order on the calling thread (kk = index inside the chunk) and returns
-// what lands in dst: 0 nothing, 1 plaintext + tag bytes, 2 zeros + tag bytes
+// Open the selected datagrams.  decide(k, S, kk) runs in packet order on one
+// thread (kk = index of packet k inside its chunk's staging S) and returns what
+// lands in dst: 0 nothing, 1 plaintext + tag bytes, 2 zeros + tag bytes
 // (session.rs:287-296: ct||tag copied into dst, opened in place, ring zeroes
-// the plaintext on a tag mismatch); the copies then run on the pool.
+// the plaintext on a tag mismatch); the copies then run on the pools.
+//  * one engine: a double-buffered chunk pipeline; each chunk is decided as it
+//    returns while the next runs on the GPU;
+//  * several engines: every engine opens its whole share at once (one chunk,
+//    in parallel on its own GPU and NUMA node); then the caller decides all
+//    packets in order; then every engine copies its share out.
 template <class Decide>
 int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *len,
                   uint8_t *const *dst, Decide decide) {
-  make_chunks(t, [&](size_t k) { return round128(len[t->sel[k]]); });
-  // direct input: every datagram 16-byte aligned inside registered memory
-  bool direct = direct_possible(t);
-  t->dsrc.resize(t->sel.size());
-  for (size_t k = 0; direct && k < t->sel.size(); ++k) {
-    const uint32_t i = t->sel[k];
-    direct = (reinterpret_cast<uint64_t>(datagram[i]) & 15u) == 0 &&
-             dev_addr(t, datagram[i], len[i], t->dsrc[k]);
-  }
-  std::vector<uint8_t> action;
-  auto pack = [&](const Chunk &ch, Staging &S) {
-    t->pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+  const bool multi = t->eng.size() > 1;
+  auto size = [&](size_t k) { return round128(len[t->sel[k]]); };
+  split(t, size);
+  auto copy_out = [&](Engine &E, const Chunk &ch, Staging &S, const std::vector<uint8_t> &action) {
+    E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
       for (size_t kk = lo; kk < hi; ++kk) {
-        const size_t k = ch.k0 + kk;
-        const uint32_t i = t->sel[k];
-        if (direct) {
-          // dst is staging: the replay decision comes after the GPU (session.rs:279-300)
-          S.h_desc[kk] = wg_packet_desc{t->dsrc[k], t->off[k] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
-        } else {
-          std::memcpy(S.h_in + t->off[k], datagram[i], len[i]);
-          S.h_desc[kk] = wg_packet_desc{t->off[k], t->off[k] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
-        }
-      }
-    });
-  };
-  auto unpack = [&](const Chunk &ch, Staging &S) {
-    action.assign(ch.k1 - ch.k0, 0);
-    for (size_t kk = 0; kk < action.size(); ++kk) action[kk] = decide(ch.k0 + kk, S, kk);
-    t->pool->run(action.size(), [&](size_t lo, size_t hi) {
-      for (size_t kk = lo; kk < hi; ++kk) {
-        if (!action[kk]) continue;
+        const uint8_t a = action[ch.k0 + kk - (multi ? 0 : ch.k0)];
+        if (!a) continue;
         const size_t k = ch.k0 + kk;
         const uint32_t i = t->sel[k];
         const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
-        if (action[kk] == 1) std::memcpy(dst[i], S.h_out + S.h_desc[kk].dst_off, P);
+        if (a == 1) std::memcpy(dst[i], S.h_out + S.h_desc[kk].dst_off, P);
         else std::memset(dst[i], 0, P);
         std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
       }
     });
   };
-  return run_chunks(t, false, pack, unpack, direct, false);
+  std::vector<uint8_t> action;
+  if (multi) action.assign(t->sel.size(), 0);
+  auto engine_job = [&](Engine &E) -> int {
+    make_chunks(E, size, multi ? ~size_t(0) : 0);
+    // direct input: every datagram 16-byte aligned inside memory registered on this engine
+    bool direct = direct_possible(E);
+    E.dsrc.resize(E.k1 - E.k0);
+    for (size_t k = E.k0; direct && k < E.k1; ++k) {
+      const uint32_t i = t->sel[k];
+      direct = (reinterpret_cast<uint64_t>(datagram[i]) & 15u) == 0 &&
+               dev_addr(E, datagram[i], len[i], E.dsrc[k - E.k0]);
+    }
+    auto pack = [&](const Chunk &ch, Staging &S) {
+      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+        for (size_t kk = lo; kk < hi; ++kk) {
+          const size_t k = ch.k0 + kk, j = k - E.k0;
+          const uint32_t i = t->sel[k];
+          if (direct) {
+            // dst is staging: the replay decision comes after the GPU (session.rs:279-300)
+            S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
+          } else {
+            std::memcpy(S.h_in + E.off[j], datagram[i], len[i]);
+            S.h_desc[kk] = wg_packet_desc{E.off[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
+          }
+        }
+      });
+    };
+    std::vector<uint8_t> act;
+    auto unpack = [&](const Chunk &ch, Staging &S) {
+      if (multi) return;  // decided after every engine is back
+      act.assign(ch.k1 - ch.k0, 0);
+      for (size_t kk = 0; kk < act.size(); ++kk) act[kk] = decide(ch.k0 + kk, S, kk);
+      copy_out(E, ch, S, act);
+    };
+    return run_chunks(E, false, pack, unpack, direct, false);
+  };
+  int rc = for_engines(t, engine_job);
+  if (rc || !multi) return rc;
+  // several engines: one chunk each, its results still in staging set 0
+  for (Engine *E : t->eng) {
+    if (E->chunks.empty()) continue;
+    for (size_t k = E->k0; k < E->k1; ++k) action[k] = decide(k, E->st[0], k - E->k0);
+  }
+  return for_engines(t, [&](Engine &E) -> int {
+    if (!E.chunks.empty()) copy_out(E, E.chunks[0], E.st[0], action);
+    return WG_RC_OK;
+  });
+}
+
+void destroy_engine(Engine *E) {
+  if (!E) return;
+  delete E->driver;  // joins the driver thread first
+  {
+    DevGuard g(E->device);
+    for (auto &S : E->st) {
+      if (S.stream) (void)hipStreamSynchronize(S.stream);
+      free_buffers(S);
+      if (S.done) (void)hipEventDestroy(S.done);
+      if (S.stream) (void)hipStreamDestroy(S.stream);
+    }
+  }
+  delete E->pool;
+  delete E;
+}
+
+int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out) {
+  Engine *E = new (std::nothrow) Engine;
+  if (!E) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: host alloc", hipSuccess);
+  E->ctx = ctx;
+  E->device = wg_ctx_device(ctx);
+  if (multi) {
+    E->numa = device_numa_node(E->device);
+    for (auto &S : E->st) S.host_flags = E->numa >= 0 ? hipHostMallocNumaUser : hipHostMallocDefault;
+  }
+  DevGuard g(E->device);
+  for (auto &S : E->st) {
+    hipError_t e = hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      destroy_engine(E);
+      return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", e);
+    }
+  }
+  E->pool = new (std::nothrow) Pool(pool_workers(engines), E->numa);
+  if (multi && E->pool) E->driver = new (std::nothrow) Driver(E->numa);
+  if (!E->pool || (multi && !E->driver)) {
+    destroy_engine(E);
+    return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: threads", hipSuccess);
+  }
+  *out = E;
+  return WG_RC_OK;
 }
 
 }  // namespace
 
 extern "C" {
 
-int wg_tunn_create(wg_gpu_ctx *ctx, uint32_t first_slot, wg_tunn **out) {
-  if (!ctx || !out) return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: null", hipSuccess);
-  if ((uint64_t)first_slot + 2 * WG_N_SESSIONS > wg_gpu_ctx_key_slots(ctx))
-    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: needs 16 key slots", hipSuccess);
+int wg_tunn_create_multi(wg_gpu_ctx *const *ctxs, uint32_t nctx, uint32_t first_slot,
+                         wg_tunn **out) {
+  if (!ctxs || !out || nctx == 0 || nctx > WG_TUNN_MAX_ENGINES)
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: bad contexts", hipSuccess);
+  for (uint32_t e = 0; e < nctx; ++e) {
+    if (!ctxs[e]) return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: null context", hipSuccess);
+    if ((uint64_t)first_slot + 2 * WG_N_SESSIONS > wg_gpu_ctx_key_slots(ctxs[e]))
+      return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: needs 16 key slots", hipSuccess);
+  }
   wg_tunn *t = new (std::nothrow) wg_tunn;
   if (!t) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: host alloc", hipSuccess);
-  t->ctx = ctx;
-  t->device = wg_ctx_device(ctx);
   t->first_slot = first_slot;
-  DevGuard g(t->device);
-  for (auto &S : t->st) {
-    hipError_t e = hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming);
-    if (e != hipSuccess) {
+  for (uint32_t e = 0; e < nctx; ++e) {
+    Engine *E = nullptr;
+    const int rc = make_engine(ctxs[e], nctx > 1, nctx, &E);
+    if (rc) {
       wg_tunn_destroy(t);
-      return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", e);
+      return rc;
     }
-  }
-  t->pool = new (std::nothrow) Pool(pool_workers());
-  if (!t->pool) {
-    wg_tunn_destroy(t);
-    return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: pool", hipSuccess);
+    t->eng.push_back(E);
   }
   *out = t;
   return WG_RC_OK;
 }
 
+int wg_tunn_create(wg_gpu_ctx *ctx, uint32_t first_slot, wg_tunn **out) {
+  if (!ctx || !out) return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: null", hipSuccess);
+  return wg_tunn_create_multi(&ctx, 1, first_slot, out);
+}
+
 int wg_tunn_destroy(wg_tunn *t) {
   if (!t) return WG_RC_OK;
-  DevGuard g(t->device);
-  for (auto &S : t->st) {
-    if (S.stream) (void)hipStreamSynchronize(S.stream);
-    free_buffers(S);
-    if (S.done) (void)hipEventDestroy(S.done);
-    if (S.stream) (void)hipStreamDestroy(S.stream);
-  }
-  delete t->pool;
+  for (Engine *E : t->eng) destroy_engine(E);
   delete t;
+  return WG_RC_OK;
+}
+
+uint32_t wg_tunn_engines(const wg_tunn *t) { return t ? (uint32_t)t->eng.size() : 0u; }
+
+int wg_tunn_engine_info(const wg_tunn *t, uint32_t engine, int *device, int *numa_node) {
+  if (!t || engine >= t->eng.size()) return WG_RC_INVALID_ARGUMENT;
+  if (device) *device = t->eng[engine]->device;
+  if (numa_node) *numa_node = t->eng[engine]->numa;
   return WG_RC_OK;
 }
 
@@ -635,9 +897,11 @@ int wg_tunn_install_session(wg_tunn *t, uint32_t local_index, uint32_t peer_inde
   std::memcpy(keys + 32, sending_key, 32);
   // receiving slot checks our index; sending slot writes the peer's (session.rs:226, :275)
   const uint32_t idx[2] = {local_index, peer_index};
-  DevGuard g(t->device);
-  const int rc = wg_gpu_set_keys(t->ctx, t->first_slot + 2 * ring, 2, keys, idx, t->st[0].stream);
-  if (rc) return rc;
+  for (Engine *E : t->eng) {  // every GPU holds the session's keys
+    DevGuard g(E->device);
+    const int rc = wg_gpu_set_keys(E->ctx, t->first_slot + 2 * ring, 2, keys, idx, E->st[0].stream);
+    if (rc) return rc;
+  }
   Session &s = t->sessions[ring];
   s = Session{};
   s.live = true;
@@ -677,7 +941,6 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   if (!t || (n && (!src || !src_len || !dst || !dst_cap || !res)))
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "encapsulate_batch: null", hipSuccess);
   if (n == 0) return WG_RC_OK;
-  DevGuard g(t->device);
   Session &s = t->sessions[t->current % WG_N_SESSIONS];  // mod.rs:310
   const uint32_t slot = t->first_slot + 2 * (uint32_t)(t->current % WG_N_SESSIONS) + 1;
   // pass 1 (host, in order): checks and counter reservation
@@ -708,56 +971,64 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   // until its chunk comes back a selected packet reads as failed (a batch that
   // errors part-way leaves no stale or zeroed results behind)
   for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);
-  const uint64_t ctr0 = s.sending_counter;  // one fetch_add per batch (session.rs:219)
+  // one fetch_add per batch (session.rs:219), BEFORE the split: every engine's
+  // packets carry counters ctr0 + k, disjoint across GPUs
+  const uint64_t ctr0 = s.sending_counter;
   s.sending_counter += t->sel.size();
-  // direct mode: src and dst of every packet 16-byte aligned inside registered
-  // memory -> the kernel reads the caller's plaintext and writes the caller's
-  // datagram over PCIe, no host copies at all (and, no staging, one launch)
-  bool direct = direct_possible(t);
-  t->dsrc.resize(t->sel.size());
-  t->ddst.resize(t->sel.size());
-  for (size_t k = 0; direct && k < t->sel.size(); ++k) {
-    const uint32_t i = t->sel[k];
-    direct = ((reinterpret_cast<uint64_t>(src[i]) | reinterpret_cast<uint64_t>(dst[i])) & 15u) == 0 &&
-             dev_addr(t, src[i], src_len[i], t->dsrc[k]) &&
-             dev_addr(t, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, t->ddst[k]);
-  }
-  make_chunks(t, [&](size_t k) { return round128((uint64_t)src_len[t->sel[k]] + WG_DATA_OVERHEAD_SZ); },
-              direct ? ~size_t(0) : 0);
-  auto pack = [&](const Chunk &ch, Staging &S) {
-    t->pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
-      for (size_t kk = lo; kk < hi; ++kk) {
-        const size_t k = ch.k0 + kk;
-        const uint32_t i = t->sel[k];
-        if (direct) {
-          S.h_desc[kk] = wg_packet_desc{t->dsrc[k], t->ddst[k], ctr0 + k, src_len[i], slot};
-        } else {
-          std::memcpy(S.h_in + t->off[k] + WG_DATA_OFFSET, src[i], src_len[i]);  // NepTUN slot layout
-          S.h_desc[kk] = wg_packet_desc{t->off[k] + WG_DATA_OFFSET, t->off[k], ctr0 + k, src_len[i], slot};
+  auto size = [&](size_t k) { return round128((uint64_t)src_len[t->sel[k]] + WG_DATA_OVERHEAD_SZ); };
+  split(t, size);
+  const int rc = for_engines(t, [&](Engine &E) -> int {
+    // direct mode: src and dst of every packet 16-byte aligned inside memory
+    // registered on this engine -> the kernel reads the caller's plaintext and
+    // writes the caller's datagram over PCIe, no host copies at all
+    bool direct = direct_possible(E);
+    E.dsrc.resize(E.k1 - E.k0);
+    E.ddst.resize(E.k1 - E.k0);
+    for (size_t k = E.k0; direct && k < E.k1; ++k) {
+      const uint32_t i = t->sel[k];
+      const size_t j = k - E.k0;
+      direct = ((reinterpret_cast<uint64_t>(src[i]) | reinterpret_cast<uint64_t>(dst[i])) & 15u) == 0 &&
+               dev_addr(E, src[i], src_len[i], E.dsrc[j]) &&
+               dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[j]);
+    }
+    make_chunks(E, size, direct ? ~size_t(0) : 0);
+    auto pack = [&](const Chunk &ch, Staging &S) {
+      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+        for (size_t kk = lo; kk < hi; ++kk) {
+          const size_t k = ch.k0 + kk, j = k - E.k0;
+          const uint32_t i = t->sel[k];
+          if (direct) {
+            S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.ddst[j], ctr0 + k, src_len[i], slot};
+          } else {
+            std::memcpy(S.h_in + E.off[j] + WG_DATA_OFFSET, src[i], src_len[i]);  // NepTUN slot layout
+            S.h_desc[kk] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr0 + k, src_len[i], slot};
+          }
         }
-      }
-    });
-  };
-  auto unpack = [&](const Chunk &ch, Staging &S) {
-    t->pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
-      for (size_t kk = lo; kk < hi; ++kk) {
-        const uint32_t i = t->sel[ch.k0 + kk];
-        const uint32_t w = src_len[i] + WG_DATA_OVERHEAD_SZ;
-        if (S.h_st[kk] != WG_STATUS_OK) {  // the GPU path has no other failure mode
-          set_err(res[i], WG_STATUS_CRYPTO_FAILED);
-          continue;
+      });
+    };
+    auto unpack = [&](const Chunk &ch, Staging &S) {
+      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+        for (size_t kk = lo; kk < hi; ++kk) {
+          const uint32_t i = t->sel[ch.k0 + kk];
+          const uint32_t w = src_len[i] + WG_DATA_OVERHEAD_SZ;
+          if (S.h_st[kk] != WG_STATUS_OK) {  // the GPU path has no other failure mode
+            set_err(res[i], WG_STATUS_CRYPTO_FAILED);
+            continue;
+          }
+          // the whole dst[..P+32]: header, ciphertext, tag (dst[16..] held src before)
+          if (!direct) std::memcpy(dst[i], S.h_out + S.h_desc[kk].dst_off, w);
+          std::memset(&res[i], 0, sizeof res[i]);
+          res[i].kind = WG_TUNN_WRITE_TO_NETWORK;
+          res[i].len = w;
         }
-        // the whole dst[..P+32]: header, ciphertext, tag (dst[16..] held src before)
-        if (!direct) std::memcpy(dst[i], S.h_out + S.h_desc[kk].dst_off, w);
-        std::memset(&res[i], 0, sizeof res[i]);
-        res[i].kind = WG_TUNN_WRITE_TO_NETWORK;
-        res[i].len = w;
-      }
-    });
-    for (size_t kk = 0; kk < ch.k1 - ch.k0; ++kk)  // mod.rs:321
-      if (S.h_st[kk] == WG_STATUS_OK) t->tx_bytes += src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
-  };
-  return run_chunks(t, true, pack, unpack, direct, direct);
+      });
+      for (size_t kk = 0; kk < ch.k1 - ch.k0; ++kk)  // mod.rs:321
+        if (S.h_st[kk] == WG_STATUS_OK) E.tx += src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
+    };
+    return run_chunks(E, true, pack, unpack, direct, direct);
+  });
+  for (Engine *E : t->eng) t->tx_bytes += E->tx;
+  return rc;
 }
 
 int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
@@ -766,7 +1037,6 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
   if (!t || (n && (!datagram || !len || !dst || !dst_cap || !res)))
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decapsulate_batch: null", hipSuccess);
   if (n == 0) return WG_RC_OK;
-  DevGuard g(t->device);
   // pass 1 (stateless checks, reference order): parse, session, dst size, index
   t->sel.clear();
   t->slot.clear();
@@ -797,7 +1067,7 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
   if (t->sel.empty()) return WG_RC_OK;
   for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);  // until its chunk returns
   // pass 2 (sequential, packet order, per chunk as it returns): replay window,
-  // validation, stats; the byte copies follow on the pool
+  // validation, stats; the byte copies follow on the pools
   return open_selected(t, datagram, len, dst, [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
     const uint32_t i = t->sel[k];
     std::memset(&res[i], 0, sizeof res[i]);
@@ -825,7 +1095,6 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
   if (!t || (n && (!datagram || !len || !dst || !dst_cap || !res)))
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decrypt_batch: null", hipSuccess);
   if (n == 0) return WG_RC_OK;
-  DevGuard g(t->device);
   t->sel.clear();
   t->slot.clear();
   for (uint32_t i = 0; i < n; ++i) {

@@ -46,6 +46,10 @@ def _bind(L):
     L.wg_tunn_install_session.argtypes = [vp, u32, u32, c.c_char_p, c.c_char_p, c.c_int]
     L.wg_tunn_stats.argtypes = [vp, c.POINTER(u64), c.POINTER(u64)]
     L.wg_tunn_set_time.argtypes = [vp, u64]
+    L.wg_tunn_create_multi.argtypes = [c.POINTER(vp), u32, u32, c.POINTER(vp)]
+    L.wg_tunn_engines.argtypes = [vp]
+    L.wg_tunn_engines.restype = u32
+    L.wg_tunn_engine_info.argtypes = [vp, u32, c.POINTER(c.c_int), c.POINTER(c.c_int)]
     L.wg_tunn_session_counters.argtypes = [vp, u32, c.POINTER(u64), c.POINTER(Replay)]
     for fn in (L.wg_tunn_encapsulate_batch, L.wg_tunn_decapsulate_batch, L.wg_tunn_decrypt_batch):
         fn.argtypes = [vp, u32, vp, vp, vp, vp, c.POINTER(TunnResult)]
@@ -71,12 +75,31 @@ class ReplayWindow:
 class Tunn:
     """Tunn mirror bound to a GpuContext; uses 16 key slots from `first_slot`."""
 
-    def __init__(self, ctx: GpuContext, first_slot: int = 0):
-        self._lib = _bind(ctx._lib)
-        self._ctx = ctx
+    def __init__(self, ctx, first_slot: int = 0):
+        """ctx: one GpuContext, or a list of them (wg_tunn_create_multi: batches are
+        split across the contexts' GPUs)."""
+        ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx]
+        self._lib = _bind(ctxs[0]._lib)
+        self._ctx = ctxs
         h = ctypes.c_void_p()
-        check(self._lib.wg_tunn_create(ctx._h, first_slot, ctypes.byref(h)), "wg_tunn_create")
+        if len(ctxs) == 1:
+            check(self._lib.wg_tunn_create(ctxs[0]._h, first_slot, ctypes.byref(h)), "wg_tunn_create")
+        else:
+            arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value if isinstance(c._h, ctypes.c_void_p) else c._h
+                                                  for c in ctxs])
+            check(self._lib.wg_tunn_create_multi(arr, len(ctxs), first_slot, ctypes.byref(h)),
+                  "wg_tunn_create_multi")
         self._h = h
+
+    def engines(self):
+        """[(device, numa_node)] of the Tunn's engines."""
+        out = []
+        for e in range(self._lib.wg_tunn_engines(self._h)):
+            d, n = ctypes.c_int(), ctypes.c_int()
+            check(self._lib.wg_tunn_engine_info(self._h, e, ctypes.byref(d), ctypes.byref(n)),
+                  "wg_tunn_engine_info")
+            out.append((d.value, n.value))
+        return out
 
     def close(self):
         if getattr(self, "_h", None):

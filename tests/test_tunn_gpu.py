@@ -414,3 +414,54 @@ def test_registered_direct_batches_match_sequential_tunn(gpu, seed):
     for a in (a_src, a_dst, a_in, a_out):
         gpu.unregister_host(a.window()[0])
     tg.close()
+
+
+def test_multi_engine_split_matches_sequential_tunn(torch_cuda):
+    """wg_tunn_create_multi over two contexts on device 0 (the 1-GPU stand-in for
+    one context per GPU): every batch is split into two byte-balanced shares that
+    run concurrently on their own driver threads, streams and pinned staging, after
+    ONE counter reservation (session.rs:219).  Results, destination bytes,
+    counters, replay windows and stats equal N sequential calls of the model."""
+    from neptun_amd import GpuContext
+    from neptun_amd.tunn import Tunn
+    rng = random.Random(51)
+    ctxs = [GpuContext(0, key_slots=64), GpuContext(0, key_slots=64)]
+    tm, tg = M.Tunn(), Tunn(ctxs, 16)
+    eng = tg.engines()
+    assert len(eng) == 2 and all(d == 0 and n >= -1 for d, n in eng)
+    sessions = []
+    for j, local in enumerate((5, 22)):
+        rk, sk, peer = rng.randbytes(32), rng.randbytes(32), rng.getrandbits(32)
+        for t in (tm, tg):
+            t.set_time(10 * (j + 1))
+            t.install_session(local, peer, rk, sk, True)
+        sessions.append((local, peer, rk, sk))
+    ctr_state = {}
+    for batch in range(3):
+        srcs = [ipv4(rng, rng.choice([64, 1350, rng.randrange(20, 1500)])) for _ in range(2500)]
+        srcs += [rng.randbytes(rng.choice([0, 17, 8900])) for _ in range(50)]
+        rng.shuffle(srcs)
+        caps = [len(s) + 32 if rng.random() > 0.02 else len(s) + 20 for s in srcs]
+        dm = [bytearray(b"\xee" * c) for c in caps]
+        dg = [bytearray(b"\xee" * c) for c in caps]
+        res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dm)]
+        check_same(tg.encapsulate_batch(srcs, dg), res_m, dg, dm, f"multi encap {batch}")
+        dgs = datagrams(rng, sessions, 2500, ctr_state)
+        caps = [max(len(d) - 16, 0) if rng.random() > 0.02 else max(len(d) - 20, 0) for d in dgs]
+        dm = [bytearray(b"\xee" * c) for c in caps]
+        dg = [bytearray(b"\xee" * c) for c in caps]
+        res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+        check_same(tg.decapsulate_batch(dgs, dg), res_m, dg, dm, f"multi decap {batch}")
+        dm = [bytearray(b"\xee" * c) for c in caps]
+        dg = [bytearray(b"\xee" * c) for c in caps]
+        res_m = [tm.decrypt(d, x) for d, x in zip(dgs, dm)]
+        check_same(tg.decrypt_batch(dgs, dg), res_m, dg, dm, f"multi decrypt {batch}")
+    for local, *_ in sessions:
+        ctr, w = tg.session_counters(local % M.N_SESSIONS)
+        sm = tm.sessions[local % M.N_SESSIONS]
+        assert ctr == sm.sending_counter
+        assert w.next == sm.window.next and list(w.bitmap) == sm.window.bitmap
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    tg.close()
+    for c in ctxs:
+        c.close()
