@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Socket-to-socket rate of the batched Tunn behind UDP (examples/udp_gateway.c):
+N x P-byte IPv4 packets through encapsulate (GPU) -> sendmmsg -> 127.0.0.1 ->
+recvmmsg -> decapsulate (GPU), for several max_inter_thread_batched_pkts-style
+batch sizes (the reference's default is 50, packet_workers.rs:27).
+
+    python tools/bench_gateway.py [N] [P] [batch ...]   -> JSON lines
+"""
+import json
+import os
+import random
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from tests.test_udp_gateway import ipv4, write_input  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    P = int(sys.argv[2]) if len(sys.argv) > 2 else 1350
+    batches = [int(b) for b in sys.argv[3:]] or [50, 256, 1024, 4096]
+    with tempfile.TemporaryDirectory() as d:
+        exe = os.path.join(d, "udp_gateway")
+        lib = os.path.join(ROOT, "neptun_amd")
+        subprocess.run(["gcc", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "examples", "udp_gateway.c"), "-L", lib, "-lneptun_gpu",
+                        f"-Wl,-rpath,{lib}", "-o", exe], check=True)
+        rng = random.Random(7)
+        inp = os.path.join(d, "in.bin")
+        write_input(inp, [ipv4(rng, P) for _ in range(n)], 11, 22, rng.randbytes(32), rng.randbytes(32))
+        for b in batches:
+            r = subprocess.run([exe, inp, os.path.join(d, "out.bin"), str(b)], capture_output=True,
+                               text=True, timeout=600)
+            line = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {
+                "error": r.stderr[-300:], "batch": b}
+            line["packet_bytes"] = P
+            print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
