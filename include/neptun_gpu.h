@@ -213,6 +213,92 @@ int wg_gpu_handshake_anon_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32
                                 wg_half_handshake *out, void *stream);
 
 /*
+ * Responder side, batched.  The reference's
+ * receive_handshake_initialization (noise/handshake.rs:527-613) holds two
+ * pieces of sequential per-peer state: the last TAI64N timestamp (replay
+ * check, :592-596) and next_index (inc_index, :508-513, consumed by
+ * format_handshake_response :853-949).  The batch API splits there:
+ *   1. wg_gpu_handshake_consume_batch: the crypto of
+ *      receive_handshake_initialization for n initiations whose peer the
+ *      caller has identified (parse_handshake_anon / its peer table): DH,
+ *      HASH/HMAC chain, AEAD-open of the static key (compared with the
+ *      peer's: WG_STATUS_WRONG_KEY) and of the timestamp.  out[i] is the
+ *      InitReceived state + the decrypted timestamp, or a status
+ *      (WRONG_PACKET_TYPE, INVALID_AEAD_TAG, WRONG_KEY).
+ *   2. the caller, in packet order: wg_handshake_timestamp_after (else
+ *      WrongTai64nTimestamp), last timestamp update, inc_index().
+ *   3. wg_gpu_handshake_respond_batch: format_handshake_response +
+ *      append_mac1_and_mac2 (:732-765) from the states: the 92-byte response
+ *      and the session keys (Session::new(local, peer, temp2, temp3), :948).
+ *      Entries whose state status != 0 are skipped (message zeroed).
+ * Under load (RateLimiter::verify_packet, rate_limiter.rs:197-218):
+ *   wg_gpu_mac2_check_batch: cookie = MAC(secret, LE64(counter) || addr) and the
+ *     mac2 check of each handshake message (len 148 or 92); status 0 valid,
+ *     1 = answer with a cookie reply; the cookie is returned.
+ *   wg_gpu_cookie_reply_batch: format_cookie_reply (rate_limiter.rs:133-170):
+ *     nonce = b2s_mac_24(nonce_key, LE64(nonce_ctr)) (the caller hands out
+ *     nonce_ctr in reply order, :112-121), XChaCha20-Poly1305(cookie_key, nonce,
+ *     aad = mac1, cookie) -> 64-byte COOKIE_REPLY messages.
+ * Device pointers for the arrays, host pointers for the 16/32-byte keys.
+ */
+typedef struct wg_responder_peer {
+  uint8_t peer_static_public[32];  /* NoiseParams::peer_static_public */
+  uint8_t static_shared[32];       /* NoiseParams::static_shared = DH(static_private, peer_static_public) */
+} wg_responder_peer;
+
+typedef struct wg_init_received {  /* HandshakeState::InitReceived + the timestamp */
+  int32_t status;
+  uint32_t peer_index;
+  uint8_t timestamp[12];           /* TAI64N, big-endian seconds then nanoseconds */
+  uint8_t chaining_key[32];
+  uint8_t hash[32];
+  uint8_t peer_ephemeral[32];
+  uint8_t pad[12];
+} wg_init_received;                /* 128 bytes */
+
+typedef struct wg_response_job {
+  uint8_t ephemeral_private[32];   /* DH_GENERATE() (random, from the caller) */
+  uint8_t peer_static_public[32];
+  uint8_t preshared_key[32];       /* zeros when the peer has none (handshake.rs:920) */
+  uint8_t mac1_key[32];            /* HASH(LABEL_MAC1 || peer_static_public) */
+  uint8_t cookie[16];              /* cookies.write_cookie, when has_cookie */
+  uint32_t local_index;            /* inc_index() */
+  uint32_t has_cookie;
+  uint8_t pad[8];
+} wg_response_job;                 /* 160 bytes */
+
+typedef struct wg_response_out {
+  uint8_t message[92];             /* HANDSHAKE_RESP incl. mac1 / mac2 */
+  uint8_t pad[4];
+  uint8_t receiving_key[32];       /* temp2 */
+  uint8_t sending_key[32];         /* temp3 */
+  uint8_t mac1[16];                /* cookies.last_mac1 */
+} wg_response_out;                 /* 176 bytes */
+
+typedef struct wg_cookie_reply_job {
+  uint8_t cookie[16];
+  uint8_t mac1[16];                /* mac1 of the message being answered (the AAD) */
+  uint64_t nonce_ctr;
+  uint32_t receiver_idx;           /* the message's sender index */
+  uint32_t pad;
+} wg_cookie_reply_job;             /* 48 bytes */
+
+int wg_gpu_handshake_consume_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32], uint32_t n,
+                                   const uint8_t *msgs, uint64_t stride,
+                                   const wg_responder_peer *peers, wg_init_received *out,
+                                   void *stream);
+/* Tai64N::after (handshake.rs:267-269): 1 if ts is strictly later than last */
+int wg_handshake_timestamp_after(const uint8_t ts[12], const uint8_t last[12]);
+int wg_gpu_handshake_respond_batch(wg_gpu_ctx *ctx, uint32_t n, const wg_init_received *states,
+                                   const wg_response_job *jobs, wg_response_out *out, void *stream);
+int wg_gpu_mac2_check_batch(wg_gpu_ctx *ctx, const uint8_t secret_key[16], uint64_t cookie_counter,
+                            uint32_t n, const uint8_t *msgs, uint64_t stride, const uint32_t *lens,
+                            const uint8_t *addrs, uint8_t *cookies, int32_t *status, void *stream);
+int wg_gpu_cookie_reply_batch(wg_gpu_ctx *ctx, const uint8_t cookie_key[32],
+                              const uint8_t nonce_key[32], uint32_t n,
+                              const wg_cookie_reply_job *jobs, uint8_t *out, void *stream);
+
+/*
  * Host memory registration (hipHostRegister, mapped) for copy-free batches:
  * the kernels can then address the caller's buffers directly (absolute
  * device addresses in descriptors with NULL src / dst bases, or the Tunn

@@ -59,27 +59,28 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #endif
 
 // Cache policy of the streaming traffic (every byte is read once and written
-// once): 0 = default, 1 = non-temporal ("nt": no retention in L2 / MALL).
-// The kernel is power-capped (PPT 1400 W, tools/power_probe.py), so what the
-// memory hierarchy spends per byte is clock the VALU does not get.
-#ifndef WG_LOAD_NT
-#define WG_LOAD_NT 0
+// once), as LLVM CPol bits for gfx940+: 1 = sc0, 2 = nt, 16 = sc1 (and sums).
+// The kernels are power-capped (PPT 1400 W, profiles/r02_power.json), so what
+// the memory hierarchy spends per byte is clock the VALU does not get; the
+// default policy measured best (nt on loads and/or stores: -8 %, tools/ab.py).
+#ifndef WG_LOAD_CPOL
+#define WG_LOAD_CPOL 0
 #endif
-#ifndef WG_STORE_NT
-#define WG_STORE_NT 0
+#ifndef WG_STORE_CPOL
+#define WG_STORE_CPOL 0
 #endif
-#define WG_LOAD_CPOL (WG_LOAD_NT ? 2 : 0)    // LLVM CPol::NT (gfx940+)
-#define WG_STORE_CPOL (WG_STORE_NT ? 2 : 0)
-#if WG_STORE_NT
-#define WG_STORE_NT_ASM " nt"
-#else
-#define WG_STORE_NT_ASM ""
-#endif
-#if WG_LOAD_NT
-#define WG_LOAD_NT_ASM " nt"
-#else
-#define WG_LOAD_NT_ASM ""
-#endif
+#define WG_CPOL_ASM_0 ""
+#define WG_CPOL_ASM_1 " sc0"
+#define WG_CPOL_ASM_2 " nt"
+#define WG_CPOL_ASM_3 " sc0 nt"
+#define WG_CPOL_ASM_16 " sc1"
+#define WG_CPOL_ASM_17 " sc0 sc1"
+#define WG_CPOL_ASM_18 " nt sc1"
+#define WG_CPOL_ASM_19 " sc0 nt sc1"
+#define WG_CPOL_ASM_(x) WG_CPOL_ASM_##x
+#define WG_CPOL_ASM(x) WG_CPOL_ASM_(x)
+#define WG_LOAD_NT_ASM WG_CPOL_ASM(WG_LOAD_CPOL)
+#define WG_STORE_NT_ASM WG_CPOL_ASM(WG_STORE_CPOL)
 
 #ifndef WG_SYNC_KEY_BLOCK
 #define WG_SYNC_KEY_BLOCK 1  // phase-locked Poly1305 key block on the sync paths

@@ -91,8 +91,44 @@ struct HandshakeAnonParams {
   uint32_t hash0[8];           // HASH(INITIAL_CHAIN_HASH || static_public)
   uint32_t mac1_key[8];        // HASH(LABEL_MAC1 || static_public)
 };
+struct HandshakeConsumeParams {
+  const uint8_t *msgs;  // n handshake initiations, 148 bytes each at `stride`
+  uint64_t stride;
+  const wg_responder_peer *peers;
+  wg_init_received *out;
+  uint32_t n;
+  uint32_t static_private[8];
+  uint32_t hash0[8];  // HASH(INITIAL_CHAIN_HASH || static_public)
+};
+struct HandshakeRespondParams {
+  const wg_init_received *states;
+  const wg_response_job *jobs;
+  wg_response_out *out;
+  uint32_t n;
+};
+struct Mac2CheckParams {
+  const uint8_t *msgs;
+  uint64_t stride;
+  const uint32_t *lens;
+  const uint8_t *addrs;  // 16 bytes each
+  uint8_t *cookies;      // 16 bytes each (out)
+  int32_t *status;       // out: 0 valid mac2, 1 cookie reply needed
+  uint64_t counter;      // cur_counter (rate_limiter.rs:104)
+  uint32_t n;
+  uint32_t secret[4];
+};
+struct CookieReplyParams {
+  const wg_cookie_reply_job *jobs;
+  uint8_t *out;  // 64 bytes each
+  uint32_t n;
+  uint32_t cookie_key[8], nonce_key[8];
+};
 __global__ void x25519_kernel(uint32_t n, const uint8_t *scalars, const uint8_t *points,
                               uint8_t *out);
 __global__ void handshake_anon_kernel(HandshakeAnonParams prm);
+__global__ void handshake_consume_kernel(HandshakeConsumeParams prm);
+__global__ void handshake_respond_kernel(HandshakeRespondParams prm);
+__global__ void mac2_check_kernel(Mac2CheckParams prm);
+__global__ void cookie_reply_kernel(CookieReplyParams prm);
 
 }  // namespace wg

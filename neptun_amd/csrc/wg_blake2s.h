@@ -126,5 +126,39 @@ WG_HD void mac16_116(uint32_t out[4], const uint32_t key[8], const uint32_t msg[
   for (int i = 0; i < 4; ++i) out[i] = h[i];
 }
 
+// BLAKE2s-256(a[8] || b[0..blen)) for blen <= 64 (b as zero-padded words) --
+// b2s_hash(hash, data) of the handshake with a 32-byte chaining hash first
+WG_HD void hash_cat(uint32_t out[8], const uint32_t a[8], const uint32_t b[16], uint32_t blen) {
+  uint32_t m[16];
+  init(out, 32, 0);
+  if (blen <= 32) {
+    for (int i = 0; i < 16; ++i) m[i] = i < 8 ? a[i] : b[i - 8];
+    compress(out, m, 32 + blen, true);
+    return;
+  }
+  for (int i = 0; i < 16; ++i) m[i] = i < 8 ? a[i] : b[i - 8];
+  compress(out, m, 64, false);
+  for (int i = 0; i < 16; ++i) m[i] = i < 8 ? b[8 + i] : 0u;
+  compress(out, m, 32 + blen, true);
+}
+
+// Keyed BLAKE2s (RFC 7693 MAC mode) with an outlen-byte digest over dlen bytes
+// given as zero-padded words (words past dlen must read as 0 up to the next
+// 64-byte boundary): Blake2sMac -- b2s_keyed_mac_16 / _16_2 / b2s_mac_24
+// (handshake.rs:74-97).  keylen is 16 or 32 (key words past it are ignored).
+WG_HD void keyed_mac(uint32_t *out, uint32_t outlen, const uint32_t key[8], uint32_t keylen,
+                     const uint32_t *data, uint32_t dlen) {
+  uint32_t h[8], m[16];
+  init(h, outlen, keylen);
+  for (int i = 0; i < 16; ++i) m[i] = i < (int)(keylen / 4) ? key[i] : 0u;
+  compress(h, m, 64, dlen == 0);
+  for (uint32_t off = 0; off < dlen; off += 64) {
+    const bool last = off + 64 >= dlen;
+    for (int i = 0; i < 16; ++i) m[i] = off + 4u * i < dlen ? data[off / 4 + i] : 0u;
+    compress(h, m, 64 + (last ? dlen : off + 64), last);
+  }
+  for (uint32_t i = 0; i < outlen / 4; ++i) out[i] = h[i];
+}
+
 }  // namespace b2s
 }  // namespace wg

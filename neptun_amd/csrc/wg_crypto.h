@@ -59,6 +59,24 @@ __device__ __forceinline__ void chacha20_block(uint32_t ks[16], const uint32_t k
   ks[12] = x12 + blk; ks[13] = x13; ks[14] = x14 + n1; ks[15] = x15 + n2;
 }
 
+// HChaCha20 (draft-irtf-cfrg-xchacha 2.2): the 20 rounds over (sigma, key,
+// n[0..3]) without the feed-forward; out = words 0-3 and 12-15.  The subkey of
+// XChaCha20-Poly1305 (chacha20poly1305 0.10, the cookie AEAD of
+// rate_limiter.rs:156-164 / handshake.rs:719).
+__device__ __forceinline__ void hchacha20(uint32_t out[8], const uint32_t k[8], const uint32_t n[4]) {
+  uint32_t x0 = kSigma0, x1 = kSigma1, x2 = kSigma2, x3 = kSigma3;
+  uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3];
+  uint32_t x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+  uint32_t x12 = n[0], x13 = n[1], x14 = n[2], x15 = n[3];
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
+    WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
+  }
+  out[0] = x0; out[1] = x1; out[2] = x2; out[3] = x3;
+  out[4] = x12; out[5] = x13; out[6] = x14; out[7] = x15;
+}
+
 // ---------------------------------------------------------------------------
 // Two consecutive keystream blocks in phase-locked steps.
 //

@@ -120,4 +120,290 @@ __global__ __launch_bounds__(256) void handshake_anon_kernel(HandshakeAnonParams
   prm.out[i] = r;
 }
 
+// ---------------------------------------------------------------------------
+// Responder side: receive_handshake_initialization split where
+// the reference's sequential state sits between its halves -- the device does
+// the crypto, the host keeps the TAI64N replay comparison and inc_index().
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ld_words(uint32_t *w, const uint8_t *p, int n) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+  for (int j = 0; j < n; ++j) w[j] = q[j];
+}
+__device__ __forceinline__ void st_words(uint8_t *p, const uint32_t *w, int n) {
+  uint32_t *q = reinterpret_cast<uint32_t *>(p);
+  for (int j = 0; j < n; ++j) q[j] = w[j];
+}
+__device__ __forceinline__ void hmac_1(uint32_t out[8], const uint32_t key[8], uint32_t byte) {
+  uint32_t d[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d[j] = j == 0 ? byte : 0u;
+  b2s::hmac(out, key, d, 1);
+}
+__device__ __forceinline__ void hmac_32(uint32_t out[8], const uint32_t key[8], const uint32_t a[8]) {
+  uint32_t d[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d[j] = j < 8 ? a[j] : 0u;
+  b2s::hmac(out, key, d, 32);
+}
+// b2s_hmac2(key, a(32 bytes), [byte]) (handshake.rs:58-72)
+__device__ __forceinline__ void hmac_33(uint32_t out[8], const uint32_t key[8], const uint32_t a[8],
+                                        uint32_t byte) {
+  uint32_t d[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d[j] = j < 8 ? a[j] : (j == 8 ? byte : 0u);
+  b2s::hmac(out, key, d, 33);
+}
+// RFC 8439 AEAD tag over a 32-byte AAD and `ct_len` <= 32 bytes of ciphertext
+// (zero-padded words), key block 0 of (key, nonce 0): aead_chacha20_seal/open
+// of handshake.rs:101-193 for the handshake's short messages.
+__device__ __forceinline__ void tag_aad32(uint32_t tag[4], const uint32_t key[8], const uint32_t aad[8],
+                                          const uint32_t ct[8], uint32_t ct_len) {
+  uint32_t ks[16];
+  chacha20_block(ks, key, 0u, 0u, 0u);
+  Poly poly;
+  poly_init(poly, ks);
+  const uint32_t s[4] = {ks[4], ks[5], ks[6], ks[7]};
+  poly_block(poly, aad[0], aad[1], aad[2], aad[3]);
+  poly_block(poly, aad[4], aad[5], aad[6], aad[7]);
+  if (ct_len > 0) poly_block(poly, ct[0], ct[1], ct[2], ct[3]);  // (pad16 zero-fills)
+  if (ct_len > 16) poly_block(poly, ct[4], ct[5], ct[6], ct[7]);
+  poly_block(poly, 32u, 0u, ct_len, 0u);
+  poly_finish(poly, s, tag);
+}
+
+__global__ __launch_bounds__(256) void handshake_consume_kernel(HandshakeConsumeParams prm) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= prm.n) return;
+  uint32_t w[37];
+  ld_words(w, prm.msgs + prm.stride * i, 37);
+  const wg_responder_peer &peer = prm.peers[i];
+  uint32_t eph[8], h[8], t[8], ck[8], dh[8], key[8], d[16], tag[4], ks[16];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) eph[j] = w[2 + j];
+  // hash = HASH(HASH(INITIAL_CHAIN_HASH || static_public) || ephemeral)
+  b2s::hash64(h, prm.hash0, eph);
+  // chaining_key = HMAC(HMAC(INITIAL_CHAIN_KEY, ephemeral), 0x1)
+  uint32_t ck0[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ck0[j] = kChainKey0[j];
+  hmac_32(t, ck0, eph);
+  hmac_1(ck, t, 1u);
+  // temp = HMAC(ck, DH(static_private, ephemeral)); ck = HMAC(temp, 1); key = HMAC(temp, ck || 2)
+  x25519::scalarmult(dh, prm.static_private, eph);
+  hmac_32(t, ck, dh);
+  hmac_1(ck, t, 1u);
+  hmac_33(key, t, ck, 2u);
+  // open encrypted_static (AAD = hash), compare with the configured peer (handshake.rs:562-577)
+  int32_t status = w[0] == 1u ? WG_STATUS_OK : WG_STATUS_WRONG_PACKET_TYPE;
+  uint32_t ct[8], pk[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ct[j] = w[10 + j];
+  tag_aad32(tag, key, h, ct, 32);
+  if (status == WG_STATUS_OK && ((tag[0] ^ w[18]) | (tag[1] ^ w[19]) | (tag[2] ^ w[20]) | (tag[3] ^ w[21])))
+    status = WG_STATUS_INVALID_AEAD_TAG;
+  chacha20_block(ks, key, 1u, 0u, 0u);
+  uint32_t want[8], diff = 0;
+  ld_words(reinterpret_cast<uint32_t *>(want), peer.peer_static_public, 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    pk[j] = ct[j] ^ ks[j];
+    diff |= pk[j] ^ want[j];
+  }
+  if (status == WG_STATUS_OK && diff) status = WG_STATUS_WRONG_KEY;
+  // hash = HASH(hash || encrypted_static (48 bytes))
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d[j] = j < 12 ? w[10 + j] : 0u;
+  uint32_t h2[8];
+  b2s::hash_cat(h2, h, d, 48);
+  // temp = HMAC(ck, static_shared); ck = HMAC(temp, 1); key = HMAC(temp, ck || 2)
+  uint32_t ss[8];
+  ld_words(ss, peer.static_shared, 8);
+  hmac_32(t, ck, ss);
+  hmac_1(ck, t, 1u);
+  hmac_33(key, t, ck, 2u);
+  // open encrypted_timestamp (12 + 16 bytes, AAD = hash)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ct[j] = j < 3 ? w[22 + j] : 0u;
+  tag_aad32(tag, key, h2, ct, 12);
+  if (status == WG_STATUS_OK && ((tag[0] ^ w[25]) | (tag[1] ^ w[26]) | (tag[2] ^ w[27]) | (tag[3] ^ w[28])))
+    status = WG_STATUS_INVALID_AEAD_TAG;
+  chacha20_block(ks, key, 1u, 0u, 0u);
+  uint32_t ts[3] = {w[22] ^ ks[0], w[23] ^ ks[1], w[24] ^ ks[2]};
+  // hash = HASH(hash || encrypted_timestamp (28 bytes))
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d[j] = j < 7 ? w[22 + j] : 0u;
+  b2s::hash_cat(h, h2, d, 28);
+  wg_init_received &o = prm.out[i];
+  const bool ok = status == WG_STATUS_OK;
+  o.status = status;
+  o.peer_index = status == WG_STATUS_WRONG_PACKET_TYPE ? 0u : w[1];
+  uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  st_words(o.timestamp, ok ? ts : z, 3);
+  st_words(o.chaining_key, ok ? ck : z, 8);
+  st_words(o.hash, ok ? h : z, 8);
+  st_words(o.peer_ephemeral, ok ? eph : z, 8);
+}
+
+__constant__ uint32_t kBasePoint[8] = {9u, 0, 0, 0, 0, 0, 0, 0};
+
+__global__ __launch_bounds__(256) void handshake_respond_kernel(HandshakeRespondParams prm) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= prm.n) return;
+  const wg_init_received &st = prm.states[i];
+  const wg_response_job &job = prm.jobs[i];
+  wg_response_out &o = prm.out[i];
+  if (st.status != WG_STATUS_OK) {
+    uint32_t z[23] = {0};
+    st_words(o.message, z, 23);
+    return;
+  }
+  uint32_t ck[8], h[8], peph[8], e[8], epub[8], t[8], dh[8], d[16];
+  ld_words(ck, st.chaining_key, 8);
+  ld_words(h, st.hash, 8);
+  ld_words(peph, st.peer_ephemeral, 8);
+  ld_words(e, job.ephemeral_private, 8);
+  uint32_t base[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) base[j] = kBasePoint[j];
+  x25519::scalarmult(epub, e, base);  // DH_PUBKEY(responder.ephemeral_private)
+  // hash = HASH(hash || eph_pub); temp = HMAC(ck, eph_pub); ck = HMAC(temp, 1)
+  b2s::hash64(d, h, epub);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = d[j];
+  hmac_32(t, ck, epub);
+  hmac_1(ck, t, 1u);
+  // DH(eph, initiator ephemeral), then DH(eph, initiator static)
+  x25519::scalarmult(dh, e, peph);
+  hmac_32(t, ck, dh);
+  hmac_1(ck, t, 1u);
+  uint32_t pst[8];
+  ld_words(pst, job.peer_static_public, 8);
+  x25519::scalarmult(dh, e, pst);
+  hmac_32(t, ck, dh);
+  hmac_1(ck, t, 1u);
+  // psk (zeros when none, handshake.rs:920)
+  uint32_t psk[8], temp[8], temp2[8], key[8];
+  ld_words(psk, job.preshared_key, 8);
+  hmac_32(temp, ck, psk);
+  hmac_1(ck, temp, 1u);
+  hmac_33(temp2, temp, ck, 2u);
+  hmac_33(key, temp, temp2, 3u);
+  b2s::hash64(d, h, temp2);
+  // encrypted_nothing = AEAD(key, 0, [], hash)
+  uint32_t tag[4], none[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  tag_aad32(tag, key, d, none, 0);
+  // message: type 2 | sender (ours) | receiver (theirs) | eph_pub | tag | mac1 | mac2
+  uint32_t m[23];
+  m[0] = 2u;  // HANDSHAKE_RESP
+  m[1] = job.local_index;
+  m[2] = st.peer_index;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[3 + j] = epub[j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[11 + j] = tag[j];
+  uint32_t mk[8], mac1[4], mac2[4] = {0, 0, 0, 0};
+  ld_words(mk, job.mac1_key, 8);
+  b2s::keyed_mac(mac1, 16, mk, 32, m, 60);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[15 + j] = mac1[j];
+  if (job.has_cookie) {
+    uint32_t ckey[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    ld_words(ckey, job.cookie, 4);
+    uint32_t mm[20];
+#pragma unroll
+    for (int j = 0; j < 20; ++j) mm[j] = j < 19 ? m[j] : 0u;
+    b2s::keyed_mac(mac2, 16, ckey, 16, mm, 76);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[19 + j] = mac2[j];
+  st_words(o.message, m, 23);
+  // session keys: temp1 = HMAC(ck, []), temp2 = HMAC(temp1, 1), temp3 = HMAC(temp1, temp2 || 2)
+  uint32_t t1[8], t2[8], t3[8], empty[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) empty[j] = 0u;
+  b2s::hmac(t1, ck, empty, 0);
+  hmac_1(t2, t1, 1u);
+  hmac_33(t3, t1, t2, 2u);
+  st_words(o.receiving_key, t2, 8);  // Session::new(local, peer, temp2, temp3) (handshake.rs:948)
+  st_words(o.sending_key, t3, 8);
+  st_words(o.mac1, mac1, 4);
+}
+
+// Under load (rate_limiter.rs:197-218): cookie = MAC(secret, LE64(counter) || addr)
+// and the mac2 check over msg[..len - 16]; status 0 = valid mac2, 1 = reply with a cookie.
+__global__ __launch_bounds__(256) void mac2_check_kernel(Mac2CheckParams prm) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= prm.n) return;
+  const uint32_t len = prm.lens[i];
+  uint32_t w[37];
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(prm.msgs + prm.stride * i);
+#pragma unroll
+  for (int j = 0; j < 37; ++j) w[j] = 4u * j < len ? q[j] : 0u;
+  uint32_t cin[16] = {0}, cookie[4], key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  cin[0] = (uint32_t)prm.counter;
+  cin[1] = (uint32_t)(prm.counter >> 32);
+  ld_words(cin + 2, prm.addrs + 16ull * i, 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) key[j] = prm.secret[j];
+  b2s::keyed_mac(cookie, 16, key, 16, cin, 24);
+  uint32_t ck8[8] = {cookie[0], cookie[1], cookie[2], cookie[3], 0, 0, 0, 0}, mac2[4];
+  // msg[..len - 16] = message + mac1; zero the words past it (len - 16 is a multiple of 4)
+  const uint32_t mlen = len - 16u;
+#pragma unroll
+  for (int j = 0; j < 37; ++j) w[j] = 4u * j < mlen ? w[j] : 0u;
+  b2s::keyed_mac(mac2, 16, ck8, 16, w, mlen);
+  const uint32_t k = mlen / 4u;
+  uint32_t diff = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) diff |= mac2[j] ^ q[k + j];
+  prm.status[i] = diff ? 1 : 0;
+  st_words(prm.cookies + 16ull * i, cookie, 4);
+}
+
+// format_cookie_reply (rate_limiter.rs:133-170): nonce = b2s_mac_24(nonce_key,
+// LE64(ctr)); XChaCha20-Poly1305(cookie_key, nonce, aad = mac1, cookie).
+__global__ __launch_bounds__(256) void cookie_reply_kernel(CookieReplyParams prm) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= prm.n) return;
+  const wg_cookie_reply_job &job = prm.jobs[i];
+  uint32_t nk[8], nin[16] = {0}, nonce[6];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) nk[j] = prm.nonce_key[j];
+  nin[0] = (uint32_t)job.nonce_ctr;
+  nin[1] = (uint32_t)(job.nonce_ctr >> 32);
+  b2s::keyed_mac(nonce, 24, nk, 32, nin, 8);
+  uint32_t ckey[8], sub[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ckey[j] = prm.cookie_key[j];
+  hchacha20(sub, ckey, nonce);
+  // RFC 8439 with nonce 0^4 || nonce[16..24): block 0 -> Poly key, block 1 -> keystream
+  uint32_t ks[16];
+  chacha20_block(ks, sub, 0u, nonce[4], nonce[5]);
+  Poly poly;
+  poly_init(poly, ks);
+  const uint32_t s[4] = {ks[4], ks[5], ks[6], ks[7]};
+  uint32_t mac1[4], cookie[4], ct[4];
+  ld_words(mac1, job.mac1, 4);
+  ld_words(cookie, job.cookie, 4);
+  chacha20_block(ks, sub, 1u, nonce[4], nonce[5]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ct[j] = cookie[j] ^ ks[j];
+  poly_block(poly, mac1[0], mac1[1], mac1[2], mac1[3]);  // AAD (16 bytes)
+  poly_block(poly, ct[0], ct[1], ct[2], ct[3]);
+  poly_block(poly, 16u, 0u, 16u, 0u);
+  uint32_t tag[4];
+  poly_finish(poly, s, tag);
+  uint32_t m[16];
+  m[0] = 3u;  // COOKIE_REPLY
+  m[1] = job.receiver_idx;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) m[2 + j] = nonce[j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    m[8 + j] = ct[j];
+    m[12 + j] = tag[j];
+  }
+  st_words(prm.out + 64ull * i, m, 16);
+}
+
 }  // namespace wg

@@ -94,4 +94,104 @@ int wg_gpu_handshake_anon_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32
                          : wg_pipe_fail(WG_RC_HIP_ERROR, "handshake_anon_batch: launch", e);
 }
 
+int wg_gpu_handshake_consume_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32], uint32_t n,
+                                   const uint8_t *msgs, uint64_t stride,
+                                   const wg_responder_peer *peers, wg_init_received *out,
+                                   void *stream) {
+  if (!ctx || !static_private || (n && (!msgs || !peers || !out)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "handshake_consume_batch: null argument", hipSuccess);
+  if (stride < 148 || (stride & 3u) || (((uintptr_t)msgs | (uintptr_t)peers | (uintptr_t)out) & 3u))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT,
+                        "handshake_consume_batch: stride >= 148 and 4-byte alignment required",
+                        hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  wg::HandshakeConsumeParams prm{};
+  prm.msgs = msgs;
+  prm.stride = stride;
+  prm.peers = peers;
+  prm.out = out;
+  prm.n = n;
+  std::memcpy(prm.static_private, static_private, 32);
+  uint32_t base[8] = {9, 0, 0, 0, 0, 0, 0, 0}, pub[8], ich[8];
+  wg::x25519::scalarmult(pub, prm.static_private, base);
+  initial_chain_hash(ich);
+  wg::b2s::hash64(prm.hash0, ich, pub);
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::handshake_consume_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), prm);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK
+                         : wg_pipe_fail(WG_RC_HIP_ERROR, "handshake_consume_batch: launch", e);
+}
+
+int wg_handshake_timestamp_after(const uint8_t ts[12], const uint8_t last[12]) {
+  return std::memcmp(ts, last, 12) > 0 ? 1 : 0;  // big-endian (secs, nanos): bytewise order
+}
+
+int wg_gpu_handshake_respond_batch(wg_gpu_ctx *ctx, uint32_t n, const wg_init_received *states,
+                                   const wg_response_job *jobs, wg_response_out *out, void *stream) {
+  if (!ctx || (n && (!states || !jobs || !out)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "handshake_respond_batch: null argument", hipSuccess);
+  if (((uintptr_t)states | (uintptr_t)jobs | (uintptr_t)out) & 7u)
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "handshake_respond_batch: 8-byte alignment required",
+                        hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  wg::HandshakeRespondParams prm{states, jobs, out, n};
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::handshake_respond_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), prm);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK
+                         : wg_pipe_fail(WG_RC_HIP_ERROR, "handshake_respond_batch: launch", e);
+}
+
+int wg_gpu_mac2_check_batch(wg_gpu_ctx *ctx, const uint8_t secret_key[16], uint64_t cookie_counter,
+                            uint32_t n, const uint8_t *msgs, uint64_t stride, const uint32_t *lens,
+                            const uint8_t *addrs, uint8_t *cookies, int32_t *status, void *stream) {
+  if (!ctx || !secret_key || (n && (!msgs || !lens || !addrs || !cookies || !status)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "mac2_check_batch: null argument", hipSuccess);
+  if (stride < 148 || (stride & 3u) ||
+      (((uintptr_t)msgs | (uintptr_t)addrs | (uintptr_t)cookies) & 3u))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT,
+                        "mac2_check_batch: stride >= 148 and 4-byte alignment required", hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  wg::Mac2CheckParams prm{};
+  prm.msgs = msgs;
+  prm.stride = stride;
+  prm.lens = lens;
+  prm.addrs = addrs;
+  prm.cookies = cookies;
+  prm.status = status;
+  prm.counter = cookie_counter;
+  prm.n = n;
+  std::memcpy(prm.secret, secret_key, 16);
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::mac2_check_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), prm);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK : wg_pipe_fail(WG_RC_HIP_ERROR, "mac2_check_batch: launch", e);
+}
+
+int wg_gpu_cookie_reply_batch(wg_gpu_ctx *ctx, const uint8_t cookie_key[32],
+                              const uint8_t nonce_key[32], uint32_t n,
+                              const wg_cookie_reply_job *jobs, uint8_t *out, void *stream) {
+  if (!ctx || !cookie_key || !nonce_key || (n && (!jobs || !out)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "cookie_reply_batch: null argument", hipSuccess);
+  if (((uintptr_t)jobs | (uintptr_t)out) & 7u)
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "cookie_reply_batch: 8-byte alignment required",
+                        hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  wg::CookieReplyParams prm{};
+  prm.jobs = jobs;
+  prm.out = out;
+  prm.n = n;
+  std::memcpy(prm.cookie_key, cookie_key, 32);
+  std::memcpy(prm.nonce_key, nonce_key, 32);
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::cookie_reply_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), prm);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK : wg_pipe_fail(WG_RC_HIP_ERROR, "cookie_reply_batch: launch", e);
+}
+
 }  // extern "C"

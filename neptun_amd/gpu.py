@@ -29,6 +29,21 @@ KEY_SLOT_INVALID_PACKET = 0xFFFFFFFE   # WG_KEY_SLOT_INVALID_PACKET
 
 HALF_HANDSHAKE_DTYPE = np.dtype([("peer_index", "<u4"), ("status", "<i4"),
                                  ("peer_static_public", "u1", (32,))])  # wg_half_handshake
+# include/neptun_gpu.h responder / cookie records
+RESPONDER_PEER_DTYPE = np.dtype([("peer_static_public", "u1", 32), ("static_shared", "u1", 32)])
+INIT_RECEIVED_DTYPE = np.dtype([("status", "<i4"), ("peer_index", "<u4"), ("timestamp", "u1", 12),
+                                ("chaining_key", "u1", 32), ("hash", "u1", 32),
+                                ("peer_ephemeral", "u1", 32), ("pad", "u1", 12)])
+RESPONSE_JOB_DTYPE = np.dtype([("ephemeral_private", "u1", 32), ("peer_static_public", "u1", 32),
+                               ("preshared_key", "u1", 32), ("mac1_key", "u1", 32),
+                               ("cookie", "u1", 16), ("local_index", "<u4"), ("has_cookie", "<u4"),
+                               ("pad", "u1", 8)])
+RESPONSE_OUT_DTYPE = np.dtype([("message", "u1", 92), ("pad", "u1", 4), ("receiving_key", "u1", 32),
+                               ("sending_key", "u1", 32), ("mac1", "u1", 16)])
+COOKIE_REPLY_JOB_DTYPE = np.dtype([("cookie", "u1", 16), ("mac1", "u1", 16), ("nonce_ctr", "<u8"),
+                                   ("receiver_idx", "<u4"), ("pad", "<u4")])
+assert (RESPONDER_PEER_DTYPE.itemsize, INIT_RECEIVED_DTYPE.itemsize, RESPONSE_JOB_DTYPE.itemsize,
+        RESPONSE_OUT_DTYPE.itemsize, COOKIE_REPLY_JOB_DTYPE.itemsize) == (64, 128, 160, 176, 48)
 
 STATUS = {
     0: "Ok", 1: "DestinationBufferTooSmall", 2: "IncorrectPacketLength", 3: "UnexpectedPacket",
@@ -141,6 +156,37 @@ class GpuContext:
                                                     stride, 1 if check_mac1 else 0, _ptr(out),
                                                     _stream(stream)),
               "wg_gpu_handshake_anon_batch")
+
+    def handshake_consume_batch(self, static_private: bytes, n: int, msgs, stride: int, peers, out,
+                                stream=None) -> None:
+        """receive_handshake_initialization crypto (device): peers RESPONDER_PEER_DTYPE,
+        out INIT_RECEIVED_DTYPE."""
+        check(self._lib.wg_gpu_handshake_consume_batch(self._h, bytes(static_private), n, _ptr(msgs),
+                                                       stride, _ptr(peers), _ptr(out), _stream(stream)),
+              "wg_gpu_handshake_consume_batch")
+
+    def timestamp_after(self, ts: bytes, last: bytes) -> bool:
+        return bool(self._lib.wg_handshake_timestamp_after(bytes(ts), bytes(last)))
+
+    def handshake_respond_batch(self, n: int, states, jobs, out, stream=None) -> None:
+        """format_handshake_response + mac1/mac2 (device): jobs RESPONSE_JOB_DTYPE,
+        out RESPONSE_OUT_DTYPE."""
+        check(self._lib.wg_gpu_handshake_respond_batch(self._h, n, _ptr(states), _ptr(jobs), _ptr(out),
+                                                       _stream(stream)),
+              "wg_gpu_handshake_respond_batch")
+
+    def mac2_check_batch(self, secret_key: bytes, counter: int, n: int, msgs, stride: int, lens,
+                         addrs, cookies, status, stream=None) -> None:
+        check(self._lib.wg_gpu_mac2_check_batch(self._h, bytes(secret_key), counter, n, _ptr(msgs),
+                                                stride, _ptr(lens), _ptr(addrs), _ptr(cookies),
+                                                _ptr(status), _stream(stream)),
+              "wg_gpu_mac2_check_batch")
+
+    def cookie_reply_batch(self, cookie_key: bytes, nonce_key: bytes, n: int, jobs, out,
+                           stream=None) -> None:
+        check(self._lib.wg_gpu_cookie_reply_batch(self._h, bytes(cookie_key), bytes(nonce_key), n,
+                                                  _ptr(jobs), _ptr(out), _stream(stream)),
+              "wg_gpu_cookie_reply_batch")
 
     def route_set(self, receiver_idx, key_slot) -> None:
         """Replace the device receiver_idx -> key slot table (host arrays)."""

@@ -118,3 +118,44 @@ def test_model_handshake_round_trip():
     assert H.parse_handshake_anon(resp_priv, H.public_key(resp_priv), bytes(bad))[0] == H.INVALID_MAC
     assert H.parse_handshake_anon(resp_priv, H.public_key(resp_priv), bytes(bad),
                                   check_mac1=False)[0] == H.INVALID_AEAD_TAG
+
+
+def test_oracle_xchacha_matches_golden_vectors():
+    """Cookie AEAD restatement (HChaCha20 + RFC 8439) vs libsodium's vectors and the
+    draft's HChaCha20 KAT (tests/golden/xchacha.json, oracle/gen_golden_xchacha.py)."""
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "xchacha.json")))
+    d = g["hchacha20_draft"]
+    assert H.hchacha20(bytes.fromhex(d["key"]), bytes.fromhex(d["nonce"])).hex() == d["subkey"]
+    for v in g["vectors"]:
+        key, nonce = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"])
+        aad, pt = bytes.fromhex(v["aad"]), bytes.fromhex(v["pt"])
+        assert H.hchacha20(key, nonce[:16]).hex() == v["hchacha20_subkey"]
+        assert H.xchacha20poly1305_seal(key, nonce, aad, pt).hex() == v["ct_tag"]
+        assert H.xchacha20poly1305_open(key, nonce, aad, bytes.fromhex(v["ct_tag"])) == pt
+
+
+def test_oracle_responder_round_trip_with_initiator():
+    """The responder restatement (consume_initiation + format_response,
+    handshake.rs:527-613, 853-949) against the initiator side (initiation /
+    receive_response, :769-830, 615-695): the initiator accepts the response and
+    both ends derive the same session keys (sending of one = receiving of the other)."""
+    rng = random.Random(23)
+    for psk in (None, rng.randbytes(32)):
+        for cookie in (None, rng.randbytes(16)):
+            si, sr, ei, er = (rng.randbytes(32) for _ in range(4))
+            pi, pr = H.public_key(si), H.public_key(sr)
+            ts = rng.randbytes(12)
+            msg, ck_i, h_i = H.initiation(si, pr, ei, rng.getrandbits(32), ts)
+            st, pidx, t, ck, h, peph = H.consume_initiation(sr, pi, H.x25519(sr, pi), msg)
+            assert st == 0 and t == ts
+            resp, rk, sk, mac1 = H.format_response(ck, h, peph, pidx, 77, er, pi, psk, cookie)
+            assert H.b2s_keyed_mac_16(H.b2s_hash(H.LABEL_MAC1, pi), resp[:60]) == resp[60:76] == mac1
+            assert (cookie is None) == (resp[76:] == bytes(16))
+            st2, send_i, recv_i = H.receive_response(ck_i, h_i, ei, si, resp, psk)
+            assert st2 == 0 and send_i == rk and recv_i == sk
+    # the wrong peer key / a damaged timestamp are refused
+    st = H.consume_initiation(sr, H.public_key(rng.randbytes(32)), H.x25519(sr, pi), msg)[0]
+    assert st == H.WRONG_KEY
+    bad = bytearray(msg)
+    bad[95] ^= 1
+    assert H.consume_initiation(sr, pi, H.x25519(sr, pi), bytes(bad))[0] == H.INVALID_AEAD_TAG

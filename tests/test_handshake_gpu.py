@@ -91,3 +91,164 @@ def test_handshake_anon_batch_matches_oracle(torch_cuda, gpu):
         # with mac1 on, every damaged message fails mac1 first; without it, the AEAD
         assert sts == ({0, H.INVALID_MAC, H.WRONG_PACKET_TYPE} if check_mac1 else
                        {0, H.INVALID_AEAD_TAG, H.WRONG_PACKET_TYPE})
+
+
+def test_responder_consume_and_respond_match_oracle(torch_cuda, gpu):
+    """receive_handshake_initialization (handshake.rs:527-613) on the device, the
+    host's TAI64N / inc_index step, then format_handshake_response + mac1/mac2
+    (:853-949, :732-765) on the device, vs the oracle -- and the initiators (oracle
+    receive_response) accept the responses and derive the same session keys."""
+    from neptun_amd import gpu as G
+    torch = torch_cuda
+    rng = random.Random(29)
+    resp_priv = rng.randbytes(32)
+    resp_pub = H.public_key(resp_priv)
+    n = 300
+    inits, peers, msgs, want_status = [], np.zeros(n, G.RESPONDER_PEER_DTYPE), [], []
+    for i in range(n):
+        si, ei = rng.randbytes(32), rng.randbytes(32)
+        pi = H.public_key(si)
+        ts = rng.randbytes(12)
+        m, ck_i, h_i = H.initiation(si, resp_pub, ei, rng.getrandbits(32), ts)
+        m = bytearray(m)
+        configured = pi
+        r = rng.random()
+        if r < 0.05:
+            m[rng.randrange(40, 88)] ^= 1          # encrypted static damaged
+        elif r < 0.10:
+            m[rng.randrange(88, 116)] ^= 1         # encrypted timestamp damaged
+        elif r < 0.15:
+            configured = H.public_key(rng.randbytes(32))  # not the peer the caller looked up
+        elif r < 0.17:
+            m[0] = 2
+        peers[i]["peer_static_public"] = np.frombuffer(configured, np.uint8)
+        peers[i]["static_shared"] = np.frombuffer(H.x25519(resp_priv, configured), np.uint8)
+        msgs.append(bytes(m))
+        inits.append((si, ei, ck_i, h_i, pi))
+    stride = 148
+    d_m = to_dev(torch, b"".join(msgs))
+    d_p = to_dev(torch, peers.tobytes())
+    d_s = torch.zeros(n * G.INIT_RECEIVED_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    gpu.handshake_consume_batch(resp_priv, n, d_m, stride, d_p, d_s)
+    torch.cuda.synchronize()
+    states = d_s.cpu().numpy().view(G.INIT_RECEIVED_DTYPE)
+    jobs = np.zeros(n, G.RESPONSE_JOB_DTYPE)
+    oracle_states = []
+    last = bytes(12)
+    for i, m in enumerate(msgs):
+        pub = peers[i]["peer_static_public"].tobytes()
+        if m[:4] != b"\x01\x00\x00\x00":
+            want = (H.WRONG_PACKET_TYPE, 0)
+        else:
+            want = H.consume_initiation(resp_priv, pub, H.x25519(resp_priv, pub), m)
+        assert int(states[i]["status"]) == want[0], (i, int(states[i]["status"]), want[0])
+        oracle_states.append(want)
+        if want[0] == 0:
+            _, idx, ts, ck, h, eph = want
+            assert int(states[i]["peer_index"]) == idx
+            assert states[i]["timestamp"].tobytes() == ts
+            assert states[i]["chaining_key"].tobytes() == ck and states[i]["hash"].tobytes() == h
+            assert states[i]["peer_ephemeral"].tobytes() == eph
+            # host step (packet order): every initiator is a different peer here
+            assert gpu.timestamp_after(ts, last) == H.timestamp_after(ts, last)
+        jobs[i]["ephemeral_private"] = np.frombuffer(rng.randbytes(32), np.uint8)
+        jobs[i]["peer_static_public"] = peers[i]["peer_static_public"]
+        jobs[i]["preshared_key"] = np.frombuffer(rng.randbytes(32) if i % 3 == 0 else bytes(32), np.uint8)
+        jobs[i]["mac1_key"] = np.frombuffer(H.b2s_hash(H.LABEL_MAC1, pub), np.uint8)
+        jobs[i]["has_cookie"] = 1 if i % 4 == 0 else 0
+        jobs[i]["cookie"] = np.frombuffer(rng.randbytes(16), np.uint8)
+        jobs[i]["local_index"] = 0x00ABC000 + i
+    assert {s[0] for s in oracle_states} >= {0, H.INVALID_AEAD_TAG, H.WRONG_KEY, H.WRONG_PACKET_TYPE}
+    d_j = to_dev(torch, jobs.tobytes())
+    d_o = torch.zeros(n * G.RESPONSE_OUT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    gpu.handshake_respond_batch(n, d_s, d_j, d_o)
+    torch.cuda.synchronize()
+    out = d_o.cpu().numpy().view(G.RESPONSE_OUT_DTYPE)
+    accepted = 0
+    for i, want in enumerate(oracle_states):
+        if want[0] != 0:
+            assert not out[i]["message"].any()
+            continue
+        _, idx, ts, ck, h, eph = want
+        j = jobs[i]
+        psk = j["preshared_key"].tobytes()
+        cookie = j["cookie"].tobytes() if j["has_cookie"] else None
+        resp, rk, sk, mac1 = H.format_response(ck, h, eph, idx, int(j["local_index"]),
+                                               j["ephemeral_private"].tobytes(),
+                                               j["peer_static_public"].tobytes(),
+                                               psk if any(psk) else None, cookie)
+        assert out[i]["message"].tobytes() == resp, i
+        assert out[i]["receiving_key"].tobytes() == rk and out[i]["sending_key"].tobytes() == sk
+        assert out[i]["mac1"].tobytes() == mac1
+        si, ei, ck_i, h_i, pi = inits[i]
+        st, send_i, recv_i = H.receive_response(ck_i, h_i, ei, si, resp, psk if any(psk) else None)
+        assert st == 0 and send_i == rk and recv_i == sk
+        accepted += 1
+    assert accepted > 200
+
+
+def test_cookie_mac2_check_and_reply_match_oracle(torch_cuda, gpu):
+    """Under load (rate_limiter.rs:197-218): cookie from (secret, counter, address),
+    mac2 check of initiations and responses, and COOKIE_REPLY messages
+    (XChaCha20-Poly1305, :133-170) -- each equal to the oracle, and the initiator
+    can open its cookie (receive_cookie_reply, handshake.rs:703-727)."""
+    torch = torch_cuda
+    rng = random.Random(37)
+    secret, nonce_key = rng.randbytes(16), rng.randbytes(32)
+    resp_pub = H.public_key(rng.randbytes(32))
+    cookie_key = H.b2s_hash(H.LABEL_COOKIE, resp_pub)
+    counter = rng.getrandbits(40)
+    n = 400
+    msgs, lens, addrs, good = [], [], [], []
+    for i in range(n):
+        addr = rng.randbytes(4) + bytes(12) if i % 2 else rng.randbytes(16)
+        ck = H.current_cookie(secret, counter, addr)
+        has = rng.random() < 0.5
+        if i % 3:
+            m = H.format_handshake_initiation(rng.randbytes(32), resp_pub, rng.randbytes(32),
+                                              rng.getrandbits(32), rng.randbytes(12),
+                                              cookie=ck if has else None)
+        else:  # a handshake response-sized message with the macs at its end
+            body = rng.randbytes(60)
+            mac1 = rng.randbytes(16)
+            m = body + mac1 + (H.b2s_keyed_mac(ck, body + mac1, 16) if has else rng.randbytes(16))
+        msgs.append(m)
+        lens.append(len(m))
+        addrs.append(addr)
+        good.append(H.mac2_ok(ck, m))
+    stride = 148
+    d_m = to_dev(torch, b"".join(m + bytes(stride - len(m)) for m in msgs))
+    d_l = to_dev(torch, np.array(lens, np.uint32).tobytes())
+    d_a = to_dev(torch, b"".join(addrs))
+    d_c = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.mac2_check_batch(secret, counter, n, d_m, stride, d_l, d_a, d_c, d_st)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    cookies = d_c.cpu().numpy().tobytes()
+    for i in range(n):
+        assert cookies[16 * i:16 * i + 16] == H.current_cookie(secret, counter, addrs[i])
+        assert st[i] == (0 if good[i] else 1), i
+    assert 0 < int(st.sum()) < n
+    # replies for the failures, nonce counters handed out in order
+    from neptun_amd import gpu as G
+    bad = [i for i in range(n) if not good[i]]
+    jobs = np.zeros(len(bad), G.COOKIE_REPLY_JOB_DTYPE)
+    ctr0 = rng.getrandbits(48)
+    for k, i in enumerate(bad):
+        jobs[k]["cookie"] = np.frombuffer(cookies[16 * i:16 * i + 16], np.uint8)
+        jobs[k]["mac1"] = np.frombuffer(msgs[i][-32:-16], np.uint8)
+        jobs[k]["nonce_ctr"] = ctr0 + k
+        jobs[k]["receiver_idx"] = int.from_bytes(msgs[i][4:8], "little")
+    d_j = to_dev(torch, jobs.tobytes())
+    d_o = torch.zeros(64 * len(bad), dtype=torch.uint8, device="cuda")
+    gpu.cookie_reply_batch(cookie_key, nonce_key, len(bad), d_j, d_o)
+    torch.cuda.synchronize()
+    out = d_o.cpu().numpy().tobytes()
+    for k, i in enumerate(bad):
+        want = H.format_cookie_reply(cookie_key, int(jobs[k]["receiver_idx"]), jobs[k]["cookie"].tobytes(),
+                                     jobs[k]["mac1"].tobytes(), H.cookie_nonce(nonce_key, ctr0 + k))
+        got = out[64 * k:64 * k + 64]
+        assert got == want, k
+        assert H.xchacha20poly1305_open(cookie_key, got[8:32], msgs[i][-32:-16], got[32:]) == \
+            jobs[k]["cookie"].tobytes()
