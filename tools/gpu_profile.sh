@@ -16,7 +16,7 @@ for c in $CONFIGS; do
   timeout -k 10 300 python3 bench.py --config "$c" --steps 20 --warmup 5 > "$OUT/bench_config$c.json"
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/trace_bench_config2.json"
+  python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --sustain-seconds 0 > "$OUT/trace_bench_config2.json"
 for c in $CONFIGS; do
   timeout -k 10 400 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_config$c.json" --config "$c" > /dev/null
   timeout -k 10 400 python3 tools/pmc_valu.py "$OUT/pmc_valu_config$c.json" --config "$c" > /dev/null

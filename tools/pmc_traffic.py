@@ -29,7 +29,7 @@ def pmc_pass(counter, outdir, bench_args):
     d = os.path.join(outdir, counter.lower())
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-           "--no-cpu-baseline"] + bench_args
+           "--no-cpu-baseline", "--sustain-seconds", "0", "--evp-sample", "0"] + bench_args
     subprocess.run(cmd, check=True, env=dict(os.environ, TMPDIR="/tmp"), timeout=600,
                    stdout=subprocess.DEVNULL)
     vals = defaultdict(list)

@@ -44,7 +44,7 @@ def main():
         target = bench_args[1:]
     else:
         target = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                  "--no-cpu-baseline"] + bench_args
+                  "--no-cpu-baseline", "--sustain-seconds", "0", "--evp-sample", "0"] + bench_args
     cmd = ["rocprofv3", "--kernel-trace", "--pmc", *COUNTERS, "--output-format", "csv", "-d", d,
            "-o", "pmc", "--"] + target
     subprocess.run(cmd, check=True, env=dict(os.environ, TMPDIR="/tmp"), timeout=600,
