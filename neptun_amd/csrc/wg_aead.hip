@@ -138,6 +138,36 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
   return x;
 }
 
+__device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
+  return __builtin_amdgcn_readfirstlane(x);
+}
+// wave-uniform copy of lane 0's 64-bit value.  (readfirstlane returns int:
+// each half must be taken back to uint32_t before widening, or a low half with
+// bit 31 set sign-extends over the high half.)
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t y = (uint64_t)__shfl_xor((long long)x, o, 64);
+    x = y < x ? y : x;
+  }
+  return uniform64(x);
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t y = (uint64_t)__shfl_xor((long long)x, o, 64);
+    x = y > x ? y : x;
+  }
+  return uniform64(x);
+}
+
 __device__ __forceinline__ void lds_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 template <bool kSeal>
@@ -179,24 +209,65 @@ struct DescGeom {
   uint64_t in_ref, out_ref;      // src - 16, dst - 16
   uint32_t *wg_rounds;           // [waves] round counts of the workgroup's waves
   uint32_t wave, alive;          // this wave, waves of the workgroup with packets
+  // Fast addressing (per group, wave-uniform; set by set()): when the wave's
+  // packets span < 2 GiB on each side, in16 / out16 hold BYTE offsets from the
+  // wave's lowest packet (kNoAccess for packets not staged) and the rounds in
+  // [r_in0, r_in1) / [r_out0, r_out1) -- where every staged packet moves a full
+  // 128-byte run -- go through one buffer resource with 1 VALU op per piece
+  // (stage_in / stage_out overloads below) instead of per-lane 64-bit addresses.
+  bool fast = false;
+  uint64_t in_wave = 0, out_wave = 0;
+  uint32_t in_rec = 0, out_rec = 0;
+  uint32_t r_in0 = 0, r_in1 = 0, r_out0 = 0, r_out1 = 0;
   __device__ bool live(uint32_t p, uint32_t r) const { return kRun * r < S.wlen[p]; }
   __device__ uint32_t wlen(uint32_t p) const { return S.wlen[p]; }
   __device__ uint64_t in_base(uint32_t p) const {
+    if (fast) return in_wave + S.in16[p];
     return in_ref + 16ull * (((uint64_t)S.in_hi[p] << 32) | S.in16[p]);
   }
   __device__ uint64_t out_base(uint32_t p) const {
+    if (fast) return out_wave + S.out16[p];
     return out_ref + 16ull * (((uint64_t)S.out_hi[p] << 32) | S.out16[p]);
   }
   // (host side: src and dst are non-null, so offsets stay below 2^44 bytes)
+  template <bool kSeal>
   __device__ void set(uint32_t lane, uint64_t in_base, uint64_t out_base, uint32_t W, bool ok) {
-    const uint64_t i16 = (in_base - in_ref) >> 4, o16 = (out_base - out_ref) >> 4;
-    S.in16[lane] = (uint32_t)i16;
-    S.in_hi[lane] = (uint8_t)(i16 >> 32);
-    S.out16[lane] = (uint32_t)o16;
-    S.out_hi[lane] = (uint8_t)(o16 >> 32);
+    const uint32_t ihi = ok ? (kSeal ? W - 16u : W) : 0u;   // Ranges<kSeal>::in_hi
+    const uint32_t ohi = ok ? (kSeal ? W : W - 16u) : 0u;   // Ranges<kSeal>::out_hi
+    const uint64_t imin = wave_min64(ok ? in_base : ~0ull), omin = wave_min64(ok ? out_base : ~0ull);
+    const uint64_t imax = wave_max64(ok ? in_base + ihi : 0ull);
+    const uint64_t omax = wave_max64(ok ? out_base + ohi : 0ull);
+    const uint32_t any = __builtin_amdgcn_readfirstlane(__ballot(ok) != 0ull ? 1u : 0u);
+    const uint64_t ispan = imax - imin, ospan = omax - omin;
+    fast = any && ispan + 16u < kNoAccessOffset - 1024u && ospan + 16u < kNoAccessOffset - 1024u;
+    if (fast) {
+      in_wave = imin;
+      out_wave = omin;
+      in_rec = (uint32_t)((ispan + 15u) & ~15ull);
+      out_rec = (uint32_t)((ospan + 15u) & ~15ull);
+      // full-run rounds: 128 r >= lo and 128 (r + 1) <= hi for every staged packet
+      r_in0 = kSeal ? 1u : 0u;
+      r_out0 = kSeal ? 0u : 1u;
+      r_in1 = wave_min32(ok ? ihi / kRun : 0xffffffffu);
+      r_out1 = wave_min32(ok ? ohi / kRun : 0xffffffffu);
+      S.in16[lane] = ok ? (uint32_t)(in_base - imin) : kNoAccessOffset;
+      S.out16[lane] = ok ? (uint32_t)(out_base - omin) : kNoAccessOffset;
+    } else {
+      const uint64_t i16 = (in_base - in_ref) >> 4, o16 = (out_base - out_ref) >> 4;
+      S.in16[lane] = (uint32_t)i16;
+      S.in_hi[lane] = (uint8_t)(i16 >> 32);
+      S.out16[lane] = (uint32_t)o16;
+      S.out_hi[lane] = (uint8_t)(o16 >> 32);
+    }
     S.wlen[lane] = ok ? W : 0u;
   }
-  __device__ void kill(uint32_t lane) { S.wlen[lane] = 0u; }
+  __device__ void kill(uint32_t lane) {
+    S.wlen[lane] = 0u;
+    if (fast) {
+      S.in16[lane] = kNoAccessOffset;
+      S.out16[lane] = kNoAccessOffset;
+    }
+  }
   // the workgroup's round count (every wave must run the same barrier steps)
   __device__ uint32_t wg_max(uint32_t wave_rounds) const {
     if ((threadIdx.x & 63u) == 0u) wg_rounds[wave] = wave_rounds;
@@ -447,6 +518,50 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   }
 }
 
+// Descriptor-batch forms (DescGeom): rounds where every staged packet of the
+// wave moves a full 128-byte run use one wave-uniform buffer resource over the
+// wave's packets (base = its lowest packet, records = its span) and the 32-bit
+// per-packet offsets from LDS -- one v_add per piece, no range checks (packets
+// not staged carry offset kNoAccess); the other rounds (the first / last ones,
+// ragged lengths) take the generic per-lane path.  The 8 offsets are read before
+// the 8 DMAs: an LDS read after a builtin LDS-DMA makes the compiler drain it.
+template <bool kSeal>
+__device__ __forceinline__ void stage_in(uint4 *run, const DescGeom &g, uint32_t lane, uint32_t r) {
+  if (!(g.fast && r >= g.r_in0 && r < g.r_in1)) {
+    stage_in<kSeal, DescGeom>(run, g, lane, r);
+    return;
+  }
+  const uint32_t y = lane >> 3, k0 = 16u * ((lane & 7u) ^ swz(y)), k1 = k0 ^ 64u;
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in_wave, g.in_rec);
+  uint32_t off[kChunks];
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j) off[j] = g.S.in16[8u * j + y] + ((j & 1u) ? k1 : k0);
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16, off[j], kRun * r, 0, WG_LOAD_CPOL);
+}
+
+template <bool kSeal>
+__device__ __forceinline__ void stage_out(uint4 *run, const DescGeom &g, uint32_t lane, uint32_t r) {
+  if (!(g.fast && r >= g.r_out0 && r < g.r_out1)) {
+    stage_out<kSeal, DescGeom>(run, g, lane, r);
+    return;
+  }
+  const uint32_t y = lane >> 3, k0 = 16u * ((lane & 7u) ^ swz(y)), k1 = k0 ^ 64u;
+  uint32_t off[kChunks];
+  uint4 v[kChunks];
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j) {
+    off[j] = g.S.out16[8u * j + y] + ((j & 1u) ? k1 : k0);
+    v[j] = run[64u * j + lane];
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kChunks; ++j) {
+    const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
+    store16(vv, g.out_wave, g.out_rec, off[j], kRun * r);
+  }
+}
+
 // One lane's chunk of ciphertext work.  m = plaintext/ciphertext byte index of
 // the chunk (wire w - 16); `ks` = its 4 keystream words.  Returns via LDS.
 template <bool kSeal>
@@ -583,7 +698,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   if constexpr (kUniform) {
     rounds = my_runs;  // uniform: job.len is a kernel argument
   } else if constexpr (kSync) {
-    g.set(lane, job.in_base, job.out_base, W, my_runs != 0u);
+    g.template set<kSeal>(lane, job.in_base, job.out_base, W, my_runs != 0u);
     rounds = g.wg_max(wave_max(my_runs));
   } else {
     S.in_base[lane] = job.in_base;

@@ -24,7 +24,87 @@ def bind(path):
     L.wg_gpu_seal_strided.argtypes = [vp, u32, u32, u32, u64, vp, u64, vp, u64, vp, vp]
     L.wg_gpu_open_strided.argtypes = [vp, u32, u32, u32, vp, u64, vp, u64, vp, vp]
     L.wg_gpu_last_error.restype = c.c_char_p
+    for fn in (L.wg_gpu_seal_batch, L.wg_gpu_open_batch):
+        fn.argtypes = [vp, vp, u32, vp, vp, vp, vp]
+    for fn in (L.wg_gpu_seal_batch_ordered, L.wg_gpu_open_batch_ordered):
+        fn.argtypes = [vp, vp, vp, u32, vp, vp, vp, vp]
+    L.wg_gpu_plan_batch.argtypes = [vp, c.c_int, vp, u32, vp, vp, vp]
     return L
+
+
+def main_desc(paths, cfg):
+    """AB_CONFIG=3|4: the descriptor kernels on BASELINE config 3 / 4 batches
+    (AB_PEERS x AB_PER_PEER for config 4, AB_PER_SIZE per size for config 3)."""
+    import numpy as np
+    import torch
+    from tools import synth, workloads
+    dev = torch.device("cuda", 0)
+    if cfg == 3:
+        b = workloads.config3(int(os.environ.get("AB_PER_SIZE", 1 << 18)), dev)
+        nkeys = 1
+    else:
+        peers = int(os.environ.get("AB_PEERS", 4096))
+        b = workloads.config4(peers, int(os.environ.get("AB_PER_PEER", 1024)), 1350, dev)
+        nkeys = peers
+    keys = synth.keys(nkeys)
+    idx = np.full(nkeys, synth.RECEIVER_IDX, np.uint32) + np.arange(nkeys, dtype=np.uint32)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    libs = []
+    for p in paths:
+        L = bind(p)
+        h = ctypes.c_void_p()
+        assert L.wg_gpu_ctx_create(0, nkeys, ctypes.byref(h)) == 0, L.wg_gpu_last_error()
+        assert L.wg_gpu_set_keys(h, 0, nkeys, keys.ctypes.data, idx.ctypes.data, stream) == 0
+        libs.append((os.path.basename(p), L, h))
+
+    def seal(L, h):
+        if cfg == 3:
+            assert L.wg_gpu_plan_batch(h, 1, b.d_seal.data_ptr(), b.n, b.order.data_ptr(),
+                                       b.scratch.data_ptr(), stream) == 0
+            assert L.wg_gpu_seal_batch_ordered(h, b.d_seal.data_ptr(), b.order.data_ptr(), b.n,
+                                               b.pt.data_ptr(), b.wire.data_ptr(),
+                                               b.st_seal.data_ptr(), stream) == 0
+        else:
+            assert L.wg_gpu_seal_batch(h, b.d_seal.data_ptr(), b.n, b.pt.data_ptr(), b.wire.data_ptr(),
+                                       b.st_seal.data_ptr(), stream) == 0
+
+    def open_(L, h):
+        if cfg == 3:
+            assert L.wg_gpu_open_batch_ordered(h, b.d_open.data_ptr(), b.order.data_ptr(), b.n,
+                                               b.wire.data_ptr(), b.out.data_ptr(),
+                                               b.st_open.data_ptr(), stream) == 0
+        else:
+            assert L.wg_gpu_open_batch(h, b.d_open.data_ptr(), b.n, b.wire.data_ptr(), b.out.data_ptr(),
+                                       b.st_open.data_ptr(), stream) == 0
+
+    ref = None
+    for name, L, h in libs:
+        b.wire.zero_(); b.out.zero_()
+        seal(L, h); open_(L, h)
+        torch.cuda.synchronize()
+        ok = int((b.st_seal != 0).sum()) == 0 and int((b.st_open != 0).sum()) == 0 and b.round_trip_equal()
+        if ref is None:
+            ref = b.wire.clone()
+        print(f"{name}: round-trip {'ok' if ok else 'FAIL'}, wire "
+              f"{'identical' if torch.equal(b.wire, ref) else 'DIFFERS'}", flush=True)
+    burst = int(os.environ.get("AB_BURST", 2))
+    rounds = int(os.environ.get("AB_ROUNDS", 10))
+    times = {name: ([], []) for name, _, _ in libs}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for _ in range(rounds):
+        for name, L, h in libs:
+            for _ in range(burst):
+                seal(L, h); open_(L, h)
+            ev[0].record(); seal(L, h); ev[1].record(); open_(L, h); ev[2].record()
+            torch.cuda.synchronize()
+            times[name][0].append(ev[0].elapsed_time(ev[1]))
+            times[name][1].append(ev[1].elapsed_time(ev[2]))
+    pay = float(b.sizes.astype(np.int64).sum())
+    for name, (s_, o_) in times.items():
+        rt = [a + c for a, c in zip(s_, o_)]
+        print(f"{name:40s} config {cfg}: seal med {statistics.median(s_):.4f} | open med "
+              f"{statistics.median(o_):.4f} | round trip {statistics.median(rt):.4f} ms = "
+              f"{pay * 8 / (statistics.median(rt) * 1e-3) / 1e9:.0f} Gbit/s", flush=True)
 
 
 def main():
@@ -32,6 +112,8 @@ def main():
     import torch
     from tools import synth
     paths = sys.argv[1:]
+    if os.environ.get("AB_CONFIG", "2") != "2":
+        return main_desc(paths, int(os.environ["AB_CONFIG"]))
     n, P, S = 1 << 20, int(os.environ.get("AB_SIZE", 1350)), 0
     S = synth.round_up(P + 32, 128)
     rounds = int(os.environ.get("AB_ROUNDS", 15))

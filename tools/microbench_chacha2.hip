@@ -5,6 +5,8 @@
 // took an add8/xor8/rot8 stream from 3.96 to 2.4-2.8 cycles per instruction).
 //   hipcc --offload-arch=gfx950 -O3 -I neptun_amd/csrc tools/microbench_chacha2.hip -o tools/microbench_chacha2
 #include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <cstring>
 #include <cstdint>
 #include <cstdio>
 
@@ -177,6 +179,33 @@ int main(int argc, char** argv) {
     {"asm, no bar wg1024 1 WG/CU (LDS)", k_asm<0, 1024>, 1024, 96 << 10},
     {"compiled wg256 4 WG/CU (LDS)", k_c<256>, 256, 36 << 10},
   };
+  // `microbench_chacha2 only IDX SECONDS`: one variant back to back for ~SECONDS
+  // (tools/power_probe.py: energy per block of the phase-locked vs the
+  // compiler-scheduled keystream)
+  if (argc > 3 && !strcmp(argv[1], "only")) {
+    auto& k = ks[atoi(argv[2])];
+    const int threads_total = cus * 4 * 4 * 64 * 8;
+    const int blocks = threads_total / k.wg;
+    hipLaunchKernelGGL(k.f, dim3(blocks), dim3(k.wg), k.lds, 0, out, keys);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k.f, dim3(blocks), dim3(k.wg), k.lds, 0, out, keys);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms1;
+    CHECK(hipEventElapsedTime(&ms1, e0, e1));
+    const int n = (int)(atof(argv[3]) * 1e3 / ms1) + 1;
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < n; ++i) hipLaunchKernelGGL(k.f, dim3(blocks), dim3(k.wg), k.lds, 0, out, keys);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    const double blocks_total = (double)threads_total * 2 * kPairs * n;
+    printf("{\"variant\": \"%s\", \"seconds\": %.3f, \"wave_blocks_per_s\": %.4e}\n", k.name,
+           ms * 1e-3, blocks_total / 64.0 / (ms * 1e-3));
+    return 0;
+  }
   // total waves = 4 waves/SIMD resident x 8 rounds; per wave 2*kPairs blocks
   for (auto& k : ks) {
     for (int wps : {4}) {
