@@ -19,7 +19,10 @@
  * the receive buffer overflows, so the sender keeps at most W datagrams in
  * flight (W from the socket's effective SO_RCVBUF).
  *
- *   udp_gateway IN OUT [B]   -> one JSON line on stdout
+ *   udp_gateway IN OUT [B] [PAIRS]   -> one JSON line on stdout
+ * PAIRS > 1 runs that many independent peers side by side (own Tunns, sockets
+ * and threads, one GPU context), the way NepTUN serves peers on its n_threads
+ * event loops.
  * IN : "NGW1" | u32 n | u32 a_idx | u32 b_idx | k1[32] | k2[32] | n x (u32 len | bytes)
  * OUT: "NGWO" | u32 sent | sent x (u32 len | datagram)
  *             | u32 recv | recv x (u32 len | datagram | wg_tunn_result | u32 dst_len | dst bytes)
@@ -51,9 +54,10 @@ typedef struct {
 
 typedef struct {
   input_t *in;
+  uint32_t i0, i1;  /* this pair's share of the input packets */
   wg_tunn *a, *b;
   int sa, sb;
-  uint32_t batch, window;
+  uint32_t batch, window, slot;  /* slot: bytes per preallocated packet buffer */
   /* sender output */
   uint8_t **sent;
   uint32_t *sent_len;
@@ -70,6 +74,8 @@ typedef struct {
   _Atomic uint32_t n_dec;
   _Atomic int failed;
   double t_end;
+  /* where the time goes (seconds, per thread) */
+  double t_encap, t_send, t_wait, t_recv, t_decap;
 } gw_t;
 
 static double now(void) {
@@ -104,19 +110,19 @@ static int load_input(const char *path, input_t *in) {
 /* encrypt worker: batch -> GPU encapsulate -> sendmmsg */
 static void *sender(void *arg) {
   gw_t *g = arg;
-  const uint32_t n = g->in->n, B = g->batch;
+  const uint32_t n = g->i1, B = g->batch;
   wg_tunn_result *res = calloc(B, sizeof *res);
   uint32_t *cap = calloc(B, sizeof *cap);
   struct mmsghdr *msgs = calloc(B, sizeof *msgs);
   struct iovec *iov = calloc(B, sizeof *iov);
-  for (uint32_t i0 = 0; i0 < n && !atomic_load(&g->failed); i0 += B) {
+  for (uint32_t i0 = g->i0; i0 < n && !atomic_load(&g->failed); i0 += B) {
     const uint32_t m = n - i0 < B ? n - i0 : B;
-    for (uint32_t j = 0; j < m; ++j) {
-      g->sent[i0 + j] = malloc(g->in->len[i0 + j] + 32);
-      cap[j] = g->in->len[i0 + j] + 32;
-    }
-    if (wg_tunn_encapsulate_batch(g->a, m, (const uint8_t *const *)&g->in->pkt[i0], &g->in->len[i0],
-                                  &g->sent[i0], cap, res)) {
+    for (uint32_t j = 0; j < m; ++j) cap[j] = g->slot;
+    double t = now();
+    const int erc = wg_tunn_encapsulate_batch(g->a, m, (const uint8_t *const *)&g->in->pkt[i0],
+                                              &g->in->len[i0], &g->sent[i0], cap, res);
+    g->t_encap += now() - t;
+    if (erc) {
       fprintf(stderr, "encapsulate_batch: %s\n", wg_gpu_last_error());
       atomic_store(&g->failed, 1);
       break;
@@ -137,12 +143,16 @@ static void *sender(void *arg) {
     while (done < k) {
       const uint32_t inflight = atomic_load(&g->n_sent) - atomic_load(&g->n_rx);
       if (inflight >= g->window) {
+        t = now();
         sched_yield();
+        g->t_wait += now() - t;
         continue;
       }
       uint32_t can = g->window - inflight;
       if (can > k - done) can = k - done;
+      t = now();
       const int r = sendmmsg(g->sa, &msgs[done], can, 0);
+      g->t_send += now() - t;
       if (r < 0) {
         perror("sendmmsg");
         atomic_store(&g->failed, 1);
@@ -159,7 +169,7 @@ static void *sender(void *arg) {
 /* socket reader: recvmmsg into the arrival-ordered store */
 static void *reader(void *arg) {
   gw_t *g = arg;
-  const uint32_t n = g->in->n, B = g->batch;
+  const uint32_t n = g->i1 - g->i0, B = g->batch;
   struct mmsghdr *msgs = calloc(B, sizeof *msgs);
   struct iovec *iov = calloc(B, sizeof *iov);
   double idle_since = now();
@@ -167,15 +177,16 @@ static void *reader(void *arg) {
     const uint32_t base = atomic_load(&g->n_rx);
     const uint32_t m = n - base < B ? n - base : B;
     for (uint32_t j = 0; j < m; ++j) {
-      if (!g->rx[base + j]) g->rx[base + j] = malloc(MAX_DGRAM);
       iov[j].iov_base = g->rx[base + j];
-      iov[j].iov_len = MAX_DGRAM;
+      iov[j].iov_len = g->slot;
       memset(&msgs[j], 0, sizeof msgs[j]);
       msgs[j].msg_hdr.msg_iov = &iov[j];
       msgs[j].msg_hdr.msg_iovlen = 1;
     }
     struct timespec to = {0, 50 * 1000 * 1000};
+    const double t = now();
     const int r = recvmmsg(g->sb, msgs, m, MSG_WAITFORONE, &to);
+    g->t_recv += now() - t;
     if (r <= 0) {
       /* every datagram that was sent has arrived or is lost: stop after 2 s idle */
       if (now() - idle_since > 2.0) break;
@@ -206,10 +217,12 @@ static void *decryptor(void *arg) {
     for (uint32_t j = 0; j < m; ++j) {
       const uint32_t L = g->rx_len[d + j];
       g->dst_cap[d + j] = L > 16 ? L - 16 : 0;
-      g->dst[d + j] = malloc(g->dst_cap[d + j] + 1);
     }
-    if (wg_tunn_decapsulate_batch(g->b, m, (const uint8_t *const *)&g->rx[d], &g->rx_len[d],
-                                  &g->dst[d], &g->dst_cap[d], &g->res[d])) {
+    const double t = now();
+    const int drc = wg_tunn_decapsulate_batch(g->b, m, (const uint8_t *const *)&g->rx[d], &g->rx_len[d],
+                                              &g->dst[d], &g->dst_cap[d], &g->res[d]);
+    g->t_decap += now() - t;
+    if (drc) {
       fprintf(stderr, "decapsulate_batch: %s\n", wg_gpu_last_error());
       atomic_store(&g->failed, 1);
       break;
@@ -248,7 +261,7 @@ static int udp_socket(struct sockaddr_in *addr) {
 
 int main(int argc, char **argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s IN OUT [batch]\n", argv[0]);
+    fprintf(stderr, "usage: %s IN OUT [batch] [pairs]\n", argv[0]);
     return 2;
   }
   input_t in;
@@ -256,79 +269,117 @@ int main(int argc, char **argv) {
     fprintf(stderr, "bad input %s\n", argv[1]);
     return 2;
   }
-  gw_t g;
-  memset(&g, 0, sizeof g);
-  g.in = &in;
-  g.batch = argc > 3 ? (uint32_t)atoi(argv[3]) : 512;
-  if (g.batch == 0) g.batch = 1;
+  const uint32_t batch = argc > 3 && atoi(argv[3]) > 0 ? (uint32_t)atoi(argv[3]) : 512;
+  /* pairs > 1: that many independent peers (Tunn pairs, socket pairs and
+   * threads) share the input -- NepTUN's per-peer Mutex<Tunn> + n_threads
+   * event loops; the output file is written for pairs == 1 only */
+  const uint32_t pairs = argc > 4 && atoi(argv[4]) > 0 ? (uint32_t)atoi(argv[4]) : 1;
   wg_gpu_ctx *ctx = NULL;
-  CHECK(wg_gpu_ctx_create(0, 32, &ctx));
-  CHECK(wg_tunn_create(ctx, 0, &g.a));
-  CHECK(wg_tunn_create(ctx, 16, &g.b));
-  /* A sends with k1 to b_idx and receives with k2; B the mirror image */
-  CHECK(wg_tunn_install_session(g.a, in.a_idx, in.b_idx, in.k2, in.k1, 1));
-  CHECK(wg_tunn_install_session(g.b, in.b_idx, in.a_idx, in.k1, in.k2, 1));
-  struct sockaddr_in aa, ab;
-  g.sa = udp_socket(&aa);
-  g.sb = udp_socket(&ab);
-  if (g.sa < 0 || g.sb < 0 || connect(g.sa, (struct sockaddr *)&ab, sizeof ab)) {
-    perror("socket");
-    return 1;
-  }
-  int rcvbuf = 0;
-  socklen_t ol = sizeof rcvbuf;
-  (void)getsockopt(g.sb, SOL_SOCKET, SO_RCVBUF, &rcvbuf, &ol);
-  /* loopback charges each datagram its skb truesize (~2-4 KiB for <= 1500 B) */
-  g.window = rcvbuf / 4096 > 16 ? (uint32_t)(rcvbuf / 4096) : 16;
+  CHECK(wg_gpu_ctx_create(0, 32 * pairs, &ctx));
   const uint32_t n = in.n;
-  g.sent = calloc(n, sizeof *g.sent);
-  g.sent_len = calloc(n, sizeof *g.sent_len);
-  g.rx = calloc(n, sizeof *g.rx);
-  g.rx_len = calloc(n, sizeof *g.rx_len);
-  g.dst = calloc(n, sizeof *g.dst);
-  g.dst_cap = calloc(n, sizeof *g.dst_cap);
-  g.res = calloc(n, sizeof *g.res);
-
-  const double t0 = now();
-  pthread_t ts, tr, td;
-  pthread_create(&tr, NULL, reader, &g);
-  pthread_create(&td, NULL, decryptor, &g);
-  pthread_create(&ts, NULL, sender, &g);
-  pthread_join(ts, NULL);
-  pthread_join(tr, NULL);
-  pthread_join(td, NULL);
-  if (atomic_load(&g.failed)) return 1;
-
-  const uint32_t nrx = atomic_load(&g.n_rx), nsent = atomic_load(&g.n_sent);
-  uint64_t bytes = 0;
-  for (uint32_t i = 0; i < nrx; ++i)
-    if (g.res[i].kind == WG_TUNN_WRITE_TO_TUNNEL) bytes += g.res[i].len;
-  const double secs = g.t_end > t0 ? g.t_end - t0 : 1e-9;
-
-  FILE *f = fopen(argv[2], "wb");
-  if (!f) return 1;
-  fwrite("NGWO", 1, 4, f);
-  fwrite(&n, 4, 1, f);
+  uint8_t **sent = calloc(n, sizeof *sent), **rx = calloc(n, sizeof *rx), **dst = calloc(n, sizeof *dst);
+  uint32_t *sent_len = calloc(n, 4), *rx_len = calloc(n, 4), *dst_cap = calloc(n, 4);
+  wg_tunn_result *res = calloc(n, sizeof *res);
+  /* every packet buffer is preallocated and touched before the clock starts, as
+   * a gateway's buffer pools are: the timed region holds no malloc or page fault */
+  uint32_t max_len = 0;
+  for (uint32_t i = 0; i < n; ++i) max_len = in.len[i] > max_len ? in.len[i] : max_len;
+  const uint32_t slot = (max_len + 64 + 63) & ~63u;
+  uint8_t *slabs = malloc((size_t)3 * n * slot + 1);
+  memset(slabs, 0, (size_t)3 * n * slot + 1);
   for (uint32_t i = 0; i < n; ++i) {
-    fwrite(&g.sent_len[i], 4, 1, f);
-    fwrite(g.sent[i], 1, g.sent_len[i], f);
+    sent[i] = slabs + (size_t)i * slot;
+    rx[i] = slabs + ((size_t)n + i) * slot;
+    dst[i] = slabs + ((size_t)2 * n + i) * slot;
   }
-  fwrite(&nrx, 4, 1, f);
-  for (uint32_t i = 0; i < nrx; ++i) {
-    fwrite(&g.rx_len[i], 4, 1, f);
-    fwrite(g.rx[i], 1, g.rx_len[i], f);
-    fwrite(&g.res[i], sizeof g.res[i], 1, f);
-    fwrite(&g.dst_cap[i], 4, 1, f);
-    fwrite(g.dst[i], 1, g.dst_cap[i], f);
+  gw_t *gs = calloc(pairs, sizeof *gs);
+  int rcvbuf = 0;
+  for (uint32_t p = 0; p < pairs; ++p) {
+    gw_t *g = &gs[p];
+    g->in = &in;
+    g->i0 = (uint32_t)((uint64_t)n * p / pairs);
+    g->i1 = (uint32_t)((uint64_t)n * (p + 1) / pairs);
+    g->batch = batch;
+    g->slot = slot;
+    CHECK(wg_tunn_create(ctx, 32 * p, &g->a));
+    CHECK(wg_tunn_create(ctx, 32 * p + 16, &g->b));
+    /* A sends with k1 to b_idx and receives with k2; B the mirror image */
+    CHECK(wg_tunn_install_session(g->a, in.a_idx + 256 * p, in.b_idx + 256 * p, in.k2, in.k1, 1));
+    CHECK(wg_tunn_install_session(g->b, in.b_idx + 256 * p, in.a_idx + 256 * p, in.k1, in.k2, 1));
+    struct sockaddr_in aa, ab;
+    g->sa = udp_socket(&aa);
+    g->sb = udp_socket(&ab);
+    if (g->sa < 0 || g->sb < 0 || connect(g->sa, (struct sockaddr *)&ab, sizeof ab)) {
+      perror("socket");
+      return 1;
+    }
+    socklen_t ol = sizeof rcvbuf;
+    (void)getsockopt(g->sb, SOL_SOCKET, SO_RCVBUF, &rcvbuf, &ol);
+    /* loopback charges each datagram its skb truesize (~2-4 KiB for <= 1500 B) */
+    g->window = rcvbuf / 4096 > 16 ? (uint32_t)(rcvbuf / 4096) : 16;
+    /* the pair's arrays are windows into the shared ones (sent: input order;
+     * rx / dst / res: this pair's arrival order) */
+    g->sent = sent;
+    g->sent_len = sent_len;
+    g->rx = rx + g->i0;
+    g->rx_len = rx_len + g->i0;
+    g->dst = dst + g->i0;
+    g->dst_cap = dst_cap + g->i0;
+    g->res = res + g->i0;
   }
-  fclose(f);
+  const double t0 = now();
+  pthread_t *th = calloc(3 * pairs, sizeof *th);
+  for (uint32_t p = 0; p < pairs; ++p) {
+    pthread_create(&th[3 * p], NULL, reader, &gs[p]);
+    pthread_create(&th[3 * p + 1], NULL, decryptor, &gs[p]);
+    pthread_create(&th[3 * p + 2], NULL, sender, &gs[p]);
+  }
+  for (uint32_t k = 0; k < 3 * pairs; ++k) pthread_join(th[k], NULL);
+  uint32_t nrx = 0, nsent = 0;
+  uint64_t bytes = 0;
+  double te = 0, ts = 0, tw = 0, tr = 0, td = 0;
+  double t_end = t0;
+  for (uint32_t p = 0; p < pairs; ++p) {
+    gw_t *g = &gs[p];
+    if (atomic_load(&g->failed)) return 1;
+    const uint32_t r = atomic_load(&g->n_rx);
+    nrx += r;
+    nsent += atomic_load(&g->n_sent);
+    for (uint32_t i = 0; i < r; ++i)
+      if (g->res[i].kind == WG_TUNN_WRITE_TO_TUNNEL) bytes += g->res[i].len;
+    if (g->t_end > t_end) t_end = g->t_end;
+    te += g->t_encap, ts += g->t_send, tw += g->t_wait, tr += g->t_recv, td += g->t_decap;
+  }
+  const double secs = t_end > t0 ? t_end - t0 : 1e-9;
+  if (pairs == 1) {
+    FILE *f = fopen(argv[2], "wb");
+    if (!f) return 1;
+    fwrite("NGWO", 1, 4, f);
+    fwrite(&n, 4, 1, f);
+    for (uint32_t i = 0; i < n; ++i) {
+      fwrite(&sent_len[i], 4, 1, f);
+      fwrite(sent[i], 1, sent_len[i], f);
+    }
+    fwrite(&nrx, 4, 1, f);
+    for (uint32_t i = 0; i < nrx; ++i) {
+      fwrite(&rx_len[i], 4, 1, f);
+      fwrite(rx[i], 1, rx_len[i], f);
+      fwrite(&res[i], sizeof res[i], 1, f);
+      fwrite(&dst_cap[i], 4, 1, f);
+      fwrite(dst[i], 1, dst_cap[i], f);
+    }
+    fclose(f);
+  }
   printf("{\"packets\": %u, \"sent\": %u, \"received\": %u, \"lost\": %u, \"batch\": %u, "
-         "\"window\": %u, \"rcvbuf\": %d, \"seconds\": %.6f, \"ip_bytes\": %llu, "
-         "\"socket_to_socket_gbps\": %.3f}\n",
-         n, nsent, nrx, nsent - nrx, g.batch, g.window, rcvbuf, secs, (unsigned long long)bytes,
-         bytes * 8.0 / secs / 1e9);
-  wg_tunn_destroy(g.a);
-  wg_tunn_destroy(g.b);
+         "\"pairs\": %u, \"window\": %u, \"rcvbuf\": %d, \"seconds\": %.6f, \"ip_bytes\": %llu, "
+         "\"socket_to_socket_gbps\": %.3f, \"thread_seconds\": {\"encapsulate\": %.4f, "
+         "\"sendmmsg\": %.4f, \"window_wait\": %.4f, \"recvmmsg\": %.4f, \"decapsulate\": %.4f}}\n",
+         n, nsent, nrx, nsent - nrx, batch, pairs, gs[0].window, rcvbuf, secs,
+         (unsigned long long)bytes, bytes * 8.0 / secs / 1e9, te, ts, tw, tr, td);
+  for (uint32_t p = 0; p < pairs; ++p) {
+    wg_tunn_destroy(gs[p].a);
+    wg_tunn_destroy(gs[p].b);
+  }
   wg_gpu_ctx_destroy(ctx);
   return 0;
 }

@@ -51,7 +51,8 @@ def main():
     # handshake initiations: 4096 distinct valid messages tiled over the batch
     resp_priv = bytes(range(32))
     resp_pub = H.public_key(resp_priv)
-    base = [H.format_handshake_initiation(rng.randbytes(32), resp_pub, rng.randbytes(32), i,
+    init_privs = [rng.randbytes(32) for _ in range(512)]
+    base = [H.format_handshake_initiation(init_privs[i], resp_pub, rng.randbytes(32), i,
                                           rng.randbytes(12)) for i in range(512)]
     tile = b"".join(base)
     msgs = torch.from_numpy(np.frombuffer(tile * (n // len(base)), np.uint8).copy()).cuda()
@@ -75,6 +76,87 @@ def main():
     print(json.dumps({"op": "handshake_anon (mac1 + parse_handshake_anon)", "n": m,
                       "ms": round(t * 1e3, 3), "msgs_per_s": round(m / t, 1),
                       "verified_sample": ok}), flush=True)
+
+    # responder: receive_handshake_initialization crypto, then format_handshake_response
+    from neptun_amd import gpu as G
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        tt = []
+        for _ in range(5):
+            ev[0].record()
+            fn()
+            ev[1].record()
+            torch.cuda.synchronize()
+            tt.append(ev[0].elapsed_time(ev[1]) * 1e-3)
+        return statistics.median(tt)
+
+    peers_base = np.zeros(len(base), G.RESPONDER_PEER_DTYPE)
+    for i, k in enumerate(init_privs):
+        pub = H.public_key(k)
+        peers_base[i]["peer_static_public"] = np.frombuffer(pub, np.uint8)
+        peers_base[i]["static_shared"] = np.frombuffer(H.x25519(resp_priv, pub), np.uint8)
+    peers = torch.from_numpy(np.tile(peers_base, m // len(base)).view(np.uint8).copy()).cuda()
+    states = torch.zeros(m * G.INIT_RECEIVED_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    t = timed(lambda: ctx.handshake_consume_batch(resp_priv, m, msgs, 148, peers, states))
+    st = states.cpu().numpy().view(G.INIT_RECEIVED_DTYPE)
+    ok = bool((st["status"] == 0).all())
+    for i in rng.sample(range(m), 16):
+        want = H.consume_initiation(resp_priv, peers_base[i % len(base)]["peer_static_public"].tobytes(),
+                                    peers_base[i % len(base)]["static_shared"].tobytes(),
+                                    base[i % len(base)])
+        ok = ok and st[i]["chaining_key"].tobytes() == want[3] and st[i]["hash"].tobytes() == want[4]
+    print(json.dumps({"op": "handshake_consume (receive_handshake_initialization crypto)", "n": m,
+                      "ms": round(t * 1e3, 3), "msgs_per_s": round(m / t, 1),
+                      "verified_sample": ok}), flush=True)
+    jobs_np = np.zeros(m, G.RESPONSE_JOB_DTYPE)
+    jobs_np["ephemeral_private"] = np.frombuffer(rng.randbytes(32 * m), np.uint8).reshape(m, 32)
+    jobs_np["peer_static_public"] = np.tile(peers_base, m // len(base))["peer_static_public"]
+    # the response's mac1 is keyed by the INITIATOR's static public key
+    mac1_keys = np.stack([np.frombuffer(H.b2s_hash(H.LABEL_MAC1, p["peer_static_public"].tobytes()),
+                                        np.uint8) for p in peers_base])
+    jobs_np["mac1_key"] = np.tile(mac1_keys, (m // len(base), 1))
+    jobs_np["local_index"] = np.arange(m, dtype=np.uint32)
+    jobs = torch.from_numpy(jobs_np.view(np.uint8).copy()).cuda()
+    outs = torch.zeros(m * G.RESPONSE_OUT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    t = timed(lambda: ctx.handshake_respond_batch(m, states, jobs, outs))
+    o = outs.cpu().numpy().view(G.RESPONSE_OUT_DTYPE)
+    ok = True
+    for i in rng.sample(range(m), 8):
+        _, idx, ts_, ck, h, eph = H.consume_initiation(
+            resp_priv, peers_base[i % len(base)]["peer_static_public"].tobytes(),
+            peers_base[i % len(base)]["static_shared"].tobytes(), base[i % len(base)])
+        resp = H.format_response(ck, h, eph, idx, i, jobs_np[i]["ephemeral_private"].tobytes(),
+                                 jobs_np[i]["peer_static_public"].tobytes())[0]
+        ok = ok and o[i]["message"].tobytes() == resp
+    print(json.dumps({"op": "handshake_respond (format_handshake_response + mac1)", "n": m,
+                      "ms": round(t * 1e3, 3), "msgs_per_s": round(m / t, 1),
+                      "verified_sample": ok}), flush=True)
+    # under load: mac2 check of every initiation, cookie reply for each
+    lens = torch.full((m,), 148, dtype=torch.int32, device="cuda")
+    addrs = torch.randint(0, 256, (16 * m,), dtype=torch.uint8, device="cuda", generator=g)
+    cookies = torch.zeros(16 * m, dtype=torch.uint8, device="cuda")
+    cst = torch.zeros(m, dtype=torch.int32, device="cuda")
+    secret = rng.randbytes(16)
+    t = timed(lambda: ctx.mac2_check_batch(secret, 7, m, msgs, 148, lens, addrs, cookies, cst))
+    ok = bool((cst == 1).all())
+    print(json.dumps({"op": "mac2_check (current_cookie + mac2, under load)", "n": m,
+                      "ms": round(t * 1e3, 3), "msgs_per_s": round(m / t, 1),
+                      "verified_sample": ok}), flush=True)
+    cj = np.zeros(m, G.COOKIE_REPLY_JOB_DTYPE)
+    cj["cookie"] = cookies.cpu().numpy().reshape(m, 16)
+    cj["nonce_ctr"] = np.arange(m, dtype=np.uint64)
+    d_cj = torch.from_numpy(cj.view(np.uint8).copy()).cuda()
+    replies = torch.zeros(64 * m, dtype=torch.uint8, device="cuda")
+    ck_key, n_key = H.b2s_hash(H.LABEL_COOKIE, resp_pub), rng.randbytes(32)
+    t = timed(lambda: ctx.cookie_reply_batch(ck_key, n_key, m, d_cj, replies))
+    rb = replies.cpu().numpy().tobytes()
+    ok = all(rb[64 * i:64 * i + 64] == H.format_cookie_reply(ck_key, 0, cj[i]["cookie"].tobytes(),
+                                                            bytes(16), H.cookie_nonce(n_key, i))
+             for i in rng.sample(range(m), 16))
+    print(json.dumps({"op": "cookie_reply (XChaCha20-Poly1305)", "n": m, "ms": round(t * 1e3, 3),
+                      "msgs_per_s": round(m / t, 1), "verified_sample": ok}), flush=True)
     exe = os.path.join(ROOT, "oracle", "build", "cpu_x25519")
     if os.path.exists(exe):
         threads = min(16, len(os.sched_getaffinity(0)))
