@@ -50,6 +50,16 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_ABLATE_NO_CRYPT 0
 #endif
 
+// timing-only energy / bound probes (wrong outputs): no Poly1305 blocks / no
+// LDS traffic of the crypt step (text words taken from registers, results
+// dropped).  DESIGN.md 3.1 has what they showed.
+#ifndef WG_ABLATE_NO_POLY
+#define WG_ABLATE_NO_POLY 0
+#endif
+#ifndef WG_ABLATE_NO_LDS_CRYPT
+#define WG_ABLATE_NO_LDS_CRYPT 0
+#endif
+
 #ifndef WG_WAVES_PER_SIMD
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
 #endif
@@ -567,8 +577,12 @@ __device__ __forceinline__ void stage_out(uint4 *run, const DescGeom &g, uint32_
 template <bool kSeal>
 __device__ __forceinline__ void crypt_chunk(uint4 &slot, Poly &p, int m, uint32_t P,
                                             uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+#if WG_ABLATE_NO_LDS_CRYPT
+  uint32_t i0 = (uint32_t)m, i1 = P, i2 = a + (uint32_t)m, i3 = b ^ P;
+#else
   const uint4 v = slot;
   uint32_t i0 = v.x, i1 = v.y, i2 = v.z, i3 = v.w;
+#endif
   uint32_t o0 = i0 ^ a, o1 = i1 ^ b, o2 = i2 ^ c, o3 = i3 ^ d;
   const int valid = (int)P - m;
   if (valid < 16) {  // the packet's last, partial chunk: AEAD pad16 zero-fills it
@@ -577,9 +591,17 @@ __device__ __forceinline__ void crypt_chunk(uint4 &slot, Poly &p, int m, uint32_
     i0 &= m0; i1 &= m1; i2 &= m2; i3 &= m3;
     o0 &= m0; o1 &= m1; o2 &= m2; o3 &= m3;
   }
+#if WG_ABLATE_NO_POLY
+  p.h0 ^= o0 ^ i1; p.h1 ^= o1 ^ i2; p.h2 ^= o2 ^ i3; p.h3 ^= o3 ^ i0;
+#else
   if (kSeal) poly_block(p, o0, o1, o2, o3);  // MAC the ciphertext
   else poly_block(p, i0, i1, i2, i3);
+#endif
+#if WG_ABLATE_NO_LDS_CRYPT
+  p.h4 ^= o0 ^ o1 ^ o2 ^ o3;
+#else
   slot = make_uint4(o0, o1, o2, o3);
+#endif
 }
 
 // Process round r of this lane's packet: chunk k sits at wire w = 128r + 16k,
