@@ -59,6 +59,12 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #ifndef WG_ABLATE_NO_LDS_CRYPT
 #define WG_ABLATE_NO_LDS_CRYPT 0
 #endif
+#ifndef WG_ABLATE_ALL_INTERIOR
+#define WG_ABLATE_ALL_INTERIOR 0  // every round staged as a full 128-byte run (edge bytes wrong)
+#endif
+#ifndef WG_ABLATE_NO_KEYBLOCK
+#define WG_ABLATE_NO_KEYBLOCK 0  // seal: skip the per-packet Poly1305 key block
+#endif
 
 #ifndef WG_WAVES_PER_SIMD
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
@@ -434,7 +440,7 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint3
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   // (open: packets dropped at the header check are loaded like the others --
   // harmless, their lanes skip the crypto and stage_out never writes them back)
-  if (kRun * r >= Ranges<kSeal>::in_lo() && kRun * r + kRun <= hi) {
+  if (WG_ABLATE_ALL_INTERIOR || (kRun * r >= Ranges<kSeal>::in_lo() && kRun * r + kRun <= hi)) {
     // interior round (wave-uniform test): every lane moves a full chunk, the
     // per-lane offsets are round-independent -- no range checks
     const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
@@ -468,7 +474,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   // drain the DMA in flight
   uint64_t dead = kSeal ? 0ull : g.dead;
   if constexpr (!kSeal) asm volatile("" : "+s"(dead));
-  if (kRun * r >= Ranges<kSeal>::out_lo() && kRun * r + kRun <= hi && dead == 0) {
+  if (WG_ABLATE_ALL_INTERIOR || (kRun * r >= Ranges<kSeal>::out_lo() && kRun * r + kRun <= hi && dead == 0)) {
     // interior round: 8 full-chunk stores at round-independent per-lane offsets
     // (all 8 LDS reads first: the asm stores are memory barriers to the
     // compiler, which otherwise serialises read -> wait -> store per piece)
@@ -483,7 +489,6 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
     }
     return;
   }
-  bool partial = false;
   uint4 v[kChunks];
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) v[j] = run[64u * j + lane];
@@ -496,35 +501,27 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
     const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
     store16(vv, g.out0, records, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
             8u * j * stride + kRun * r);
-    partial |= ok && hi - w < 16u;
   }
-  if (partial) {  // the packet's last, partial chunk (last round only)
-    // n = 1..15 bytes as 3 dword + 1 short + 1 byte buffer stores, each masked
-    // per lane by an out-of-range offset: a static instruction count, so the
-    // compiler's vmcnt bookkeeping stays exact across rounds
-#pragma unroll
-    for (uint32_t j = 0; j < kChunks; ++j) {
-      const uint32_t k = (j & 1u) ? k1 : k0;
-      const uint32_t w = kRun * r + 16u * k;
-      const bool gone = !kSeal && ((((uint32_t)(dead >> (8u * j))) >> y) & 1u);
-      const bool mine = !gone && w >= Ranges<kSeal>::out_lo() && w < hi && hi - w < 16u;
-      const uint32_t n = mine ? hi - w : 0u;
-      const uint4 v = run[64u * j + lane];
-      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-      const uint32_t base = y * stride + 16u * k, soff = 8u * j * stride + kRun * r;
-#pragma unroll
-      for (uint32_t d = 0; d < 3; ++d)
-        __builtin_amdgcn_raw_buffer_store_b32(wv[d], rs, 4u * (d + 1u) <= n ? base + 4u * d
-                                                                            : kNoAccess, soff,
-                                              WG_STORE_CPOL);
-      const uint32_t nd = n >> 2, rem = n & 3u;
-      const uint32_t last = nd == 0 ? wv[0] : nd == 1 ? wv[1] : nd == 2 ? wv[2] : wv[3];
-      __builtin_amdgcn_raw_buffer_store_b16((unsigned short)last, rs,
-                                            rem >= 2u ? base + 4u * nd : kNoAccess, soff, WG_STORE_CPOL);
+  // The packets' last, partial chunk: q = hi % 16 bytes at wire offset wp, the
+  // same for every packet of the wave (uniform length).  Its owner lane stores
+  // it straight from its per-packet LDS row: at most 3 dword + 1 short + 1 byte
+  // stores for the whole wave (wave-uniform branches, so the compiler's vmcnt
+  // bookkeeping stays exact), instead of the cooperative shape's 5 per piece.
+  const uint32_t q = hi & 15u, wp = hi & ~15u;
+  if (q && (wp >> 7) == r && wp >= Ranges<kSeal>::out_lo()) {
+    const bool gone = !kSeal && ((dead >> lane) & 1ull);
+    const uint4 c = run[8u * lane + (((wp >> 4) & 7u) ^ swz(lane))];
+    const uint32_t base = gone ? kNoAccess : lane * stride + wp;
+    if (q >= 4u) __builtin_amdgcn_raw_buffer_store_b32(c.x, rs, base, 0, WG_STORE_CPOL);
+    if (q >= 8u) __builtin_amdgcn_raw_buffer_store_b32(c.y, rs, base + 4u, 0, WG_STORE_CPOL);
+    if (q >= 12u) __builtin_amdgcn_raw_buffer_store_b32(c.z, rs, base + 8u, 0, WG_STORE_CPOL);
+    const uint32_t nd = q >> 2, rem = q & 3u;
+    const uint32_t last = nd == 0 ? c.x : nd == 1 ? c.y : nd == 2 ? c.z : c.w;
+    if (rem >= 2u)
+      __builtin_amdgcn_raw_buffer_store_b16((unsigned short)last, rs, base + 4u * nd, 0, WG_STORE_CPOL);
+    if (rem & 1u)
       __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(last >> (8u * (rem & 2u))), rs,
-                                           (rem & 1u) ? base + 4u * nd + (rem & 2u) : kNoAccess,
-                                           soff, WG_STORE_CPOL);
-    }
+                                           base + 4u * nd + (rem & 2u), 0, WG_STORE_CPOL);
   }
 }
 
@@ -685,6 +682,14 @@ __device__ __forceinline__ void tail_words(const uint32_t (&ct)[4], const uint32
   for (int j = 0; j < 8; ++j) out[j] = r[j] | bytes_at(tag, 4 * j - q);
 }
 
+// A uniform batch's one session key, loaded once per kernel into SGPRs: a
+// per-group key load would be a vector load whose wait drains the previous
+// group's stores at every group start.
+struct SessionKey {
+  uint32_t k[8];
+  uint32_t sidx;
+};
+
 struct PacketJob {
   uint64_t in_base, out_base;  // wire-coordinate origins (see WaveStage)
   uint64_t counter;            // seal: nonce counter; open: from the header
@@ -699,7 +704,7 @@ struct PacketJob {
 template <bool kSeal, bool kUniform, bool kSync, class Stage, class Geom>
 __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
-                                         int32_t *status_out) {
+                                         int32_t *status_out, const SessionKey *pre = nullptr) {
   // phase-locked: every wave of the workgroup runs the same number of rounds
   // (uniform batches by construction, descriptor batches via DescGeom::wg_max)
   // ---- per-packet setup (owner lane) ------------------------------------
@@ -732,7 +737,11 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 
   uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t sidx = 0;
-  if (kUniform || job.status == WG_STATUS_OK) {
+  if (kUniform && pre) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) key[j] = pre->k[j];
+    sidx = pre->sidx;
+  } else if (kUniform || job.status == WG_STATUS_OK) {
     const uint4 a = ld16(keys + 32u * job.slot), b = ld16(keys + 32u * job.slot + 16u);
     key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
     key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
@@ -862,7 +871,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 #if !WG_ABLATE_NO_MEM
       stage_in<kSeal>(run, g, lane, 0);
 #endif
-      if (kSeal) one_time_key();  // while round 0's DMA is in flight (every wave: phase-locked)
+      if (kSeal && !WG_ABLATE_NO_KEYBLOCK) one_time_key();  // while round 0's DMA is in flight (every wave: phase-locked)
       if (!kSeal && my_runs) open_header(hdr);
     }
     for (uint32_t r = 0; r < rounds; ++r) {
@@ -974,7 +983,8 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 // one wave's 64 packets [pkt0, pkt0 + 64) of a strided batch
 template <bool kSeal, bool kTail, class Stage>
 __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams &prm,
-                                              uint32_t pkt0, uint32_t lane) {
+                                              uint32_t pkt0, uint32_t lane,
+                                              const SessionKey *sk = nullptr) {
   const uint32_t i = pkt0 + lane;
   PacketJob job;
   job.slot = prm.key_slot;
@@ -992,7 +1002,7 @@ __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams 
     const uint32_t W = kSeal ? prm.len + WG_DATA_OVERHEAD_SZ : prm.len;
     UniformGeom g{in0, out0, prm.src_stride, prm.dst_stride, 0ull, W,
                   (kSeal || prm.len >= WG_DATA_OVERHEAD_SZ) ? (W + kRun - 1) / kRun : 0u};
-    run_wave<kSeal, true, WG_SYNC != 0>(stage, g, lane, job, prm.keys, prm.key_index, st);
+    run_wave<kSeal, true, WG_SYNC != 0>(stage, g, lane, job, prm.keys, prm.key_index, st, sk);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
     LdsGeom g{stage};
@@ -1016,12 +1026,21 @@ aead_strided_kernel(StridedParams prm) {
     // workgroups stay in their steady, mutually de-phased rhythm (one DMA
     // in flight while the other computes) instead of restarting in step
     const uint32_t groups = (prm.n / 64u + kWaves - 1u) / kWaves;
+    SessionKey sk;
+    {
+      const uint8_t *kp = prm.keys + 32u * prm.key_slot;
+      const uint4 a = ld16(kp), b = ld16(kp + 16u);
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sk.k[j] = __builtin_amdgcn_readfirstlane(w[j]);
+      sk.sidx = __builtin_amdgcn_readfirstlane(prm.key_index[prm.key_slot]);
+    }
     for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
       const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
       // only the last group can be partial, and it is this workgroup's last
       // iteration: a wave without packets ends (ended waves leave the barrier)
       if (pkt0 + 64u > prm.n) return;
-      strided_group<kSeal, false>(stage[wave], prm, pkt0, lane);
+      strided_group<kSeal, false>(stage[wave], prm, pkt0, lane, &sk);
     }
   }
 }

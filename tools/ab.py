@@ -115,6 +115,7 @@ def main():
     if os.environ.get("AB_CONFIG", "2") != "2":
         return main_desc(paths, int(os.environ["AB_CONFIG"]))
     n, P, S = 1 << 20, int(os.environ.get("AB_SIZE", 1350)), 0
+    oo = int(os.environ.get("AB_OPEN_OFF", 16))  # open's plaintext offset in its output slot
     S = synth.round_up(P + 32, 128)
     rounds = int(os.environ.get("AB_ROUNDS", 15))
     dev = torch.device("cuda", 0)
@@ -138,7 +139,7 @@ def main():
                                      st.data_ptr(), stream) == 0
 
     def open_(L, h):
-        assert L.wg_gpu_open_strided(h, n, P + 32, 0, wire.data_ptr(), S, back.data_ptr() + 16, S,
+        assert L.wg_gpu_open_strided(h, n, P + 32, 0, wire.data_ptr(), S, back.data_ptr() + oo, S,
                                      st.data_ptr(), stream) == 0
 
     ref_wire = None
@@ -146,7 +147,7 @@ def main():
         wire.zero_(); back.zero_()
         seal(L, h); open_(L, h)
         torch.cuda.synchronize()
-        ok = torch.equal(back.view(n, S)[:, 16:16 + P], pt.view(n, S)[:, 16:16 + P]) and int(st.abs().sum()) == 0
+        ok = torch.equal(back.view(n, S)[:, oo:oo + P], pt.view(n, S)[:, 16:16 + P]) and int(st.abs().sum()) == 0
         w = wire.view(n, S)[:, :P + 32]
         if ref_wire is None:
             ref_wire = w.clone()
