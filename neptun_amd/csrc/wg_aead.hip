@@ -186,13 +186,21 @@ __device__ __forceinline__ uint64_t wave_max64(uint64_t x) {
 
 __device__ __forceinline__ void lds_wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-template <bool kSeal>
+// Run grids.  The wire grid (kText = false) cuts every packet into 128-byte
+// runs of the DATAGRAM (grid coordinate = wire offset): seal's output and
+// NepTUN's TUN-buffer plaintext (16 bytes in) both sit on it.  The text grid
+// (open only) cuts the TEXT into runs (grid coordinate = wire offset - 16): for
+// plaintext destinations that start on a 128-byte boundary, so every output
+// line is written whole, in one round (the datagram header is then outside the
+// grid and fetched on its own).
+template <bool kSeal, bool kText = false>
 struct Ranges {
-  // input bytes live in [in_lo, in_hi) and output bytes in [out_lo, out_hi) of wire coordinates
+  // input bytes live in [in_lo, in_hi) and output bytes in [out_lo, out_hi) of grid coordinates
+  static_assert(!(kSeal && kText), "the text grid is for open");
   __device__ static uint32_t in_lo() { return kSeal ? 16u : 0u; }
-  __device__ static uint32_t in_hi(uint32_t W) { return kSeal ? W - 16u : W; }
-  __device__ static uint32_t out_lo() { return kSeal ? 0u : 16u; }
-  __device__ static uint32_t out_hi(uint32_t W) { return kSeal ? W : W - 16u; }
+  __device__ static uint32_t in_hi(uint32_t W) { return kSeal || kText ? W - 16u : W; }
+  __device__ static uint32_t out_lo() { return kSeal || kText ? 0u : 16u; }
+  __device__ static uint32_t out_hi(uint32_t W) { return kSeal ? W : kText ? W - 32u : W - 16u; }
 };
 
 // Per-packet geometry of the wave's 64 packets, two flavours:
@@ -201,6 +209,7 @@ struct Ranges {
 //  * UniformGeom: one length, strided slots, all 64 lanes live -- arithmetic,
 //    wave-uniform lengths, so every length-dependent branch is a scalar one.
 struct LdsGeom {
+  static constexpr bool kTextGrid = false;
   WaveStage &S;
   __device__ bool live(uint32_t p, uint32_t r) const { return r < S.nruns[p]; }
   __device__ uint32_t wlen(uint32_t p) const { return S.wlen[p]; }
@@ -221,6 +230,7 @@ struct WaveStageDesc {
 };
 
 struct DescGeom {
+  static constexpr bool kTextGrid = false;
   WaveStageDesc &S;
   uint64_t in_ref, out_ref;      // src - 16, dst - 16
   uint32_t *wg_rounds;           // [waves] round counts of the workgroup's waves
@@ -295,8 +305,10 @@ struct DescGeom {
   }
 };
 
-struct UniformGeom {
-  uint64_t in0, out0, in_stride, out_stride;
+template <bool kText>
+struct UniformGeomT {
+  static constexpr bool kTextGrid = kText;
+  uint64_t in0, out0, in_stride, out_stride;  // grid origins of packet 0, slot strides
   uint64_t dead;   // wave mask of packets dropped at the header check (open)
   uint32_t W, nr;  // datagram length and rounds, same for every packet
   __device__ bool live(uint32_t p, uint32_t r) const { return r < nr && !((dead >> p) & 1u); }
@@ -304,6 +316,7 @@ struct UniformGeom {
   __device__ uint64_t in_base(uint32_t p) const { return in0 + (uint64_t)p * in_stride; }
   __device__ uint64_t out_base(uint32_t p) const { return out0 + (uint64_t)p * out_stride; }
 };
+using UniformGeom = UniformGeomT<false>;
 
 // Memory instructions of the generic (per-packet address) staging, written so
 // that the compiler inserts no waits of its own between them:
@@ -426,11 +439,12 @@ __device__ __forceinline__ void store16(u32x4 data, uint64_t base, uint32_t byte
                :: "v"(data), "v"(voff), "s"(rs), "s"(soff) : "memory");
 }
 
-template <bool kSeal>
-__device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint32_t lane,
+template <bool kSeal, bool kText>
+__device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &g, uint32_t lane,
                                          uint32_t r) {
+  using R = Ranges<kSeal, kText>;
   const uint32_t stride = (uint32_t)g.in_stride;
-  const uint32_t hi = Ranges<kSeal>::in_hi(g.W);
+  const uint32_t hi = R::in_hi(g.W);
   // num_records = the end of the wave's last packet's input, rounded up to its
   // 16-byte chunk: the range check drops a WHOLE 16-byte access that crosses
   // num_records (the tail chunk reads up to 15 bytes past the packet -- inside
@@ -440,7 +454,7 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint3
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   // (open: packets dropped at the header check are loaded like the others --
   // harmless, their lanes skip the crypto and stage_out never writes them back)
-  if (WG_ABLATE_ALL_INTERIOR || (kRun * r >= Ranges<kSeal>::in_lo() && kRun * r + kRun <= hi)) {
+  if (WG_ABLATE_ALL_INTERIOR || (kRun * r >= R::in_lo() && kRun * r + kRun <= hi)) {
     // interior round (wave-uniform test): every lane moves a full chunk, the
     // per-lane offsets are round-independent -- no range checks
     const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
@@ -454,18 +468,19 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeom &g, uint3
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
-    const bool ok = w >= Ranges<kSeal>::in_lo() && w < hi;
+    const bool ok = w >= R::in_lo() && w < hi;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16,
                                              ok ? y * stride + 16u * k : kNoAccess,
                                              8u * j * stride + kRun * r, 0, WG_LOAD_CPOL);
   }
 }
 
-template <bool kSeal>
-__device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint32_t lane,
+template <bool kSeal, bool kText>
+__device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> &g, uint32_t lane,
                                           uint32_t r) {
+  using R = Ranges<kSeal, kText>;
   const uint32_t stride = (uint32_t)g.out_stride;
-  const uint32_t hi = Ranges<kSeal>::out_hi(g.W);
+  const uint32_t hi = R::out_hi(g.W);
   const uint32_t records = 63u * stride + ((hi + 15u) & ~15u);  // (see stage_in)
   const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, records);
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
@@ -474,7 +489,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   // drain the DMA in flight
   uint64_t dead = kSeal ? 0ull : g.dead;
   if constexpr (!kSeal) asm volatile("" : "+s"(dead));
-  if (WG_ABLATE_ALL_INTERIOR || (kRun * r >= Ranges<kSeal>::out_lo() && kRun * r + kRun <= hi && dead == 0)) {
+  if (WG_ABLATE_ALL_INTERIOR || (kRun * r >= R::out_lo() && kRun * r + kRun <= hi && dead == 0)) {
     // interior round: 8 full-chunk stores at round-independent per-lane offsets
     // (all 8 LDS reads first: the asm stores are memory barriers to the
     // compiler, which otherwise serialises read -> wait -> store per piece)
@@ -497,7 +512,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
     const bool gone = !kSeal && ((((uint32_t)(dead >> (8u * j))) >> y) & 1u);
-    const bool ok = !gone && w >= Ranges<kSeal>::out_lo() && w < hi;
+    const bool ok = !gone && w >= R::out_lo() && w < hi;
     const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
     store16(vv, g.out0, records, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
             8u * j * stride + kRun * r);
@@ -508,7 +523,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeom &g, uint
   // stores for the whole wave (wave-uniform branches, so the compiler's vmcnt
   // bookkeeping stays exact), instead of the cooperative shape's 5 per piece.
   const uint32_t q = hi & 15u, wp = hi & ~15u;
-  if (q && (wp >> 7) == r && wp >= Ranges<kSeal>::out_lo()) {
+  if (q && (wp >> 7) == r && wp >= R::out_lo()) {
     const bool gone = !kSeal && ((dead >> lane) & 1ull);
     const uint4 c = run[8u * lane + (((wp >> 4) & 7u) ^ swz(lane))];
     const uint32_t base = gone ? kNoAccess : lane * stride + wp;
@@ -642,21 +657,42 @@ __device__ __forceinline__ void crypt_round(uint4 *run, uint32_t lane, uint32_t 
 // The same round with both keystream blocks computed beforehand
 // (chacha20_block2_sync(ka, kb, key, 2r + 1, ...)): chunk 0 (keystream saved
 // from the previous round), then chunks 1-7.
-template <bool kSeal>
+// (text grid: chunk k of round r is text 128r + 16k -- blocks 2r + 1 and
+// 2r + 2 cover the round exactly, nothing is carried between rounds)
+template <bool kSeal, bool kText = false>
 __device__ __forceinline__ void apply_chunk0(uint4 *run, uint32_t lane, uint32_t r, uint32_t P,
                                              Poly &p, const uint32_t ks_save[4]) {
+  if constexpr (kText) return;
   const int m0 = (int)(kRun * r) - 16;
   if (r > 0 && m0 < (int)P)
     crypt_chunk<kSeal>(run[8u * lane + (0u ^ swz(lane))], p, m0, P, ks_save[0], ks_save[1],
                        ks_save[2], ks_save[3]);
 }
 
-template <bool kSeal>
+template <bool kSeal, bool kText = false>
 __device__ __forceinline__ void apply_blocks(uint4 *run, uint32_t lane, uint32_t r, uint32_t P,
                                              const uint32_t (&ka)[16], const uint32_t (&kb)[16],
                                              Poly &p, uint32_t ks_save[4]) {
-  const int m0 = (int)(kRun * r) - 16;
   const uint32_t row = 8u * lane, sw = swz(lane);
+  if constexpr (kText) {
+    const int m0 = (int)(kRun * r);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int m = m0 + 16 * k;
+      if (m < (int)P)
+        crypt_chunk<kSeal>(run[row + ((uint32_t)k ^ sw)], p, m, P, ka[4 * k], ka[4 * k + 1],
+                           ka[4 * k + 2], ka[4 * k + 3]);
+    }
+#pragma unroll
+    for (int k = 4; k < 8; ++k) {
+      const int m = m0 + 16 * k;
+      if (m < (int)P)
+        crypt_chunk<kSeal>(run[row + ((uint32_t)k ^ sw)], p, m, P, kb[4 * k - 16], kb[4 * k - 15],
+                           kb[4 * k - 14], kb[4 * k - 13]);
+    }
+    return;
+  }
+  const int m0 = (int)(kRun * r) - 16;
 #pragma unroll
   for (int k = 1; k <= 4; ++k) {
     const int m = m0 + 16 * k;
@@ -705,6 +741,10 @@ template <bool kSeal, bool kUniform, bool kSync, class Stage, class Geom>
 __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
                                          int32_t *status_out, const SessionKey *pre = nullptr) {
+  // run grid (Ranges): kG = grid coordinate of text byte 0
+  constexpr bool kText = Geom::kTextGrid;
+  constexpr uint32_t kG = kText ? 0u : 16u;
+  static_assert(!kText || (kSync && kUniform && !kSeal), "text grid: uniform phase-locked open only");
   // phase-locked: every wave of the workgroup runs the same number of rounds
   // (uniform batches by construction, descriptor batches via DescGeom::wg_max)
   // ---- per-packet setup (owner lane) ------------------------------------
@@ -720,7 +760,8 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       P = W - WG_DATA_OVERHEAD_SZ;
     }
   }
-  uint32_t my_runs = job.status == WG_STATUS_OK ? (W + kRun - 1) / kRun : 0u;
+  // runs covering the grid span of the datagram (text grid: without its header)
+  uint32_t my_runs = job.status == WG_STATUS_OK ? (W - (16u - kG) + kRun - 1) / kRun : 0u;
   uint32_t rounds;
   if constexpr (kUniform) {
     rounds = my_runs;  // uniform: job.len is a kernel argument
@@ -752,7 +793,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   uint32_t ks_save[4] = {0, 0, 0, 0};
   uint32_t n1 = (uint32_t)job.counter, n2 = (uint32_t)(job.counter >> 32);
   const uint32_t q = P & 15u;                    // bytes in the partial ciphertext chunk
-  const uint32_t wt = 16u + (P & ~15u);          // wire offset of the tail chunk
+  const uint32_t wt = kG + (P & ~15u);           // grid offset of the tail chunk
   uint32_t tailB[4] = {0, 0, 0, 0};              // seal: chunk after the tail chunk (tag rest)
   uint32_t tg[4] = {0, 0, 0, 0};                 // open: the received tag, bytes [W - 16, W)
 
@@ -865,7 +906,8 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       // (a global-address-space load: a flat one may alias LDS and makes the
       // compiler drain the LDS-DMA in flight before it)
       if (!kSeal && my_runs) {
-        const u32x4 h = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(job.in_base);
+        const u32x4 h = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(
+            job.in_base - (16u - kG));  // (the datagram start)
         hdr = make_uint4(h.x, h.y, h.z, h.w);
       }
 #if !WG_ABLATE_NO_MEM
@@ -897,14 +939,14 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         WG_STAMP_AT(kSeal, r, 2);
         landed();
         if (my_runs) {
-          apply_chunk0<kSeal>(run, lane, r, P, poly, ks_save);
-          apply_blocks<kSeal>(run, lane, r, P, ka, kb, poly, ks_save);
+          apply_chunk0<kSeal, kText>(run, lane, r, P, poly, ks_save);
+          apply_blocks<kSeal, kText>(run, lane, r, P, ka, kb, poly, ks_save);
           if (kSeal) seal_tail(run, r);
         }
       } else {
         landed();
         if (my_runs && !WG_ABLATE_NO_CRYPT) {
-          apply_chunk0<kSeal>(run, lane, r, P, poly, ks_save);
+          apply_chunk0<kSeal, kText>(run, lane, r, P, poly, ks_save);
           if (kSeal) seal_tail(run, r);
         }
       }
@@ -961,7 +1003,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // (global-address-space stores: a flat store may alias LDS and would
       // make the compiler drain in-flight LDS-DMA around it)
-      uint8_t *pt = reinterpret_cast<uint8_t *>(job.out_base) + 16u;
+      uint8_t *pt = reinterpret_cast<uint8_t *>(job.out_base) + kG;
       const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
       for (uint32_t off = 0; off + 16u <= P; off += 16u) gstore16(pt + off, zero);
       if (q) {
@@ -981,7 +1023,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 // uniform geometry; kTail = true is a one-wave launch for the n % 64 packets
 // left over (generic geometry), so the hot kernel carries no generic path.
 // one wave's 64 packets [pkt0, pkt0 + 64) of a strided batch
-template <bool kSeal, bool kTail, class Stage>
+template <bool kSeal, bool kTail, bool kText, class Stage>
 __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams &prm,
                                               uint32_t pkt0, uint32_t lane,
                                               const SessionKey *sk = nullptr) {
@@ -992,16 +1034,19 @@ __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams 
   job.counter = prm.counter_base + i;
   const uint64_t src0 = reinterpret_cast<uint64_t>(prm.src) + (uint64_t)pkt0 * prm.src_stride;
   const uint64_t dst0 = reinterpret_cast<uint64_t>(prm.dst) + (uint64_t)pkt0 * prm.dst_stride;
-  // the plaintext side is addressed at wire coordinate - 16
-  const uint64_t in0 = kSeal ? src0 - 16u : src0, out0 = kSeal ? dst0 : dst0 - 16u;
+  // grid origins (Ranges): wire grid -- the plaintext side sits at grid
+  // coordinate 16; text grid (open) -- the ciphertext starts at grid 0
+  const uint64_t in0 = kSeal ? src0 - 16u : kText ? src0 + 16u : src0;
+  const uint64_t out0 = kSeal || kText ? dst0 : dst0 - 16u;
   job.in_base = in0 + (uint64_t)lane * prm.src_stride;
   job.out_base = out0 + (uint64_t)lane * prm.dst_stride;
   int32_t *st = (prm.status && i < prm.n) ? prm.status + i : nullptr;
   if constexpr (!kTail) {
     job.status = WG_STATUS_OK;
     const uint32_t W = kSeal ? prm.len + WG_DATA_OVERHEAD_SZ : prm.len;
-    UniformGeom g{in0, out0, prm.src_stride, prm.dst_stride, 0ull, W,
-                  (kSeal || prm.len >= WG_DATA_OVERHEAD_SZ) ? (W + kRun - 1) / kRun : 0u};
+    UniformGeomT<kText> g{in0, out0, prm.src_stride, prm.dst_stride, 0ull, W,
+                          (kSeal || prm.len >= WG_DATA_OVERHEAD_SZ)
+                              ? (W - (kText ? 16u : 0u) + kRun - 1) / kRun : 0u};
     run_wave<kSeal, true, WG_SYNC != 0>(stage, g, lane, job, prm.keys, prm.key_index, st, sk);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
@@ -1010,17 +1055,15 @@ __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams 
   }
 }
 
-template <bool kSeal, bool kTail>
-__global__ __launch_bounds__(kTail ? kBlockThreads : kStridedThreads,
-                             kTail ? WG_WAVES_PER_SIMD : kStridedMinWaves) void
-aead_strided_kernel(StridedParams prm) {
+template <bool kSeal, bool kTail, bool kText>
+__device__ __forceinline__ void strided_body(const StridedParams &prm) {
   using Stage = typename std::conditional<kTail, WaveStage, WaveStageUniform>::type;
   constexpr uint32_t kWaves = (kTail ? kBlockThreads : kStridedThreads) / 64u;
   __shared__ Stage stage[kWaves];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform
   if constexpr (kTail) {
-    if (wave == 0) strided_group<kSeal, true>(stage[wave], prm, prm.n & ~63u, lane);
+    if (wave == 0) strided_group<kSeal, true, false>(stage[wave], prm, prm.n & ~63u, lane);
   } else {
     // persistent walk over workgroup-sized packet groups: the resident
     // workgroups stay in their steady, mutually de-phased rhythm (one DMA
@@ -1040,9 +1083,24 @@ aead_strided_kernel(StridedParams prm) {
       // only the last group can be partial, and it is this workgroup's last
       // iteration: a wave without packets ends (ended waves leave the barrier)
       if (pkt0 + 64u > prm.n) return;
-      strided_group<kSeal, false>(stage[wave], prm, pkt0, lane, &sk);
+      strided_group<kSeal, false, kText>(stage[wave], prm, pkt0, lane, &sk);
     }
   }
+}
+
+template <bool kSeal, bool kTail>
+__global__ __launch_bounds__(kTail ? kBlockThreads : kStridedThreads,
+                             kTail ? WG_WAVES_PER_SIMD : kStridedMinWaves) void
+aead_strided_kernel(StridedParams prm) {
+  strided_body<kSeal, kTail, false>(prm);
+}
+
+// open on the text grid (Ranges): destinations whose plaintext slots start on
+// 128-byte boundaries (launch_strided picks it); the full waves only -- the
+// last, partial wave stays on aead_strided_kernel<false, true>
+__global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_strided_open_text_kernel(
+    StridedParams prm) {
+  strided_body<false, false, true>(prm);
 }
 
 template <bool kSeal>

@@ -55,6 +55,7 @@ struct DescParams {
 };
 
 template <bool kSeal, bool kTail> __global__ void aead_strided_kernel(StridedParams prm);
+__global__ void aead_strided_open_text_kernel(StridedParams prm);
 template <bool kSeal> __global__ void aead_desc_kernel(DescParams prm);
 template <bool kSeal> __global__ void aead_desc_sync_kernel(DescParams prm);
 

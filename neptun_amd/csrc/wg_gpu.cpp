@@ -265,9 +265,15 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     // workgroup-sized packet groups (wg_aead.hip aead_strided_kernel)
     const uint32_t groups = (full_waves + waves_per_block - 1) / waves_per_block;
     const dim3 grid(std::min(groups, ctx->cus * wg::kStridedBlocksPerCU));
+    // open into plaintext slots that start on 128-byte boundaries: the text
+    // run grid keeps every output line whole (wg_aead.hip Ranges)
+    const bool text_grid = !seal && ((uintptr_t)dst % 128u) == 0 && dst_stride % 128u == 0;
     if (seal)
       hipLaunchKernelGGL((wg::aead_strided_kernel<true, false>), grid, dim3(wg::kStridedThreads),
                          0, s, prm);
+    else if (text_grid)
+      hipLaunchKernelGGL(wg::aead_strided_open_text_kernel, grid, dim3(wg::kStridedThreads), 0, s,
+                         prm);
     else
       hipLaunchKernelGGL((wg::aead_strided_kernel<false, false>), grid, dim3(wg::kStridedThreads),
                          0, s, prm);

@@ -476,12 +476,15 @@ def test_host_pipe_matches_device_path(torch_cuda, gpu, depth, chunk):
     pipe.close()
 
 
+@pytest.mark.parametrize("out_off", [16, 0])
 @pytest.mark.parametrize("P", list(range(0, 70)) + [127, 128, 129, 240, 255, 256, 257, 1000, 1349,
                                                    1350, 1351, 1407, 1500, 8900])
-def test_strided_every_tail_shape(torch_cuda, gpu, P):
+def test_strided_every_tail_shape(torch_cuda, gpu, P, out_off):
     """Uniform strided kernel (+ its one-wave tail launch) at lengths covering every
     partial-chunk size 0..15 on both sides: wire bytes equal the oracle's, nothing
-    is written outside each packet (guard bytes), open restores the plaintext."""
+    is written outside each packet (guard bytes), open restores the plaintext.
+    out_off = where open's plaintext sits in its 128-byte-multiple slot: 16 (the
+    wire run grid) or 0 (slot-aligned plaintext: the text run grid kernel)."""
     torch = torch_cuda
     n = 130  # two full uniform waves + a 2-packet tail wave
     S = synth.round_up(P + 32 + 16, 128)
@@ -505,12 +508,13 @@ def test_strided_every_tail_shape(torch_cuda, gpu, P):
     assert np.array_equal(wire.cpu().numpy(), want)  # includes the guard bytes past P + 32
     back = torch.full((n * S,), 0xCD, dtype=torch.uint8, device="cuda")
     st.fill_(-1)
-    gpu.open_strided(n, P + 32, 0, wire, S, back.data_ptr() + 16, S, st)
+    assert back.data_ptr() % 128 == 0 and S % 128 == 0
+    gpu.open_strided(n, P + 32, 0, wire, S, back.data_ptr() + out_off, S, st)
     torch.cuda.synchronize()
     assert (st == 0).all()
     got = back.cpu().numpy().reshape(n, S)
-    assert np.array_equal(got[:, 16:16 + P], src.reshape(n, S)[:, 16:16 + P])
-    assert (got[:, :16] == 0xCD).all() and (got[:, 16 + P:] == 0xCD).all()
+    assert np.array_equal(got[:, out_off:out_off + P], src.reshape(n, S)[:, 16:16 + P])
+    assert (got[:, :out_off] == 0xCD).all() and (got[:, out_off + P:] == 0xCD).all()
 
 
 def test_device_routing_then_open_matches_oracle(torch_cuda, gpu):
