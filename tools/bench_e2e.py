@@ -65,6 +65,34 @@ def main():
             if ok and (best is None or line["roundtrip_gbps"] > best["roundtrip_gbps"]):
                 best = line
             pipe.close()
+    # a full-duplex tunnel: outbound seal and inbound open batches at the same
+    # time, each through its own pipe on its own host thread (ctypes calls drop
+    # the GIL), the way a gateway's encrypt and decrypt workers overlap
+    import threading
+    c = best or {"chunk_MiB": 16, "depth": 3}
+    pa = neptun_amd.GpuPipe(ctx, chunk_bytes=c["chunk_MiB"] << 20, depth=c["depth"])
+    pb = neptun_amd.GpuPipe(ctx, chunk_bytes=c["chunk_MiB"] << 20, depth=c["depth"])
+    wire_in = wire.clone().pin_memory()  # last round's datagrams: the inbound side's input
+    st2 = torch.zeros(n, dtype=torch.int32).pin_memory()
+    walls = []
+    for _ in range(reps + 1):
+        back.zero_()
+        ta = threading.Thread(target=lambda: pa.seal_strided(n, P, 0, 0, pt.data_ptr() + 16, S, wire, S, st))
+        tb = threading.Thread(target=lambda: pb.open_strided(n, P + 32, 0, wire_in, S, back.data_ptr() + 16,
+                                                             S, st2))
+        t0 = time.perf_counter()
+        ta.start(); tb.start(); ta.join(); tb.join()
+        walls.append(time.perf_counter() - t0)
+    walls = walls[1:]
+    ok = torch.equal(back.view(n, S)[:, 16:16 + P], pt.view(n, S)[:, 16:16 + P]) and \
+        torch.equal(wire, wire_in) and int(st.abs().sum()) == 0 and int(st2.abs().sum()) == 0
+    mw = statistics.median(walls)
+    print(json.dumps({"mode": "full duplex: seal and open batches concurrently (two pipes, two threads)",
+                      "chunk_MiB": c["chunk_MiB"], "depth": c["depth"], "verified": bool(ok),
+                      "wall_ms": round(mw * 1e3, 3),
+                      "each_direction_gbps": round(n * P * 8 / mw / 1e9, 1),
+                      "both_directions_gbps": round(2 * n * P * 8 / mw / 1e9, 1)}), flush=True)
+    pa.close(); pb.close()
     # zero-copy: the strided kernels address the pinned host buffers directly
     # (torch pin_memory = mapped hipHostMalloc memory), reads and writes share PCIe
     ts, to = [], []
