@@ -391,6 +391,9 @@ def run(args, factory=None, device_fn=None, device_count=None):
 
     seal_ms = [e[0].elapsed_time(e[1]) for e in events]
     open_ms = [e[1].elapsed_time(e[2]) for e in events]
+    if os.environ.get("BENCH_STEP_TRACE"):  # diagnostics: per-step kernel times on stderr
+        print(json.dumps({"seal_ms": [round(x, 4) for x in seal_ms],
+                          "open_ms": [round(x, 4) for x in open_ms]}), file=sys.stderr, flush=True)
 
     # correctness of what was timed: statuses + round-trip identity (whole batch)
     # + a sample of sealed datagrams byte for byte against OpenSSL EVP
