@@ -44,6 +44,8 @@ def parse(argv=None):
     ap.add_argument("--peers", type=int, default=4096, help="config 4")
     ap.add_argument("--per-peer", type=int, default=4096, help="config 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-slot-padding", action="store_true",
+                    help="config 2: leave the slot bytes past each output untouched")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = one per physical core of this job's CPU share "
                          "(min of affinity, physical cores, OMP_NUM_THREADS)")
@@ -76,6 +78,10 @@ class StridedWorkload:
         self.S = S
         self.ctx = neptun_amd.GpuContext(dev.index, key_slots=1)
         self.ctx.set_keys(0, synth.keys(1), np.array([synth.RECEIVER_IDX], np.uint32))
+        # the slots' padding past each output is scratch here (as in NepTUN's
+        # MAX_PKT_SIZE buffers): outputs are zero-filled to their 128-byte line end
+        self.pad = not args.no_slot_padding
+        self.ctx.set_slot_padding(self.pad)
         # shard: rank r owns packets [r*n, (r+1)*n) of the global batch; counters follow
         self.counter_base = rank * n
         # NepTUN slot layout (WG_HEADER_OFFSET = 16, device/mod.rs:76): plaintext 16
@@ -130,7 +136,9 @@ class StridedWorkload:
         return {"workload": f"BASELINE config {'2' if world == 1 else '5'}: {self.n} x {self.P} B "
                             "packets per GPU, single session, seal then open, device-resident",
                 "packets_per_gpu": self.n, "packet_bytes": self.P, "slot_stride": self.S,
-                "global_packets": world * self.n, "parallelism": f"{world} shard(s), no collective"}
+                "global_packets": world * self.n, "parallelism": f"{world} shard(s), no collective",
+                "slot_padding": ("writable: outputs zero-filled to their 128-byte line end "
+                                 "(wg_gpu_ctx_set_slot_padding)") if self.pad else "untouched"}
 
     def close(self):
         self.ctx.close()

@@ -185,6 +185,18 @@ int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
                         uint64_t dst_stride, int32_t *status, void *stream);
 
 /*
+ * Slot padding (strided calls; new, no reference counterpart).  Default 0: no
+ * byte outside a packet's output is written.  With writable != 0 the caller
+ * declares the rest of every output slot scratch: when the output slots start
+ * on 128-byte boundaries (seal: dst; open: the 128-byte run grid's origin) and
+ * the stride is a multiple of 128, the kernels zero-fill each output from its
+ * end to the next 128-byte boundary -- never past the slot -- so every HBM line
+ * they write is written whole (no partial-line merge for the last line).
+ * Results are otherwise identical.  Applies to later calls on the context.
+ */
+int wg_gpu_ctx_set_slot_padding(wg_gpu_ctx *ctx, int writable);
+
+/*
  * Handshake-side crypto, batched.  Device pointers,
  * asynchronous on `stream`.
  *   wg_gpu_x25519_batch: out[i] = X25519(scalars[i], points[i]) (RFC 7748;

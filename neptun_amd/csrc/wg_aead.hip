@@ -311,6 +311,7 @@ struct UniformGeomT {
   uint64_t in0, out0, in_stride, out_stride;  // grid origins of packet 0, slot strides
   uint64_t dead;   // wave mask of packets dropped at the header check (open)
   uint32_t W, nr;  // datagram length and rounds, same for every packet
+  uint32_t pad;    // slot padding: zero-fill each output to its 128-byte line end
   __device__ bool live(uint32_t p, uint32_t r) const { return r < nr && !((dead >> p) & 1u); }
   __device__ uint32_t wlen(uint32_t) const { return W; }
   __device__ uint64_t in_base(uint32_t p) const { return in0 + (uint64_t)p * in_stride; }
@@ -481,7 +482,8 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
   using R = Ranges<kSeal, kText>;
   const uint32_t stride = (uint32_t)g.out_stride;
   const uint32_t hi = R::out_hi(g.W);
-  const uint32_t records = 63u * stride + ((hi + 15u) & ~15u);  // (see stage_in)
+  // (see stage_in; with slot padding the last packet's line end)
+  const uint32_t records = 63u * stride + (g.pad ? ((hi + 127u) & ~127u) : ((hi + 15u) & ~15u));
   const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out0, records);
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   // open's drop mask, opaque to the optimiser: otherwise it hoists 8 per-lane
@@ -513,9 +515,17 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
     const uint32_t w = kRun * r + 16u * k;
     const bool gone = !kSeal && ((((uint32_t)(dead >> (8u * j))) >> y) & 1u);
     const bool ok = !gone && w >= R::out_lo() && w < hi;
-    const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
-    store16(vv, g.out0, records, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
-            8u * j * stride + kRun * r);
+    if (g.pad) {  // (wave-uniform) the partial chunk and the rest of its line, zero-filled
+      const int valid = ok ? (int)min(hi - w, 16u) : 0;
+      const bool mine = ok || (!gone && w >= hi && w < ((hi + 127u) & ~127u));
+      const u32x4 vv = {v[j].x & byte_mask(valid, 0), v[j].y & byte_mask(valid, 1),
+                        v[j].z & byte_mask(valid, 2), v[j].w & byte_mask(valid, 3)};
+      store16(vv, g.out0, records, mine ? y * stride + 16u * k : kNoAccess, 8u * j * stride + kRun * r);
+    } else {
+      const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
+      store16(vv, g.out0, records, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
+              8u * j * stride + kRun * r);
+    }
   }
   // The packets' last, partial chunk: q = hi % 16 bytes at wire offset wp, the
   // same for every packet of the wave (uniform length).  Its owner lane stores
@@ -523,7 +533,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
   // stores for the whole wave (wave-uniform branches, so the compiler's vmcnt
   // bookkeeping stays exact), instead of the cooperative shape's 5 per piece.
   const uint32_t q = hi & 15u, wp = hi & ~15u;
-  if (q && (wp >> 7) == r && wp >= R::out_lo()) {
+  if (!g.pad && q && (wp >> 7) == r && wp >= R::out_lo()) {
     const bool gone = !kSeal && ((dead >> lane) & 1ull);
     const uint4 c = run[8u * lane + (((wp >> 4) & 7u) ^ swz(lane))];
     const uint32_t base = gone ? kNoAccess : lane * stride + wp;
@@ -1046,7 +1056,8 @@ __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams 
     const uint32_t W = kSeal ? prm.len + WG_DATA_OVERHEAD_SZ : prm.len;
     UniformGeomT<kText> g{in0, out0, prm.src_stride, prm.dst_stride, 0ull, W,
                           (kSeal || prm.len >= WG_DATA_OVERHEAD_SZ)
-                              ? (W - (kText ? 16u : 0u) + kRun - 1) / kRun : 0u};
+                              ? (W - (kText ? 16u : 0u) + kRun - 1) / kRun : 0u,
+                          prm.pad_tail};
     run_wave<kSeal, true, WG_SYNC != 0>(stage, g, lane, job, prm.keys, prm.key_index, st, sk);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end

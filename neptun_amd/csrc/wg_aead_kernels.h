@@ -41,6 +41,7 @@ struct StridedParams {
   uint64_t src_stride, dst_stride;
   uint64_t counter_base;      // seal only
   uint32_t n, len, key_slot;
+  uint32_t pad_tail;          // 1: zero-fill each output to its 128-byte line end (slot padding)
 };
 
 struct DescParams {

@@ -26,6 +26,7 @@ struct wg_gpu_ctx {
   uint2 *d_route = nullptr;        // receiver_idx -> key slot (wg_route.hip), 2^route_bits
   uint32_t route_bits = 0;
   uint32_t cus = 0;                // compute units (persistent strided grid)
+  bool pad_slots = false;          // wg_gpu_ctx_set_slot_padding
   struct Range {
     uint64_t host, bytes, dev;
   };
@@ -257,7 +258,21 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
   if (n == 0) return WG_RC_OK;
   DeviceGuard g(ctx->device);
   wg::StridedParams prm{ctx->d_keys, ctx->d_key_index, src, dst, status, src_stride,
-                        dst_stride, counter_base, n, len, key_slot};
+                        dst_stride, counter_base, n, len, key_slot, 0u};
+  // open into plaintext slots that start on 128-byte boundaries: the text
+  // run grid keeps every output line whole (wg_aead.hip Ranges)
+  const bool text_grid = !seal && ((uintptr_t)dst % 128u) == 0 && dst_stride % 128u == 0;
+  if (ctx->pad_slots) {
+    // zero-fill to the line end only where the output runs sit on whole lines
+    // and that line end stays inside the slot (the uniform kernels' grid origin:
+    // seal and the text grid at dst, open's wire grid 16 bytes before it)
+    const uint64_t origin = seal || text_grid ? (uintptr_t)dst : (uintptr_t)dst - 16u;
+    const uint64_t out_hi = seal ? (uint64_t)len + WG_DATA_OVERHEAD_SZ
+                                 : (text_grid ? out_len : out_len + 16u);
+    const uint64_t line_end = (out_hi + 127u) & ~127ull;
+    prm.pad_tail = origin % 128u == 0 && dst_stride % 128u == 0 && line_end <= dst_stride &&
+                   (seal || len >= WG_DATA_OVERHEAD_SZ);
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint32_t full_waves = n / 64u, waves_per_block = wg::kStridedThreads / 64u;
   if (full_waves) {
@@ -265,9 +280,6 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     // workgroup-sized packet groups (wg_aead.hip aead_strided_kernel)
     const uint32_t groups = (full_waves + waves_per_block - 1) / waves_per_block;
     const dim3 grid(std::min(groups, ctx->cus * wg::kStridedBlocksPerCU));
-    // open into plaintext slots that start on 128-byte boundaries: the text
-    // run grid keeps every output line whole (wg_aead.hip Ranges)
-    const bool text_grid = !seal && ((uintptr_t)dst % 128u) == 0 && dst_stride % 128u == 0;
     if (seal)
       hipLaunchKernelGGL((wg::aead_strided_kernel<true, false>), grid, dim3(wg::kStridedThreads),
                          0, s, prm);
@@ -302,6 +314,12 @@ int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
                         uint64_t dst_stride, int32_t *status, void *stream) {
   return launch_strided(ctx, false, n, len, key_slot, 0, src, src_stride, dst, dst_stride, status,
                         stream);
+}
+
+int wg_gpu_ctx_set_slot_padding(wg_gpu_ctx *ctx, int writable) {
+  if (!ctx) return fail(WG_RC_INVALID_ARGUMENT, "set_slot_padding: null context");
+  ctx->pad_slots = writable != 0;
+  return WG_RC_OK;
 }
 
 int wg_gpu_register_host(wg_gpu_ctx *ctx, void *base, uint64_t bytes) {

@@ -213,6 +213,12 @@ class GpuContext:
               "wg_gpu_open_batch_ordered")
 
     # --- uniform single-session batches -------------------------------------
+    def set_slot_padding(self, writable: bool) -> None:
+        """Declare the rest of every strided output slot scratch: outputs are then
+        zero-filled to their 128-byte line end (whole-line writes)."""
+        check(self._lib.wg_gpu_ctx_set_slot_padding(self._h, 1 if writable else 0),
+              "wg_gpu_ctx_set_slot_padding")
+
     def seal_strided(self, n: int, length: int, key_slot: int, counter_base: int, src,
                      src_stride: int, dst, dst_stride: int, status=None, stream=None) -> None:
         check(self._lib.wg_gpu_seal_strided(self._h, n, length, key_slot, counter_base, _ptr(src),

@@ -695,3 +695,61 @@ def test_persistent_grid_partial_group_dropped_lanes(torch_cuda, gpu):
             continue
         want_w = o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, base + int(r), prow[:P].tobytes())
         assert wrow[:P + 32].tobytes() == want_w
+
+
+@pytest.mark.parametrize("P,out_off,src_stride,dst_stride", [
+    (1350, 16, 1408, 1408), (1350, 0, 1408, 1408), (1290, 16, 1408, 1408), (64, 16, 128, 128),
+    (0, 16, 128, 128), (127, 0, 256, 256), (1392, 16, 1536, 1408), (1400, 16, 1536, 1408)])
+def test_strided_slot_padding(torch_cuda, gpu, P, out_off, src_stride, dst_stride):
+    """wg_gpu_ctx_set_slot_padding: outputs are unchanged; from each output's end to the
+    next 128-byte boundary of its slot the bytes are zero (uniform waves; the one-wave
+    tail launch does not pad); nothing past that boundary or before the output is
+    written; no padding where the boundary would leave the slot (1400 / 1408)."""
+    torch = torch_cuda
+    n = 130
+    keys = synth.keys(1, seed=P + 7)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    rng = np.random.default_rng(P + 1)
+    S = src_stride
+    src = rng.integers(0, 256, n * S, dtype=np.uint8)
+    pt = to_dev(torch, src)
+    wire = torch.full((n * S,), 0xAB, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.set_slot_padding(True)
+    try:
+        gpu.seal_strided(n, P, 0, 3, pt.data_ptr() + 16, S, wire, S, st)
+        torch.cuda.synchronize()
+        assert (st == 0).all()
+        descs = np.zeros(n, DESC)
+        descs["src_off"] = np.arange(n) * S + 16
+        descs["dst_off"] = np.arange(n) * S
+        descs["counter"] = 3 + np.arange(n, dtype=np.uint64)
+        descs["len"] = P
+        want = np.full(n * S, 0xAB, np.uint8)
+        assert (o.seal_batch(descs, keys, np.array([synth.RECEIVER_IDX], np.uint32), src, want) == 0).all()
+        want = want.reshape(n, S)
+        W = P + 32
+        end = -(-W // 128) * 128
+        if end <= S:
+            want[:n & ~63, W:end] = 0  # seal's slot = [dst, dst + stride)
+        assert np.array_equal(wire.cpu().numpy().reshape(n, S), want)
+        D = dst_stride
+        back = torch.full((n * D + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+        st.fill_(-1)
+        gpu.open_strided(n, W, 0, wire, S, back.data_ptr() + out_off, D, st)
+        torch.cuda.synchronize()
+        assert (st == 0).all()
+        got = back.cpu().numpy()
+        exp = np.full(n * D + 64, 0xCD, np.uint8)  # (outputs may straddle D-rows: flat)
+        # the run grid's origin: dst (text grid, slot-aligned plaintext) or dst - 16
+        origin = out_off if out_off % 128 == 0 else out_off - 16
+        end = origin + -(-(out_off - origin + P) // 128) * 128
+        pad = origin % 128 == 0 and D % 128 == 0 and end - origin <= D
+        rows = src.reshape(n, S)
+        for i in range(n):
+            exp[i * D + out_off:i * D + out_off + P] = rows[i, 16:16 + P]
+            if pad and i < (n & ~63):
+                exp[i * D + out_off + P:i * D + end] = 0
+        assert np.array_equal(got, exp)
+    finally:
+        gpu.set_slot_padding(False)

@@ -24,6 +24,8 @@ def bind(path):
     L.wg_gpu_seal_strided.argtypes = [vp, u32, u32, u32, u64, vp, u64, vp, u64, vp, vp]
     L.wg_gpu_open_strided.argtypes = [vp, u32, u32, u32, vp, u64, vp, u64, vp, vp]
     L.wg_gpu_last_error.restype = c.c_char_p
+    if hasattr(L, "wg_gpu_ctx_set_slot_padding"):
+        L.wg_gpu_ctx_set_slot_padding.argtypes = [vp, c.c_int]
     for fn in (L.wg_gpu_seal_batch, L.wg_gpu_open_batch):
         fn.argtypes = [vp, vp, u32, vp, vp, vp, vp]
     for fn in (L.wg_gpu_seal_batch_ordered, L.wg_gpu_open_batch_ordered):
@@ -132,6 +134,8 @@ def main():
         h = ctypes.c_void_p()
         assert L.wg_gpu_ctx_create(0, 1, ctypes.byref(h)) == 0, L.wg_gpu_last_error()
         assert L.wg_gpu_set_keys(h, 0, 1, key.ctypes.data, idx.ctypes.data, stream) == 0
+        if os.environ.get("AB_PAD"):  # slot padding (wg_gpu_ctx_set_slot_padding)
+            assert L.wg_gpu_ctx_set_slot_padding(h, int(os.environ["AB_PAD"])) == 0
         libs.append((os.path.basename(p), L, h))
 
     def seal(L, h):
