@@ -190,8 +190,9 @@ int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
  * declares the rest of every output slot scratch: when the output slots start
  * on 128-byte boundaries (seal: dst; open: the 128-byte run grid's origin) and
  * the stride is a multiple of 128, the kernels zero-fill each output from its
- * end to the next 128-byte boundary -- never past the slot -- so every HBM line
- * they write is written whole (no partial-line merge for the last line).
+ * end to the next 128-byte boundary -- never past the slot -- and an open whose
+ * plaintext sits 16 bytes into its slot also zero-fills those 16 bytes, so every
+ * HBM line they write is written whole (no partial-line merge).
  * Results are otherwise identical.  Applies to later calls on the context.
  */
 int wg_gpu_ctx_set_slot_padding(wg_gpu_ctx *ctx, int writable);

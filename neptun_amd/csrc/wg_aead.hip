@@ -517,7 +517,9 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
     const bool ok = !gone && w >= R::out_lo() && w < hi;
     if (g.pad) {  // (wave-uniform) the partial chunk and the rest of its line, zero-filled
       const int valid = ok ? (int)min(hi - w, 16u) : 0;
-      const bool mine = ok || (!gone && w >= hi && w < ((hi + 127u) & ~127u));
+      // (open on the wire grid: also the 16 slot bytes before the plaintext, so
+      // the first line is written whole too)
+      const bool mine = ok || (!gone && ((w >= hi && w < ((hi + 127u) & ~127u)) || w < R::out_lo()));
       const u32x4 vv = {v[j].x & byte_mask(valid, 0), v[j].y & byte_mask(valid, 1),
                         v[j].z & byte_mask(valid, 2), v[j].w & byte_mask(valid, 3)};
       store16(vv, g.out0, records, mine ? y * stride + 16u * k : kNoAccess, 8u * j * stride + kRun * r);

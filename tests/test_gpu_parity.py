@@ -702,9 +702,10 @@ def test_persistent_grid_partial_group_dropped_lanes(torch_cuda, gpu):
     (0, 16, 128, 128), (127, 0, 256, 256), (1392, 16, 1536, 1408), (1400, 16, 1536, 1408)])
 def test_strided_slot_padding(torch_cuda, gpu, P, out_off, src_stride, dst_stride):
     """wg_gpu_ctx_set_slot_padding: outputs are unchanged; from each output's end to the
-    next 128-byte boundary of its slot the bytes are zero (uniform waves; the one-wave
-    tail launch does not pad); nothing past that boundary or before the output is
-    written; no padding where the boundary would leave the slot (1400 / 1408)."""
+    next 128-byte boundary of its slot the bytes are zero, and for open on the wire grid
+    the 16 slot bytes before the plaintext (uniform waves; the one-wave tail launch does
+    not pad); nothing else is written; no padding where the boundary would leave the
+    slot (1400 / 1408)."""
     torch = torch_cuda
     n = 130
     keys = synth.keys(1, seed=P + 7)
@@ -750,6 +751,7 @@ def test_strided_slot_padding(torch_cuda, gpu, P, out_off, src_stride, dst_strid
             exp[i * D + out_off:i * D + out_off + P] = rows[i, 16:16 + P]
             if pad and i < (n & ~63):
                 exp[i * D + out_off + P:i * D + end] = 0
+                exp[i * D + origin:i * D + out_off] = 0  # (wire grid: the slot's 16 head bytes)
         assert np.array_equal(got, exp)
     finally:
         gpu.set_slot_padding(False)
