@@ -417,6 +417,41 @@ def test_per_peer_keys_match_oracle(torch_cuda, gpu):
     assert b.round_trip_equal()
 
 
+def test_config4_full_size_per_peer(torch_cuda, gpu):
+    """BASELINE config 4 at full size: 4096 peers x 4096 packets (16.8M x 1350 B, keys
+    per lane from the 4096-slot table): statuses, round trip, every peer's counters
+    exactly 0..4095 in its headers, sampled oracle parity -- all checks on the device
+    except the samples (the buffers are 22.6 GB each)."""
+    torch = torch_cuda
+    from tools import workloads
+    peers = per = 4096
+    b = workloads.config4(peers, per, 1350, "cuda", seed=17)
+    keys = synth.keys(peers, seed=5)
+    kidx = (np.arange(peers, dtype=np.uint32) * 2246822519).astype(np.uint32)
+    gpu.set_keys(0, keys, kidx)
+    gpu.seal_batch(b.d_seal, b.n, b.pt, b.wire, b.st_seal)
+    gpu.open_batch(b.d_open, b.n, b.wire, b.out, b.st_open)
+    torch.cuda.synchronize()
+    assert int((b.st_seal != 0).sum()) == 0 and int((b.st_open != 0).sum()) == 0
+    assert b.round_trip_equal(chunk=1 << 16)
+    # header counters: (peer, counter) pairs are exactly peers x 0..per-1
+    offs = torch.from_numpy(b.offs).cuda()
+    ctr = torch.zeros(b.n, dtype=torch.int64, device="cuda")
+    for j in range(8):
+        ctr |= b.wire[offs + 8 + j].to(torch.int64) << (8 * j)
+    peer = torch.from_numpy(b.seal_host["key_slot"].astype(np.int64)).cuda()
+    key = torch.sort(peer * per + ctr).values
+    assert torch.equal(key, torch.arange(b.n, dtype=torch.int64, device="cuda"))
+    del key, ctr, offs, peer
+    for i in range(0, b.n, 65521):
+        off, p = int(b.offs[i]), 1350
+        d = b.seal_host[i]
+        sl = int(d["key_slot"])
+        pt = b.pt[off + 16:off + 16 + p].cpu().numpy().tobytes()
+        got = b.wire[off:off + p + 32].cpu().numpy().tobytes()
+        assert got == o.format_packet_data(keys[sl].tobytes(), int(kidx[sl]), int(d["counter"]), pt)
+
+
 def test_config3_full_size_round_trip(torch_cuda, gpu):
     """BASELINE config 3 at full size (1.31M packets): statuses, round trip, sampled oracle."""
     torch = torch_cuda
