@@ -18,6 +18,10 @@
 //      is read out (128 KiB per workgroup, 1 workgroup = 8 waves per CU)
 //   H  half rounds (64 B per packet, 4 KiB pieces), two 4 KiB stages per wave:
 //      the next half's DMA goes out before this half is read (2 workgroups/CU)
+// Loop-granularity variants (flat copy of the same byte count, register loads):
+//   LK persistent waves (WPC waves per CU), grid-stride over K-KiB chunks: K loads
+//      then K stores per lane per iteration -- does a persistent loop with small K
+//      reach the one-shot float4 copy's rate?
 //   microbench_mem4 -> one line per variant
 // Build: hipcc --offload-arch=gfx950 -O3 tools/microbench_mem4.hip -o tools/microbench_mem4
 #include <hip/hip_runtime.h>
@@ -131,6 +135,21 @@ __global__ __launch_bounds__(512) void kern_pipe(const uint8_t *__restrict__ src
                     dst, (blockIdx.x * kWaves + wave) * 64u, lane);
 }
 
+template <int K>
+__global__ __launch_bounds__(256) void copy_loop(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                uint64_t chunks) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6), waves = (uint64_t)gridDim.x * 4u;
+  for (uint64_t c = wave; c < chunks; c += waves) {
+    const uint64_t base = c * 1024u * K;
+    uint4 v[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = *(const uint4 *)(src + base + j * 1024u + lane * 16u);
+#pragma unroll
+    for (int j = 0; j < K; ++j) *(uint4 *)(dst + base + j * 1024u + lane * 16u) = v[j];
+  }
+}
+
 template <char L, char S, char P>
 __global__ __launch_bounds__(512) void kern(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                             uint32_t n) {
@@ -191,6 +210,17 @@ int main() {
     V(B, B, W, pers);
     run("D  two 8 KiB stages, prefetch 1 round", [&] { hipLaunchKernelGGL(kern_pipe<0>, one, blk, 0, 0, src, dst, n); });
     run("H  two 4 KiB half-round stages", [&] { hipLaunchKernelGGL(kern_pipe<1>, one, blk, 0, 0, src, dst, n); });
+  }
+  const uint64_t tot = (uint64_t)n * kRuns * 128u;  // same byte count, flat
+  for (int wpc : {16, 32}) {
+    const dim3 g((uint32_t)(cus * wpc / 4));
+    char name[64];
+    snprintf(name, sizeof name, "LK K=1 %d waves/CU", wpc);
+    run(name, [&] { hipLaunchKernelGGL(copy_loop<1>, g, dim3(256), 0, 0, src, dst, tot / 1024); });
+    snprintf(name, sizeof name, "LK K=2 %d waves/CU", wpc);
+    run(name, [&] { hipLaunchKernelGGL(copy_loop<2>, g, dim3(256), 0, 0, src, dst, tot / 2048); });
+    snprintf(name, sizeof name, "LK K=8 %d waves/CU", wpc);
+    run(name, [&] { hipLaunchKernelGGL(copy_loop<8>, g, dim3(256), 0, 0, src, dst, tot / 8192); });
   }
   return 0;
 }
