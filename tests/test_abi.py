@@ -89,3 +89,5 @@ def test_invalid_arguments_rejected_without_launch():
     assert lib.wg_gpu_ctx_create(0, 0, ctypes.byref(ctypes.c_void_p())) == -1
     assert lib.wg_gpu_seal_batch(None, None, 1, None, None, None, None) == -1
     assert b"null" in lib.wg_gpu_last_error()
+    assert lib.wg_gpu_ctx_set_slot_padding(None, 1) == -1
+    assert b"null context" in lib.wg_gpu_last_error()
