@@ -101,6 +101,9 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #ifndef WG_SYNC_KEY_BLOCK
 #define WG_SYNC_KEY_BLOCK 1  // phase-locked Poly1305 key block on the sync paths
 #endif
+#ifndef WG_SYNC_OPEN_KEY
+#define WG_SYNC_OPEN_KEY 1  // open (uniform batches): phase-locked key block once the headers landed
+#endif
 
 // Diagnostic build only (-DWG_STAMP=1): s_memtime at the phase boundaries of
 // the phase-locked loop, wave 0 of every workgroup, read back with
@@ -811,12 +814,14 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 
   auto one_time_key = [&]() {
     uint32_t ks[16];
+    constexpr bool kSyncOpenKey = kSync && kUniform && !kSeal && WG_SYNC_OPEN_KEY;
     // RFC 8439 2.6: block 0 -> r | s.  Phase-locked for seal on the sync
     // paths, where every wave calls this once per group right after issuing
     // round 0's DMA (wave-uniform call site).  Open computes it per lane as
     // soon as the lane's header has landed: locking it there made every wave
     // wait for the slowest header (-4 %).
-    if constexpr (kSync && kSeal && WG_SYNC_KEY_BLOCK) chacha20_block_sync(ks, key, 0u, n1, n2);
+    if constexpr ((kSync && kSeal && WG_SYNC_KEY_BLOCK) || kSyncOpenKey)
+      chacha20_block_sync(ks, key, 0u, n1, n2);
     else chacha20_block(ks, key, 0u, n1, n2);
     poly_init(poly, ks);
     S.park[lane] = make_uint4(ks[4], ks[5], ks[6], ks[7]);  // s, read back for the tag
@@ -830,7 +835,14 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       if (h.x != WG_MSG_DATA) job.status = WG_STATUS_INVALID_PACKET;
       else if (h.y != sidx) job.status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
     }
-    if (job.status != WG_STATUS_OK) {
+    if constexpr (kSync && kUniform && WG_SYNC_OPEN_KEY) {
+      // every lane of every wave runs the phase-locked block (dropped lanes on
+      // garbage; their results are never used)
+      n1 = h.z;
+      n2 = h.w;
+      one_time_key();
+      if (job.status != WG_STATUS_OK) my_runs = 0;
+    } else if (job.status != WG_STATUS_OK) {
       my_runs = 0;  // nothing of this packet is stored
       if constexpr (kSync && !kUniform) g.kill(lane);
       else if constexpr (!kUniform) S.nruns[lane] = 0;
