@@ -790,3 +790,47 @@ def test_strided_slot_padding(torch_cuda, gpu, P, out_off, src_stride, dst_strid
         assert np.array_equal(got, exp)
     finally:
         gpu.set_slot_padding(False)
+
+
+def test_one_context_from_two_threads(torch_cuda, gpu):
+    """include/neptun_gpu.h: a context may be used from several host threads.  Two
+    threads seal and open their own strided batches on their own streams, with
+    different key slots, concurrently; both match the oracle."""
+    import threading
+    torch = torch_cuda
+    keys = synth.keys(2, seed=77)
+    idx = np.array([0x1234, 0x5678], np.uint32)
+    gpu.set_keys(0, keys, idx)
+    n, P, S = 4096 + 17, 1350, 1408
+    results, errors = {}, []
+
+    def worker(t):
+        try:
+            stream = torch.cuda.Stream()
+            pt = synth.device_payloads(n, P, S, "cuda", seed=100 + t)
+            wire = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+            back = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+            st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            for _ in range(20):
+                gpu.seal_strided(n, P, t, 1000 * t, pt.data_ptr() + 16, S, wire, S, st, stream=stream)
+                gpu.open_strided(n, P + 32, t, wire, S, back.data_ptr() + 16, S, st, stream=stream)
+            stream.synchronize()
+            results[t] = (pt, wire, back, st)
+        except Exception as e:  # reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in (0, 1)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for t in (0, 1):
+        pt, wire, back, st = results[t]
+        assert int((st != 0).sum()) == 0
+        assert torch.equal(back.view(n, S)[:, 16:16 + P], pt.view(n, S)[:, 16:16 + P])
+        for i in (0, 1, 63, 64, 2049, n - 1):
+            row = pt.view(n, S)[i, 16:16 + P].cpu().numpy().tobytes()
+            want = o.format_packet_data(keys[t].tobytes(), int(idx[t]), 1000 * t + i, row)
+            assert wire.view(n, S)[i, :P + 32].cpu().numpy().tobytes() == want
