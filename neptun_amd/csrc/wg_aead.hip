@@ -70,6 +70,14 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
 #endif
 
+#ifndef WG_FULL_LINES
+#define WG_FULL_LINES 1  // uniform kernels: edge rounds moved as whole lines where the host allows it
+#endif
+
+#ifndef WG_HDR_DMA
+#define WG_HDR_DMA 1  // uniform open: headers by LDS-DMA ahead of round 0, counted vmcnt(8) wait
+#endif
+
 #ifndef WG_ABLATE_ZEROING
 #define WG_ABLATE_ZEROING 0  // timing-only: forged packets keep their plaintext
 #endif
@@ -315,6 +323,7 @@ struct UniformGeomT {
   uint64_t dead;   // wave mask of packets dropped at the header check (open)
   uint32_t W, nr;  // datagram length and rounds, same for every packet
   uint32_t pad;    // slot padding: zero-fill each output to its 128-byte line end
+  uint32_t full_in;  // input runs on whole 128-byte lines: every round loads whole lines
   __device__ bool live(uint32_t p, uint32_t r) const { return r < nr && !((dead >> p) & 1u); }
   __device__ uint32_t wlen(uint32_t) const { return W; }
   __device__ uint64_t in_base(uint32_t p) const { return in0 + (uint64_t)p * in_stride; }
@@ -454,11 +463,22 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &
   // num_records (the tail chunk reads up to 15 bytes past the packet -- inside
   // the same 16-byte-aligned, so mapped, granule).  launch_strided bounds
   // 63 * stride + hi below kNoAccess.
-  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 63u * stride + ((hi + 15u) & ~15u));
+  // With full_in (input grid lines 128-byte aligned) the edge rounds load
+  // whole lines as well: a line holding any byte of the packet is mapped, and
+  // the bytes around the packet never reach an output (header chunk replaced,
+  // tail chunk masked, chunks past the end not processed and zeroed or not
+  // stored).  The resource then ends at the last packet's line end.
+  const bool full = WG_FULL_LINES && g.full_in;
+  const uint32_t rec_hi = full ? ((hi + 127u) & ~127u) : ((hi + 15u) & ~15u);
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in0, 63u * stride + rec_hi);
   const uint32_t y = lane >> 3, k0 = (lane & 7u) ^ swz(y), k1 = k0 ^ 4u;
   // (open: packets dropped at the header check are loaded like the others --
   // harmless, their lanes skip the crypto and stage_out never writes them back)
-  if (WG_ABLATE_ALL_INTERIOR || (kRun * r >= R::in_lo() && kRun * r + kRun <= hi)) {
+  // (a round past the input -- open / seal grids end apart -- loads nothing;
+  // r > 0 keeps round 0 straight-line: exactly 8 loads on every path, which
+  // open's header wait counts on)
+  if (full && r > 0u && kRun * r >= hi) return;
+  if (WG_ABLATE_ALL_INTERIOR || full || (kRun * r >= R::in_lo() && kRun * r + kRun <= hi)) {
     // interior round (wave-uniform test): every lane moves a full chunk, the
     // per-lane offsets are round-independent -- no range checks
     const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
@@ -494,7 +514,12 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
   // drain the DMA in flight
   uint64_t dead = kSeal ? 0ull : g.dead;
   if constexpr (!kSeal) asm volatile("" : "+s"(dead));
-  if (WG_ABLATE_ALL_INTERIOR || (kRun * r >= R::out_lo() && kRun * r + kRun <= hi && dead == 0)) {
+  // slot padding with no packet dropped: every output line is written whole,
+  // edge rounds included -- run_wave zeroed the stage chunks outside the
+  // output (zero_outside) -- and rounds past the output's line end store nothing
+  const bool full = WG_FULL_LINES && g.pad && dead == 0;
+  if (full && kRun * r >= hi) return;
+  if (WG_ABLATE_ALL_INTERIOR || full || (kRun * r >= R::out_lo() && kRun * r + kRun <= hi && dead == 0)) {
     // interior round: 8 full-chunk stores at round-independent per-lane offsets
     // (all 8 LDS reads first: the asm stores are memory barriers to the
     // compiler, which otherwise serialises read -> wait -> store per piece)
@@ -915,6 +940,32 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     }
   };
 
+  // Slot padding (uniform batches): stage_out writes whole output lines, so the
+  // stage chunks of the round that lie outside the output are zeroed here --
+  // those wholly past its end (input bytes, or bytes loaded past the packet),
+  // and on open's wire grid the 16 slot bytes before the plaintext (the
+  // header).  The partial chunks are zero past the end already (crypt_chunk,
+  // tail_words).  Wave-uniform: at most the last output round and round 0.
+  auto zero_outside = [&](uint4 *run, uint32_t ln, uint32_t r) {
+    if constexpr (kUniform) {
+      using R = Ranges<kSeal, kText>;
+      const uint32_t zlo = (R::out_hi(g.W) + 15u) & ~15u;  // first chunk wholly past the output
+      // (addresses from an opaque copy of the lane: computed here, in the
+      // rounds that zero, rather than hoisted and held in VGPRs)
+      uint32_t lz = ln, zero = 0u;
+      asm volatile("" : "+v"(lz), "+v"(zero));
+      const uint32_t row = 8u * lz, sw = swz(lz);
+      const uint4 z = make_uint4(zero, zero, zero, zero);
+      if ((zlo >> 7) == r) {
+        const uint32_t kz = (zlo >> 4) & 7u;
+#pragma unroll
+        for (uint32_t k = 1; k < kChunks; ++k)
+          if (k >= kz) run[row + (k ^ sw)] = z;
+      }
+      if (R::out_lo() > 0u && r == 0u) run[row + (0u ^ sw)] = z;
+    }
+  };
+
   if constexpr (kSync) {
     // Phase-locked path (workgroup-uniform control flow, one LDS stage per
     // wave): the round's DMA is issued first and its two keystream blocks are
@@ -927,23 +978,59 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     // its registers freed, before the loop body)
     if (rounds) {
       uint4 hdr = make_uint4(0u, 0u, 0u, 0u);
-      // (a global-address-space load: a flat one may alias LDS and makes the
-      // compiler drain the LDS-DMA in flight before it)
-      if (!kSeal && my_runs) {
-        const u32x4 h = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(
-            job.in_base - (16u - kG));  // (the datagram start)
+      if constexpr (!kSeal && kUniform && WG_HDR_DMA && !WG_ABLATE_NO_MEM) {
+        // Uniform open: the 64 headers go to the tag park by one LDS-DMA piece
+        // issued before round 0's 8 pieces, and are read back after an
+        // explicit vmcnt(8) -- header landed, round 0's DMA still in flight
+        // under the key block and round 0's keystream.  (With a register load
+        // the compiler placed the header's use, and its wait, between the
+        // pieces, issuing most of round 0's DMA a memory latency late.)  The
+        // tag park is free until round 0's tag bytes land (open_keep_tail).
+        if (my_runs)
+          dma_global(lds_offset(&S.tagp[0]), reinterpret_cast<const uint8_t *>(job.in_base - (16u - kG)));
+        stage_in<kSeal>(run, g, lane, 0);  // exactly 8 pieces (round 0 is straight-line)
+        u32x4 h;
+        asm volatile("s_waitcnt vmcnt(8)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(h) : "v"(lds_offset(&S.tagp[lane])) : "memory");
         hdr = make_uint4(h.x, h.y, h.z, h.w);
-      }
+      } else {
+        // (a global-address-space load: a flat one may alias LDS and makes the
+        // compiler drain the LDS-DMA in flight before it)
+        if (!kSeal && my_runs) {
+          const u32x4 h = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(
+              job.in_base - (16u - kG));  // (the datagram start)
+          hdr = make_uint4(h.x, h.y, h.z, h.w);
+        }
 #if !WG_ABLATE_NO_MEM
-      stage_in<kSeal>(run, g, lane, 0);
+        stage_in<kSeal>(run, g, lane, 0);
 #endif
+      }
       if (kSeal && !WG_ABLATE_NO_KEYBLOCK) one_time_key();  // while round 0's DMA is in flight (every wave: phase-locked)
       if (!kSeal && my_runs) open_header(hdr);
     }
-    for (uint32_t r = 0; r < rounds; ++r) {
+    // one round of the phase-locked loop
+    auto do_round = [&](uint32_t r) {
+#ifndef WG_OPAQUE_LANE
+#define WG_OPAQUE_LANE 0
+#endif
+      // (WG_OPAQUE_LANE: the lane index and P opaque per round, so that
+      // lane-derived LDS addresses, buffer offsets and the tail chunk's byte
+      // masks are recomputed each round instead of being held in VGPRs through
+      // every round -- fewer VGPRs, +1 % open time; off)
+      uint32_t ln = lane;
+      uint32_t Pr = P;
+#if WG_OPAQUE_LANE
+      asm volatile("" : "+v"(ln));
+      if constexpr (kUniform) {
+        Pr = __builtin_amdgcn_readfirstlane(P);
+        asm volatile("" : "+s"(Pr));
+      } else {
+        asm volatile("" : "+v"(Pr));
+      }
+#endif
       WG_STAMP_AT(kSeal, r, 0);
 #if !WG_ABLATE_NO_MEM
-      if (r > 0) stage_in<kSeal>(run, g, lane, r);
+      if (r > 0) stage_in<kSeal>(run, g, ln, r);
 #endif
       WG_STAMP_AT(kSeal, r, 1);
       auto landed = [&]() {
@@ -951,11 +1038,11 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         WG_STAMP_AT(kSeal, r, 3);
         if (!kSeal && my_runs) open_keep_tail(run, r);
         if (kSeal && r == 0)  // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
-          run[8u * lane + (0u ^ swz(lane))] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
+          run[8u * ln + (0u ^ swz(ln))] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
       };
       // workgroup-uniform: P for uniform batches; every round for descriptor
       // batches (lanes without ciphertext in the round ignore the keystream)
-      if ((!kUniform || (int)(kRun * r) < (int)P) && !WG_ABLATE_NO_CRYPT) {
+      if ((!kUniform || (int)(kRun * r) < (int)Pr) && !WG_ABLATE_NO_CRYPT) {
         // the keystream lives only inside this branch (kept out of phis, the
         // compiler would otherwise carry it as a register tuple and spill it)
         uint32_t ka[16], kb[16];
@@ -963,23 +1050,27 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         WG_STAMP_AT(kSeal, r, 2);
         landed();
         if (my_runs) {
-          apply_chunk0<kSeal, kText>(run, lane, r, P, poly, ks_save);
-          apply_blocks<kSeal, kText>(run, lane, r, P, ka, kb, poly, ks_save);
+          apply_chunk0<kSeal, kText>(run, ln, r, Pr, poly, ks_save);
+          apply_blocks<kSeal, kText>(run, ln, r, Pr, ka, kb, poly, ks_save);
           if (kSeal) seal_tail(run, r);
         }
       } else {
         landed();
         if (my_runs && !WG_ABLATE_NO_CRYPT) {
-          apply_chunk0<kSeal, kText>(run, lane, r, P, poly, ks_save);
+          apply_chunk0<kSeal, kText>(run, ln, r, Pr, poly, ks_save);
           if (kSeal) seal_tail(run, r);
         }
       }
+      if constexpr (kUniform) {
+        if (WG_FULL_LINES && g.pad) zero_outside(run, ln, r);
+      }
       WG_STAMP_AT(kSeal, r, 4);
 #if !WG_ABLATE_NO_MEM
-      stage_out<kSeal>(run, g, lane, r);
+      stage_out<kSeal>(run, g, ln, r);
 #endif
       WG_STAMP_AT(kSeal, r, 5);
-    }
+    };
+    for (uint32_t r = 0; r < rounds; ++r) do_round(r);
   } else {
     uint4 *run = S.run[0];
     for (uint32_t r = 0; r < rounds; ++r) {
@@ -1071,7 +1162,7 @@ __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams 
     UniformGeomT<kText> g{in0, out0, prm.src_stride, prm.dst_stride, 0ull, W,
                           (kSeal || prm.len >= WG_DATA_OVERHEAD_SZ)
                               ? (W - (kText ? 16u : 0u) + kRun - 1) / kRun : 0u,
-                          prm.pad_tail};
+                          prm.pad_tail, prm.full_in};
     run_wave<kSeal, true, WG_SYNC != 0>(stage, g, lane, job, prm.keys, prm.key_index, st, sk);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end

@@ -42,6 +42,7 @@ struct StridedParams {
   uint64_t counter_base;      // seal only
   uint32_t n, len, key_slot;
   uint32_t pad_tail;          // 1: zero-fill each output to its 128-byte line end (slot padding)
+  uint32_t full_in;           // 1: input runs are whole 128-byte lines (launch_strided)
 };
 
 struct DescParams {

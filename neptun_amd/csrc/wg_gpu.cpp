@@ -258,7 +258,7 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
   if (n == 0) return WG_RC_OK;
   DeviceGuard g(ctx->device);
   wg::StridedParams prm{ctx->d_keys, ctx->d_key_index, src, dst, status, src_stride,
-                        dst_stride, counter_base, n, len, key_slot, 0u};
+                        dst_stride, counter_base, n, len, key_slot, 0u, 0u};
   // open into plaintext slots that start on 128-byte boundaries: the text
   // run grid keeps every output line whole (wg_aead.hip Ranges)
   const bool text_grid = !seal && ((uintptr_t)dst % 128u) == 0 && dst_stride % 128u == 0;
@@ -272,6 +272,14 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     const uint64_t line_end = (out_hi + 127u) & ~127ull;
     prm.pad_tail = origin % 128u == 0 && dst_stride % 128u == 0 && line_end <= dst_stride &&
                    (seal || len >= WG_DATA_OVERHEAD_SZ);
+  }
+  // input grid origin on a 128-byte line with whole-line slots: the uniform
+  // kernels load every round as whole lines (wg_aead.hip stage_in; the lines
+  // hold packet bytes, so they are mapped, and what lies around the packet is
+  // never output)
+  {
+    const uint64_t in_origin = seal ? (uintptr_t)src - 16u : text_grid ? (uintptr_t)src + 16u : (uintptr_t)src;
+    prm.full_in = in_origin % 128u == 0 && src_stride % 128u == 0;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint32_t full_waves = n / 64u, waves_per_block = wg::kStridedThreads / 64u;
