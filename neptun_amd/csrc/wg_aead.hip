@@ -74,6 +74,18 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_FULL_LINES 1  // uniform kernels: edge rounds moved as whole lines where the host allows it
 #endif
 
+// The lane index and P opaque to the optimiser once per round (run_wave):
+// lane-derived LDS addresses, buffer offsets and the tail chunk's byte masks are
+// then recomputed each round instead of being computed once per kernel and held
+// in VGPRs through every round.  Descriptor kernels: fewer spills, config 4
+// -1.2 %; uniform kernels: +1 % open, off.
+#ifndef WG_OPAQUE_LANE
+#define WG_OPAQUE_LANE 0
+#endif
+#ifndef WG_OPAQUE_LANE_DESC
+#define WG_OPAQUE_LANE_DESC 1
+#endif
+
 #ifndef WG_HDR_DMA
 #define WG_HDR_DMA 1  // uniform open: headers by LDS-DMA ahead of round 0, counted vmcnt(8) wait
 #endif
@@ -1010,21 +1022,21 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     }
     // one round of the phase-locked loop
     auto do_round = [&](uint32_t r) {
-#ifndef WG_OPAQUE_LANE
-#define WG_OPAQUE_LANE 0
-#endif
-      // (WG_OPAQUE_LANE: the lane index and P opaque per round, so that
-      // lane-derived LDS addresses, buffer offsets and the tail chunk's byte
-      // masks are recomputed each round instead of being held in VGPRs through
-      // every round -- fewer VGPRs, +1 % open time; off)
+      // (WG_OPAQUE_LANE / WG_OPAQUE_LANE_DESC: see the knob)
       uint32_t ln = lane;
       uint32_t Pr = P;
 #if WG_OPAQUE_LANE
-      asm volatile("" : "+v"(ln));
       if constexpr (kUniform) {
+        asm volatile("" : "+v"(ln));
         Pr = __builtin_amdgcn_readfirstlane(P);
         asm volatile("" : "+s"(Pr));
       } else {
+        asm volatile("" : "+v"(ln));
+        asm volatile("" : "+v"(Pr));
+      }
+#elif WG_OPAQUE_LANE_DESC
+      if constexpr (!kUniform) {
+        asm volatile("" : "+v"(ln));
         asm volatile("" : "+v"(Pr));
       }
 #endif
