@@ -861,7 +861,13 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       chacha20_block_sync(ks, key, 0u, n1, n2);
     else chacha20_block(ks, key, 0u, n1, n2);
     poly_init(poly, ks);
-    S.park[lane] = make_uint4(ks[4], ks[5], ks[6], ks[7]);  // s, read back for the tag
+    // s, read back for the tag.  An inline-asm LDS write: the compiler cannot
+    // tell the park from the run buffer that round 0's LDS-DMA (in flight
+    // here) fills, and put a vmcnt(0) before a plain store -- draining the DMA
+    // before round 0's keystream at every group start.  (LDS accesses of one
+    // wave execute in order, so later reads of the park see this write.)
+    const u32x4 sv = {ks[4], ks[5], ks[6], ks[7]};
+    asm volatile("ds_write_b128 %0, %1" :: "v"(lds_offset(&S.park[lane])), "v"(sv) : "memory");
   };
   if (kSeal && !kSync && my_runs) one_time_key();
 
