@@ -65,6 +65,18 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #ifndef WG_ABLATE_NO_KEYBLOCK
 #define WG_ABLATE_NO_KEYBLOCK 0  // seal: skip the per-packet Poly1305 key block
 #endif
+// Wave priority of the memory phase of a phase-locked round (0: unchanged):
+// from the landing wait (WG_MEM_PRIO_AT 0) or from the stores (1) until the
+// next round's keystream steps set their own (WG_CHACHA_PRIO).
+#ifndef WG_MEM_PRIO
+#define WG_MEM_PRIO 0
+#endif
+#ifndef WG_MEM_PRIO_AT
+#define WG_MEM_PRIO_AT 0
+#endif
+#ifndef WG_ABLATE_PURE_COPY
+#define WG_ABLATE_PURE_COPY 0  // uniform kernels: staging loop only (a copy), no setup, no crypto
+#endif
 
 #ifndef WG_WAVES_PER_SIMD
 #define WG_WAVES_PER_SIMD 1  // __launch_bounds__ min waves per SIMD (VGPR cap)
@@ -1052,6 +1064,9 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 #endif
       WG_STAMP_AT(kSeal, r, 1);
       auto landed = [&]() {
+#if WG_MEM_PRIO && !WG_MEM_PRIO_AT
+        __builtin_amdgcn_s_setprio(WG_MEM_PRIO);
+#endif
         lds_wait_dma();
         WG_STAMP_AT(kSeal, r, 3);
         if (!kSeal && my_runs) open_keep_tail(run, r);
@@ -1083,6 +1098,9 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         if (WG_FULL_LINES && g.pad) zero_outside(run, ln, r);
       }
       WG_STAMP_AT(kSeal, r, 4);
+#if WG_MEM_PRIO && WG_MEM_PRIO_AT
+      __builtin_amdgcn_s_setprio(WG_MEM_PRIO);
+#endif
 #if !WG_ABLATE_NO_MEM
       stage_out<kSeal>(run, g, ln, r);
 #endif
@@ -1181,6 +1199,20 @@ __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams 
                           (kSeal || prm.len >= WG_DATA_OVERHEAD_SZ)
                               ? (W - (kText ? 16u : 0u) + kRun - 1) / kRun : 0u,
                           prm.pad_tail, prm.full_in};
+#if WG_ABLATE_PURE_COPY
+    // timing-only probe: the kernel's own staging instructions and nothing else
+    // (DMA in, wait, LDS read-out, stores), to compare with the memory-only
+    // ablation on the same box, buffers and process
+    {
+      uint4 *run = stage.run[0];
+      for (uint32_t r = 0; r < g.nr; ++r) {
+        stage_in<kSeal>(run, g, lane, r);
+        lds_wait_dma();
+        stage_out<kSeal>(run, g, lane, r);
+      }
+      return;
+    }
+#endif
     run_wave<kSeal, true, WG_SYNC != 0>(stage, g, lane, job, prm.keys, prm.key_index, st, sk);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
