@@ -161,13 +161,23 @@ def main():
     # chip is power-capped (tools/power_probe.py): a burst of >= ~0.3 s lets the
     # clock settle to what THIS variant's energy per packet allows.
     burst = int(os.environ.get("AB_BURST", 2))
+    # AB_SEAL_ONLY: bursts of seals only (timing ablations whose open fails and
+    # zero-fills would otherwise set a different power state for the next seal)
+    seal_only = bool(os.environ.get("AB_SEAL_ONLY"))
     times = {name: ([], []) for name, _, _ in libs}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     for _ in range(rounds):
         for name, L, h in libs:
             for _ in range(burst):
-                seal(L, h); open_(L, h)
-            ev[0].record(); seal(L, h); ev[1].record(); open_(L, h); ev[2].record()
+                seal(L, h)
+                if not seal_only:
+                    open_(L, h)
+            ev[0].record(); seal(L, h); ev[1].record()
+            if seal_only:
+                seal(L, h)
+            else:
+                open_(L, h)
+            ev[2].record()
             torch.cuda.synchronize()
             times[name][0].append(ev[0].elapsed_time(ev[1]))
             times[name][1].append(ev[1].elapsed_time(ev[2]))
