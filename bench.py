@@ -49,7 +49,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = one per physical core of this job's CPU share "
                          "(min of affinity, physical cores, OMP_NUM_THREADS)")
-    ap.add_argument("--sustain-seconds", type=float, default=1.5,
+    ap.add_argument("--sustain-seconds", type=float, default=2.0,
                     help="N=1: extra seconds of steps after the timed region, reported apart as "
                          "'sustained' (the power-capped steady state; never the headline value)")
     ap.add_argument("--evp-sample", type=int, default=257,
@@ -251,6 +251,40 @@ def host_cpus() -> dict:
             "logical_cpus": os.cpu_count() or 1, "allowed_cpus": allowed}
 
 
+class PowerSampler:
+    """Socket power / gfx clock / PPT state of GPU 0 (`amd-smi metric`, read-only)
+    sampled on a host thread while the supplementary sustained steps run: the
+    kernels are power-bound, so the line says at what power and
+    clock its sustained rate was reached.  Never fatal: no amd-smi -> an error note."""
+
+    def __init__(self, period: float = 0.05):
+        import threading
+        self.period, self.samples, self.error = period, [], None
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        from tools import power_probe
+        while not self._stop.is_set():
+            s = power_probe.sample()
+            if "err" in s:
+                self.error = str(s["err"])[:120]
+                return
+            self.samples.append({"m": s})
+            self._stop.wait(self.period)
+
+    def start(self):
+        self._thread.start()
+
+    def stop(self) -> dict:
+        from tools import power_probe
+        self._stop.set()
+        self._thread.join(timeout=30)
+        if self.error and not self.samples:
+            return {"error": self.error}
+        return dict(power_probe.summarize(self.samples), source="amd-smi metric during the sustained steps")
+
+
 def cpu_baseline(threads: int, cpus: dict) -> dict:
     """Config 1 on the host cores: oracle/build/cpu_baseline (NepTUN framing over
     OpenSSL EVP, the stand-in for ring's asm; see oracle/cpu_baseline.c), one
@@ -420,7 +454,10 @@ def run(args, factory=None, device_fn=None, device_count=None):
         per = max(elapsed / args.steps, 1e-4)
         k2 = max(1, int(args.sustain_seconds / per))
         ev = [new_event(), new_event()]
+        sampler = PowerSampler() if device_fn is None else None
         sync()
+        if sampler:
+            sampler.start()  # samples while the steps run (idle samples are filtered out)
         ev[0].record(stream)
         for _ in range(k2):
             wl.step(stream)
@@ -432,6 +469,8 @@ def run(args, factory=None, device_fn=None, device_count=None):
                      "ms_per_step": round(ms / k2, 4),
                      "note": "supplementary: steps run after the timed region and its "
                              "verification; not the headline value"}
+        if sampler:
+            sustained["power"] = sampler.stop()
     line = None
     if not ok:
         line = {"error": "verification failed (statuses, round trip or EVP sample)", "rank": rank,
