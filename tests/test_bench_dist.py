@@ -122,3 +122,23 @@ def test_more_ranks_than_gpus_is_refused(tmp_path):
     line = json.loads(res[0]["out"])
     assert "error" in line and line["visible_gpus"] == 1 and line["n_gpus"] == 2
     assert res[1]["out"] == ""
+
+
+def test_power_sampler_never_fails_the_bench(monkeypatch):
+    """bench.PowerSampler reports what amd-smi gives and never raises: here (no GPU)
+    the samples carry no busy GPU, or amd-smi errors out and the note says so."""
+    import bench
+    from tools import power_probe
+    calls = []
+
+    def fake_sample():
+        calls.append(1)
+        return {"err": "amd-smi: no GPU"} if len(calls) > 2 else {"gpu_data": []}
+
+    monkeypatch.setattr(power_probe, "sample", fake_sample)
+    s = bench.PowerSampler(period=0.01)
+    s.start()
+    time.sleep(0.2)
+    out = s.stop()
+    assert out.get("busy_samples") == 0 or "error" in out
+    assert len(calls) == 3  # stops sampling at the first error
