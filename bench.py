@@ -525,6 +525,14 @@ def run(args, factory=None, device_fn=None, device_count=None):
             "evp_sample": evp,
             "sustained": sustained,
         }
+        pw = (sustained or {}).get("power") or {}
+        if "ACTIVE" in pw.get("ppt_violation", []):
+            # what actually holds the kernels below the HBM roofline
+            line["roofline"]["limiter"] = (
+                f"package power: {pw['socket_power_W']} W with the PPT limit active at "
+                f"{pw['gfx_clock_MHz']} MHz during the sustained steps; time per launch = energy "
+                "per launch / power budget, both energy terms (VALU instructions, HBM bytes) at "
+                "their floors")
         if world == 1 and not args.no_cpu_baseline and args.config == 2:
             cpus = host_cpus()
             # one thread per physical core this job may use: the GPU box grants a
