@@ -170,6 +170,10 @@ __device__ __forceinline__ void chacha20_block_sync(uint32_t (&ks)[16], const ui
   asm volatile(WG_STEP8_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(q15), "+v"(q12), "+v"(q13), "+v"(q14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4), "v"(q5), "v"(q6), "v"(q7), "v"(q4)); \
   asm volatile(WG_STEP8_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14));
 
+#ifndef WG_SHARED_DIAG
+#define WG_SHARED_DIAG 1  // first diagonal round with the two blocks' common words shared
+#endif
+
 // keystream blocks blk and blk+1 (same key and nonce) into ka, kb
 __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_t (&kb)[16],
                                                      const uint32_t k[8], uint32_t blk,
@@ -183,12 +187,94 @@ __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_
   // the first column round stays compiler-scheduled: with a wave-uniform key
   // and counter its wave-uniform columns run on the scalar unit
   WG_QR(p0, p4, p8, p12) WG_QR(p1, p5, p9, p13) WG_QR(p2, p6, p10, p14) WG_QR(p3, p7, p11, p15)
+#if !WG_SHARED_DIAG
   WG_QR(q0, q4, q8, q12) WG_QR(q1, q5, q9, q13) WG_QR(q2, q6, q10, q14) WG_QR(q3, q7, q11, q15)
+#endif
   __builtin_amdgcn_s_barrier();
 #if WG_CHACHA_PRIO
   __builtin_amdgcn_s_setprio(WG_CHACHA_PRIO);  // the phase-locked steps go first
 #endif
+#if WG_SHARED_DIAG
+  {
+    // The blocks differ only in word 12, so after the first column round their
+    // columns 1-3 are equal (s*: the compiler computes them once per packet and
+    // holds them) and only column 0 is per block.  The first diagonal round
+    // reads the common words as inputs and writes fresh registers -- in-place
+    // steps made the compiler copy every common word into both blocks first
+    // (24 v_mov per round) -- and the ops whose operands are all common (words
+    // 1 and 2's first add, word 13's first xor-rotate) run once for both.
+    WG_QR(q0, q4, q8, q12)
+    const uint32_t s1 = p1, s2 = p2, s3 = p3, s5 = p5, s6 = p6, s7 = p7;
+    const uint32_t s9 = p9, s10 = p10, s11 = p11, s13 = p13, s14 = p14, s15 = p15;
+    uint32_t a1, a2, d13;
+    // step 1: a += b; d ^= a; d <<<= 16   (6 + 7 + 7 ops instead of 8 + 8 + 8)
+    asm volatile(
+        "v_add_u32 %[p0], %[p0], %[s5]\n\tv_add_u32 %[q0], %[q0], %[s5]\n\t"
+        "v_add_u32 %[a1], %[s1], %[s6]\n\tv_add_u32 %[a2], %[s2], %[s7]\n\t"
+        "v_add_u32 %[p3], %[s3], %[p4]\n\tv_add_u32 %[q3], %[s3], %[q4]\n\t"
+        "v_xor_b32 %[p15], %[s15], %[p0]\n\tv_xor_b32 %[q15], %[s15], %[q0]\n\t"
+        "v_xor_b32 %[p12], %[p12], %[a1]\n\tv_xor_b32 %[q12], %[q12], %[a1]\n\t"
+        "v_xor_b32 %[d13], %[s13], %[a2]\n\t"
+        "v_xor_b32 %[p14], %[s14], %[p3]\n\tv_xor_b32 %[q14], %[s14], %[q3]\n\t"
+        "v_alignbit_b32 %[p15], %[p15], %[p15], 16\n\tv_alignbit_b32 %[q15], %[q15], %[q15], 16\n\t"
+        "v_alignbit_b32 %[p12], %[p12], %[p12], 16\n\tv_alignbit_b32 %[q12], %[q12], %[q12], 16\n\t"
+        "v_alignbit_b32 %[d13], %[d13], %[d13], 16\n\t"
+        "v_alignbit_b32 %[p14], %[p14], %[p14], 16\n\tv_alignbit_b32 %[q14], %[q14], %[q14], 16\n\t"
+        "s_barrier"
+        : [p0] "+v"(p0), [q0] "+v"(q0), [a1] "=&v"(a1), [a2] "=&v"(a2), [p3] "=&v"(p3),
+          [q3] "=&v"(q3), [p15] "=&v"(p15), [q15] "=&v"(q15), [p12] "+v"(p12), [q12] "+v"(q12),
+          [d13] "=&v"(d13), [p14] "=&v"(p14), [q14] "=&v"(q14)
+        : [s5] "v"(s5), [s1] "v"(s1), [s6] "v"(s6), [s2] "v"(s2), [s7] "v"(s7), [s3] "v"(s3),
+          [p4] "v"(p4), [q4] "v"(q4), [s15] "v"(s15), [s13] "v"(s13), [s14] "v"(s14));
+    // step 2: c += d; b ^= c; b <<<= 12
+    asm volatile(
+        "v_add_u32 %[p10], %[s10], %[p15]\n\tv_add_u32 %[q10], %[s10], %[q15]\n\t"
+        "v_add_u32 %[p11], %[s11], %[p12]\n\tv_add_u32 %[q11], %[s11], %[q12]\n\t"
+        "v_add_u32 %[p8], %[p8], %[d13]\n\tv_add_u32 %[q8], %[q8], %[d13]\n\t"
+        "v_add_u32 %[p9], %[s9], %[p14]\n\tv_add_u32 %[q9], %[s9], %[q14]\n\t"
+        "v_xor_b32 %[p5], %[s5], %[p10]\n\tv_xor_b32 %[q5], %[s5], %[q10]\n\t"
+        "v_xor_b32 %[p6], %[s6], %[p11]\n\tv_xor_b32 %[q6], %[s6], %[q11]\n\t"
+        "v_xor_b32 %[p7], %[s7], %[p8]\n\tv_xor_b32 %[q7], %[s7], %[q8]\n\t"
+        "v_xor_b32 %[p4], %[p4], %[p9]\n\tv_xor_b32 %[q4], %[q4], %[q9]\n\t"
+        "v_alignbit_b32 %[p5], %[p5], %[p5], 20\n\tv_alignbit_b32 %[q5], %[q5], %[q5], 20\n\t"
+        "v_alignbit_b32 %[p6], %[p6], %[p6], 20\n\tv_alignbit_b32 %[q6], %[q6], %[q6], 20\n\t"
+        "v_alignbit_b32 %[p7], %[p7], %[p7], 20\n\tv_alignbit_b32 %[q7], %[q7], %[q7], 20\n\t"
+        "v_alignbit_b32 %[p4], %[p4], %[p4], 20\n\tv_alignbit_b32 %[q4], %[q4], %[q4], 20\n\t"
+        "s_barrier"
+        : [p10] "=&v"(p10), [q10] "=&v"(q10), [p11] "=&v"(p11), [q11] "=&v"(q11), [p8] "+v"(p8),
+          [q8] "+v"(q8), [p9] "=&v"(p9), [q9] "=&v"(q9), [p5] "=&v"(p5), [q5] "=&v"(q5),
+          [p6] "=&v"(p6), [q6] "=&v"(q6), [p7] "=&v"(p7), [q7] "=&v"(q7), [p4] "+v"(p4),
+          [q4] "+v"(q4)
+        : [s10] "v"(s10), [s11] "v"(s11), [s9] "v"(s9), [p15] "v"(p15), [q15] "v"(q15),
+          [p12] "v"(p12), [q12] "v"(q12), [d13] "v"(d13), [p14] "v"(p14), [q14] "v"(q14),
+          [s5] "v"(s5), [s6] "v"(s6), [s7] "v"(s7));
+    // step 3: a += b; d ^= a; d <<<= 8   (words 1, 2 and 13 split into the two blocks here)
+    asm volatile(
+        "v_add_u32 %[p0], %[p0], %[p5]\n\tv_add_u32 %[q0], %[q0], %[q5]\n\t"
+        "v_add_u32 %[p1], %[a1], %[p6]\n\tv_add_u32 %[q1], %[a1], %[q6]\n\t"
+        "v_add_u32 %[p2], %[a2], %[p7]\n\tv_add_u32 %[q2], %[a2], %[q7]\n\t"
+        "v_add_u32 %[p3], %[p3], %[p4]\n\tv_add_u32 %[q3], %[q3], %[q4]\n\t"
+        "v_xor_b32 %[p15], %[p15], %[p0]\n\tv_xor_b32 %[q15], %[q15], %[q0]\n\t"
+        "v_xor_b32 %[p12], %[p12], %[p1]\n\tv_xor_b32 %[q12], %[q12], %[q1]\n\t"
+        "v_xor_b32 %[p13], %[d13], %[p2]\n\tv_xor_b32 %[q13], %[d13], %[q2]\n\t"
+        "v_xor_b32 %[p14], %[p14], %[p3]\n\tv_xor_b32 %[q14], %[q14], %[q3]\n\t"
+        "v_alignbit_b32 %[p15], %[p15], %[p15], 24\n\tv_alignbit_b32 %[q15], %[q15], %[q15], 24\n\t"
+        "v_alignbit_b32 %[p12], %[p12], %[p12], 24\n\tv_alignbit_b32 %[q12], %[q12], %[q12], 24\n\t"
+        "v_alignbit_b32 %[p13], %[p13], %[p13], 24\n\tv_alignbit_b32 %[q13], %[q13], %[q13], 24\n\t"
+        "v_alignbit_b32 %[p14], %[p14], %[p14], 24\n\tv_alignbit_b32 %[q14], %[q14], %[q14], 24\n\t"
+        "s_barrier"
+        : [p0] "+v"(p0), [q0] "+v"(q0), [p1] "=&v"(p1), [q1] "=&v"(q1), [p2] "=&v"(p2),
+          [q2] "=&v"(q2), [p3] "+v"(p3), [q3] "+v"(q3), [p15] "+v"(p15), [q15] "+v"(q15),
+          [p12] "+v"(p12), [q12] "+v"(q12), [p13] "=&v"(p13), [q13] "=&v"(q13), [p14] "+v"(p14),
+          [q14] "+v"(q14)
+        : [p5] "v"(p5), [q5] "v"(q5), [a1] "v"(a1), [p6] "v"(p6), [q6] "v"(q6), [a2] "v"(a2),
+          [p7] "v"(p7), [q7] "v"(q7), [d13] "v"(d13), [p4] "v"(p4), [q4] "v"(q4));
+    // step 4: the ordinary in-place step (no common words left)
+    asm volatile(WG_STEP8_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14));
+  }
+#else
   WG_DIAGONAL_ROUND2
+#endif
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
     WG_COLUMN_ROUND2
