@@ -476,6 +476,26 @@ __device__ __forceinline__ void store16(u32x4 data, uint64_t base, uint32_t byte
                :: "v"(data), "v"(voff), "s"(rs), "s"(soff) : "memory");
 }
 
+// Per-piece LDS destinations (m0) and soffsets of a uniform round, derived
+// from two values made opaque to the optimiser each round: otherwise it hoists
+// the 8 destinations and 8 soffsets out of the round loop, runs out of SGPRs
+// and restores them from VGPR lanes -- 16 v_readlane (VALU, energy at the power
+// limit) per round.  Recomputed, they cost one SALU add each.
+#ifndef WG_STAGE_CHAIN
+#define WG_STAGE_CHAIN 1
+#endif
+struct StageChain {
+  uint32_t lds0, step, soff0;
+  __device__ StageChain(uint4 *run, uint32_t stride, uint32_t r)
+      : lds0(lds_offset(run)), step(8u * stride), soff0(kRun * r) {
+    asm volatile("" : "+s"(lds0), "+s"(step));
+  }
+  __device__ __attribute__((address_space(3))) void *lds(uint32_t j) const {
+    return (__attribute__((address_space(3))) void *)(uintptr_t)(lds0 + 1024u * j);
+  }
+  __device__ uint32_t soff(uint32_t j) const { return soff0 + j * step; }
+};
+
 template <bool kSeal, bool kText>
 __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &g, uint32_t lane,
                                          uint32_t r) {
@@ -506,20 +526,36 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &
     // interior round (wave-uniform test): every lane moves a full chunk, the
     // per-lane offsets are round-independent -- no range checks
     const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
+#if WG_STAGE_CHAIN
+    StageChain c(run, stride, r);
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, c.lds(j), 16, (j & 1u) ? v1 : v0, c.soff(j), 0,
+                                               WG_LOAD_CPOL);
+#else
 #pragma unroll
     for (uint32_t j = 0; j < kChunks; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16, (j & 1u) ? v1 : v0,
                                                8u * j * stride + kRun * r, 0, WG_LOAD_CPOL);
+#endif
     return;
   }
+#if WG_STAGE_CHAIN
+  StageChain c(run, stride, r);
+#endif
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
     const bool ok = w >= R::in_lo() && w < hi;
+#if WG_STAGE_CHAIN
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, c.lds(j), 16, ok ? y * stride + 16u * k : kNoAccess,
+                                             c.soff(j), 0, WG_LOAD_CPOL);
+#else
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16,
                                              ok ? y * stride + 16u * k : kNoAccess,
                                              8u * j * stride + kRun * r, 0, WG_LOAD_CPOL);
+#endif
   }
 }
 
@@ -980,19 +1016,31 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     if constexpr (kUniform) {
       using R = Ranges<kSeal, kText>;
       const uint32_t zlo = (R::out_hi(g.W) + 15u) & ~15u;  // first chunk wholly past the output
-      // (addresses from an opaque copy of the lane: computed here, in the
-      // rounds that zero, rather than hoisted and held in VGPRs)
-      uint32_t lz = ln, zero = 0u;
-      asm volatile("" : "+v"(lz), "+v"(zero));
-      const uint32_t row = 8u * lz, sw = swz(lz);
-      const uint4 z = make_uint4(zero, zero, zero, zero);
+      // (addresses from an opaque copy of the lane, computed inside the
+      // wave-uniform branches: only the rounds that zero pay for them, and
+      // nothing is hoisted and held in VGPRs)
+      auto slots = [&](uint32_t &row, uint32_t &sw, uint4 &z) {
+        uint32_t lz = ln, zero = 0u;
+        asm volatile("" : "+v"(lz), "+v"(zero));
+        row = 8u * lz;
+        sw = swz(lz);
+        z = make_uint4(zero, zero, zero, zero);
+      };
       if ((zlo >> 7) == r) {
         const uint32_t kz = (zlo >> 4) & 7u;
+        uint32_t row, sw;
+        uint4 z;
+        slots(row, sw, z);
 #pragma unroll
         for (uint32_t k = 1; k < kChunks; ++k)
           if (k >= kz) run[row + (k ^ sw)] = z;
       }
-      if (R::out_lo() > 0u && r == 0u) run[row + (0u ^ sw)] = z;
+      if (R::out_lo() > 0u && r == 0u) {
+        uint32_t row, sw;
+        uint4 z;
+        slots(row, sw, z);
+        run[row + (0u ^ sw)] = z;
+      }
     }
   };
 
@@ -1079,7 +1127,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // the keystream lives only inside this branch (kept out of phis, the
         // compiler would otherwise carry it as a register tuple and spill it)
         uint32_t ka[16], kb[16];
-        chacha20_block2_sync(ka, kb, key, 2u * r + 1u, n1, n2);
+        chacha20_block2_sync<WG_SHARED_DIAG && kUniform>(ka, kb, key, 2u * r + 1u, n1, n2);
         WG_STAMP_AT(kSeal, r, 2);
         landed();
         if (my_runs) {

@@ -174,7 +174,10 @@ __device__ __forceinline__ void chacha20_block_sync(uint32_t (&ks)[16], const ui
 #define WG_SHARED_DIAG 1  // first diagonal round with the two blocks' common words shared
 #endif
 
-// keystream blocks blk and blk+1 (same key and nonce) into ka, kb
+// keystream blocks blk and blk+1 (same key and nonce) into ka, kb.  kShared:
+// the first diagonal round on the blocks' common words (below); the descriptor
+// kernels (per-lane keys) keep the in-place form, where it cost one more spill.
+template <bool kShared = WG_SHARED_DIAG>
 __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_t (&kb)[16],
                                                      const uint32_t k[8], uint32_t blk,
                                                      uint32_t n1, uint32_t n2) {
@@ -187,15 +190,14 @@ __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_
   // the first column round stays compiler-scheduled: with a wave-uniform key
   // and counter its wave-uniform columns run on the scalar unit
   WG_QR(p0, p4, p8, p12) WG_QR(p1, p5, p9, p13) WG_QR(p2, p6, p10, p14) WG_QR(p3, p7, p11, p15)
-#if !WG_SHARED_DIAG
-  WG_QR(q0, q4, q8, q12) WG_QR(q1, q5, q9, q13) WG_QR(q2, q6, q10, q14) WG_QR(q3, q7, q11, q15)
-#endif
+  if constexpr (!kShared) {
+    WG_QR(q0, q4, q8, q12) WG_QR(q1, q5, q9, q13) WG_QR(q2, q6, q10, q14) WG_QR(q3, q7, q11, q15)
+  }
   __builtin_amdgcn_s_barrier();
 #if WG_CHACHA_PRIO
   __builtin_amdgcn_s_setprio(WG_CHACHA_PRIO);  // the phase-locked steps go first
 #endif
-#if WG_SHARED_DIAG
-  {
+  if constexpr (kShared) {
     // The blocks differ only in word 12, so after the first column round their
     // columns 1-3 are equal (s*: the compiler computes them once per packet and
     // holds them) and only column 0 is per block.  The first diagonal round
@@ -271,10 +273,9 @@ __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_
           [p7] "v"(p7), [q7] "v"(q7), [d13] "v"(d13), [p4] "v"(p4), [q4] "v"(q4));
     // step 4: the ordinary in-place step (no common words left)
     asm volatile(WG_STEP8_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14));
+  } else {
+    WG_DIAGONAL_ROUND2
   }
-#else
-  WG_DIAGONAL_ROUND2
-#endif
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
     WG_COLUMN_ROUND2
