@@ -109,13 +109,16 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 // Cache policy of the streaming traffic (every byte is read once and written
 // once), as LLVM CPol bits for gfx940+: 1 = sc0, 2 = nt, 16 = sc1 (and sums).
 // The kernels are power-capped (PPT 1400 W, profiles/r02_power.json), so what
-// the memory hierarchy spends per byte is clock the VALU does not get; the
-// default policy measured best (nt on loads and/or stores: -8 %, tools/ab.py).
+// the memory hierarchy spends per byte is clock the VALU does not get:
+// non-temporal loads and stores (nt) run config 2's round trip 2.5 % and
+// config 4's 2.9 % faster than the default policy (profiles/r02_ab_cache_policy.txt;
+// nt stores alone let the seal run at 2.09 instead of 1.90 GHz under the same
+// limit).  (Round 1 measured nt 8 % slower, on kernels not yet at the limit.)
 #ifndef WG_LOAD_CPOL
-#define WG_LOAD_CPOL 0
+#define WG_LOAD_CPOL 2
 #endif
 #ifndef WG_STORE_CPOL
-#define WG_STORE_CPOL 0
+#define WG_STORE_CPOL 2
 #endif
 #define WG_CPOL_ASM_0 ""
 #define WG_CPOL_ASM_1 " sc0"
