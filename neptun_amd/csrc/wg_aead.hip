@@ -120,6 +120,15 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #ifndef WG_STORE_CPOL
 #define WG_STORE_CPOL 2
 #endif
+// the owner-lane stores of a packet's partial last chunk (dword / short / byte,
+// no slot padding) keep the default policy: as nt stores their partial writes
+// made an unpadded round trip 18 % slower
+#ifndef WG_PARTIAL_STORE_CPOL
+#define WG_PARTIAL_STORE_CPOL 0
+#endif
+#ifndef WG_EDGE_STORE_NT
+#define WG_EDGE_STORE_NT 0  // unpadded edge rounds' 16-byte stores: 0 = default policy
+#endif
 #define WG_CPOL_ASM_0 ""
 #define WG_CPOL_ASM_1 " sc0"
 #define WG_CPOL_ASM_2 " nt"
@@ -132,6 +141,7 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_CPOL_ASM(x) WG_CPOL_ASM_(x)
 #define WG_LOAD_NT_ASM WG_CPOL_ASM(WG_LOAD_CPOL)
 #define WG_STORE_NT_ASM WG_CPOL_ASM(WG_STORE_CPOL)
+#define WG_PARTIAL_STORE_ASM WG_CPOL_ASM(WG_PARTIAL_STORE_CPOL)
 
 #ifndef WG_SYNC_KEY_BLOCK
 #define WG_SYNC_KEY_BLOCK 1  // phase-locked Poly1305 key block on the sync paths
@@ -472,11 +482,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(uint64_t base, uint3
 // the new values (tools/diff_variants.py found 1 % of packets corrupted in a
 // build whose register allocation did that).  The asm form keeps two wait
 // states between the store and any later write of its data registers.
+// kStream = false: the default cache policy, for stores into lines that are
+// only partly written (an unpadded packet's last line): as nt stores those cost
+// an unpadded round trip several % (profiles/r02_ab_cache_policy.txt).
+template <bool kStream = true>
 __device__ __forceinline__ void store16(u32x4 data, uint64_t base, uint32_t bytes, uint32_t voff,
                                         uint32_t soff) {
   const u32x4 rs = {(uint32_t)base, (uint32_t)(base >> 32) & 0xffffu, bytes, 0x00020000u};
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen" WG_STORE_NT_ASM "\n\ts_nop 1"
-               :: "v"(data), "v"(voff), "s"(rs), "s"(soff) : "memory");
+  if constexpr (kStream)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen" WG_STORE_NT_ASM "\n\ts_nop 1"
+                 :: "v"(data), "v"(voff), "s"(rs), "s"(soff) : "memory");
+  else
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen" WG_PARTIAL_STORE_ASM "\n\ts_nop 1"
+                 :: "v"(data), "v"(voff), "s"(rs), "s"(soff) : "memory");
 }
 
 // Per-piece LDS destinations (m0) and soffsets of a uniform round, derived
@@ -616,7 +634,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
       store16(vv, g.out0, records, mine ? y * stride + 16u * k : kNoAccess, 8u * j * stride + kRun * r);
     } else {
       const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
-      store16(vv, g.out0, records, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
+      store16<WG_EDGE_STORE_NT != 0>(vv, g.out0, records, ok && hi - w >= 16u ? y * stride + 16u * k : kNoAccess,
               8u * j * stride + kRun * r);
     }
   }
@@ -630,16 +648,16 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
     const bool gone = !kSeal && ((dead >> lane) & 1ull);
     const uint4 c = run[8u * lane + (((wp >> 4) & 7u) ^ swz(lane))];
     const uint32_t base = gone ? kNoAccess : lane * stride + wp;
-    if (q >= 4u) __builtin_amdgcn_raw_buffer_store_b32(c.x, rs, base, 0, WG_STORE_CPOL);
-    if (q >= 8u) __builtin_amdgcn_raw_buffer_store_b32(c.y, rs, base + 4u, 0, WG_STORE_CPOL);
-    if (q >= 12u) __builtin_amdgcn_raw_buffer_store_b32(c.z, rs, base + 8u, 0, WG_STORE_CPOL);
+    if (q >= 4u) __builtin_amdgcn_raw_buffer_store_b32(c.x, rs, base, 0, WG_PARTIAL_STORE_CPOL);
+    if (q >= 8u) __builtin_amdgcn_raw_buffer_store_b32(c.y, rs, base + 4u, 0, WG_PARTIAL_STORE_CPOL);
+    if (q >= 12u) __builtin_amdgcn_raw_buffer_store_b32(c.z, rs, base + 8u, 0, WG_PARTIAL_STORE_CPOL);
     const uint32_t nd = q >> 2, rem = q & 3u;
     const uint32_t last = nd == 0 ? c.x : nd == 1 ? c.y : nd == 2 ? c.z : c.w;
     if (rem >= 2u)
-      __builtin_amdgcn_raw_buffer_store_b16((unsigned short)last, rs, base + 4u * nd, 0, WG_STORE_CPOL);
+      __builtin_amdgcn_raw_buffer_store_b16((unsigned short)last, rs, base + 4u * nd, 0, WG_PARTIAL_STORE_CPOL);
     if (rem & 1u)
       __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(last >> (8u * (rem & 2u))), rs,
-                                           base + 4u * nd + (rem & 2u), 0, WG_STORE_CPOL);
+                                           base + 4u * nd + (rem & 2u), 0, WG_PARTIAL_STORE_CPOL);
   }
 }
 
