@@ -396,10 +396,17 @@ __device__ __forceinline__ void dma_global(uint32_t lds, const uint8_t *src) {
 }
 #pragma clang diagnostic pop
 
+// kStream = false: the default cache policy (stores into partly written lines,
+// see store16)
+template <bool kStream = true>
 __device__ __forceinline__ void gstore16(uint8_t *dst, const uint4 v) {
   const u32x4 vv = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off" WG_STORE_NT_ASM "\n\ts_nop 1" :: "v"(dst), "v"(vv)
-               : "memory");
+  if constexpr (kStream)
+    asm volatile("global_store_dwordx4 %0, %1, off" WG_STORE_NT_ASM "\n\ts_nop 1" :: "v"(dst), "v"(vv)
+                 : "memory");
+  else
+    asm volatile("global_store_dwordx4 %0, %1, off" WG_PARTIAL_STORE_ASM "\n\ts_nop 1" :: "v"(dst),
+                 "v"(vv) : "memory");
 }
 
 // the first k (1..15) bytes of a chunk, through global-address-space pointers
@@ -450,7 +457,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const Geom &g, uint32_t la
       uint8_t *dst = reinterpret_cast<uint8_t *>(g.out_base(p)) + w;
       const uint32_t n = hi - w;
       if (n >= 16u) {
-        gstore16(dst, v);
+        gstore16<WG_EDGE_STORE_NT != 0>(dst, v);  // (edge rounds: lines partly written)
       } else {
         const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
         gstore_partial(dst, wv, (int)n);
