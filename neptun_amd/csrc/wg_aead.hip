@@ -98,6 +98,9 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_OPAQUE_LANE_DESC 1
 #endif
 
+#ifndef WG_HDR_NT
+#define WG_HDR_NT 0  // open's early header fetch with the streaming (nt) policy
+#endif
 #ifndef WG_HDR_DMA
 #define WG_HDR_DMA 1  // uniform open: headers by LDS-DMA ahead of round 0, counted vmcnt(8) wait
 #endif
@@ -390,9 +393,17 @@ __device__ __forceinline__ uint32_t lds_offset(const uint4 *p) {
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
+// kStream = false: the default cache policy -- for open's early header fetch,
+// whose line round 0 loads again right after (as nt, HBM served that line
+// twice: +1.1 % of open's traffic, PMC)
+template <bool kStream = true>
 __device__ __forceinline__ void dma_global(uint32_t lds, const uint8_t *src) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, off" WG_LOAD_NT_ASM
-               :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(src) : "memory", "m0");
+  if constexpr (kStream)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, off" WG_LOAD_NT_ASM
+                 :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(src) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, off"
+                 :: "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(src) : "memory", "m0");
 }
 #pragma clang diagnostic pop
 
@@ -1093,7 +1104,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // pieces, issuing most of round 0's DMA a memory latency late.)  The
         // tag park is free until round 0's tag bytes land (open_keep_tail).
         if (my_runs)
-          dma_global(lds_offset(&S.tagp[0]), reinterpret_cast<const uint8_t *>(job.in_base - (16u - kG)));
+          dma_global<WG_HDR_NT != 0>(lds_offset(&S.tagp[0]), reinterpret_cast<const uint8_t *>(job.in_base - (16u - kG)));
         stage_in<kSeal>(run, g, lane, 0);  // exactly 8 pieces (round 0 is straight-line)
         u32x4 h;
         asm volatile("s_waitcnt vmcnt(8)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
