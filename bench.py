@@ -40,6 +40,11 @@ def parse(argv=None):
     ap.add_argument("--packets", type=int, default=1 << 20, help="config 2: packets per GPU")
     ap.add_argument("--size", type=int, default=1350)
     ap.add_argument("--stride", type=int, default=0, help="config 2 slot stride (0 = round up to 128)")
+    ap.add_argument("--layout", default="slots", choices=("slots", "neptun"),
+                    help="config 2 buffers: 'slots' = datagram at slot+0 / plaintext at slot+16 on both "
+                         "sides with slot padding (the fast layout); 'neptun' = NepTUN's own layouts: "
+                         "seal in place (device/mod.rs:1297-1337), open into a fresh buffer at offset 0 "
+                         "(device/mod.rs:1140-1148), no slot padding")
     ap.add_argument("--per-size", type=int, default=1 << 18, help="config 3: packets per size")
     ap.add_argument("--peers", type=int, default=4096, help="config 4")
     ap.add_argument("--per-peer", type=int, default=4096, help="config 4")
@@ -49,6 +54,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = one per physical core of this job's CPU share "
                          "(min of affinity, physical cores, OMP_NUM_THREADS)")
+    ap.add_argument("--cpu-curve", default="1,2,4,8",
+                    help="extra thread counts timed for the CPU baseline's scaling curve (capped by "
+                         "the thread count above; empty = none)")
     ap.add_argument("--sustain-seconds", type=float, default=2.0,
                     help="N=1: extra seconds of steps after the timed region, reported apart as "
                          "'sustained' (the power-capped steady state; never the headline value)")
@@ -63,7 +71,15 @@ def parse(argv=None):
 # {seal, open}, .kernels {seal, open} (rocprof names), .describe() -> dict
 # ---------------------------------------------------------------------------
 class StridedWorkload:
-    """Config 2 / 5: one session, uniform 1350 B, counters = base + lane index."""
+    """Config 2 / 5: one session, uniform 1350 B, counters = base + lane index.
+
+    layout "slots": plaintext at slot+16 (NepTUN's WG_HEADER_OFFSET, device/mod.rs:76)
+    sealed into a separate wire buffer (datagram at slot+0) and opened back to
+    slot+16, with slot padding -- both sides 128-byte-run aligned.
+    layout "neptun": the buffers NepTUN itself hands to Tunn -- encapsulate_in_place
+    seals the TUN buffer in place (plaintext at +16, datagram written over it at
+    +0, device/mod.rs:1297-1337) and decapsulate opens the UDP buffer into a fresh
+    buffer at offset 0 (device/mod.rs:1140-1148, the text-grid open); no padding."""
 
     def __init__(self, args, dev, rank, world):
         import numpy as np
@@ -76,18 +92,26 @@ class StridedWorkload:
         if S % 16 or S < P + 32:
             raise SystemExit("--stride must be a multiple of 16 and hold P + 32 bytes")
         self.S = S
+        self.layout = getattr(args, "layout", "slots")
         self.ctx = neptun_amd.GpuContext(dev.index, key_slots=1)
         self.ctx.set_keys(0, synth.keys(1), np.array([synth.RECEIVER_IDX], np.uint32))
         # the slots' padding past each output is scratch here (as in NepTUN's
         # MAX_PKT_SIZE buffers): outputs are zero-filled to their 128-byte line end
-        self.pad = not args.no_slot_padding
+        self.pad = not args.no_slot_padding and self.layout == "slots"
         self.ctx.set_slot_padding(self.pad)
         # shard: rank r owns packets [r*n, (r+1)*n) of the global batch; counters follow
         self.counter_base = rank * n
         # NepTUN slot layout (WG_HEADER_OFFSET = 16, device/mod.rs:76): plaintext 16
         # bytes into each slot, the datagram at the slot start -- both run-aligned
         self.pt = synth.device_payloads(n, P, S, dev, seed=synth.SEED + rank, offset=16)
-        self.wire = torch.zeros(n * S, dtype=torch.uint8, device=dev)
+        if self.layout == "neptun":
+            # the TUN buffers: sealed in place, so each step re-seals what the last
+            # one left there (same work); verify() restores them from self.pt first
+            self.wire = self.pt.clone()
+            self.open_off = 0
+        else:
+            self.wire = torch.zeros(n * S, dtype=torch.uint8, device=dev)
+            self.open_off = 16
         self.back = torch.zeros(n * S, dtype=torch.uint8, device=dev)
         self.st_seal = torch.full((n,), -1, dtype=torch.int32, device=dev)
         self.st_open = torch.full((n,), -1, dtype=torch.int32, device=dev)
@@ -96,26 +120,38 @@ class StridedWorkload:
         # algorithmic HBM bytes per launch: seal reads P, writes P+32; open the reverse
         self.launch_bytes = {"seal": n * (2 * P + 32), "open": n * (2 * P + 32)}
         self.kernels = {"seal": "aead_strided_kernel<true, false>",
-                        "open": "aead_strided_kernel<false, false>"}
+                        "open": "aead_strided_open_text_kernel" if self.layout == "neptun"
+                        else "aead_strided_kernel<false, false>"}
+        self.profile_tag = "config2_neptun" if self.layout == "neptun" else "config2"
+
+    def _seal_src(self):
+        return (self.wire if self.layout == "neptun" else self.pt).data_ptr() + 16
 
     def step(self, stream, evs=None):
         S, P, n = self.S, self.P, self.n
         if evs:
             evs[0].record(stream)
-        self.ctx.seal_strided(n, P, 0, self.counter_base, self.pt.data_ptr() + 16, S, self.wire, S,
+        self.ctx.seal_strided(n, P, 0, self.counter_base, self._seal_src(), S, self.wire, S,
                               self.st_seal, stream)
         if evs:
             evs[1].record(stream)
-        self.ctx.open_strided(n, P + 32, 0, self.wire, S, self.back.data_ptr() + 16, S,
+        self.ctx.open_strided(n, P + 32, 0, self.wire, S, self.back.data_ptr() + self.open_off, S,
                               self.st_open, stream)
         if evs:
             evs[2].record(stream)
 
     def verify(self):
         import torch
-        n, S, P = self.n, self.S, self.P
+        n, S, P, o = self.n, self.S, self.P, self.open_off
+        if self.layout == "neptun":
+            # the timed steps re-sealed the TUN buffers in place: one more step from
+            # the original plaintext, then check that one
+            self.wire.copy_(self.pt)
+            self.back.zero_()
+            self.step(None)
+            torch.cuda.synchronize()
         ok = int((self.st_seal != 0).sum()) == 0 and int((self.st_open != 0).sum()) == 0
-        return ok and torch.equal(self.back.view(n, S)[:, 16:16 + P], self.pt.view(n, S)[:, 16:16 + P])
+        return ok and torch.equal(self.back.view(n, S)[:, o:o + P], self.pt.view(n, S)[:, 16:16 + P])
 
     def size_hist(self):
         return {self.P: self.n}
@@ -133,12 +169,18 @@ class StridedWorkload:
                  wire[j, :self.P + 32].tobytes()) for j, i in enumerate(idx)]
 
     def describe(self, world):
-        return {"workload": f"BASELINE config {'2' if world == 1 else '5'}: {self.n} x {self.P} B "
-                            "packets per GPU, single session, seal then open, device-resident",
-                "packets_per_gpu": self.n, "packet_bytes": self.P, "slot_stride": self.S,
-                "global_packets": world * self.n, "parallelism": f"{world} shard(s), no collective",
-                "slot_padding": ("writable: outputs zero-filled to their 128-byte line end "
-                                 "(wg_gpu_ctx_set_slot_padding)") if self.pad else "untouched"}
+        d = {"workload": f"BASELINE config {'2' if world == 1 else '5'}: {self.n} x {self.P} B "
+                         "packets per GPU, single session, seal then open, device-resident",
+             "packets_per_gpu": self.n, "packet_bytes": self.P, "slot_stride": self.S,
+             "global_packets": world * self.n, "parallelism": f"{world} shard(s), no collective",
+             "layout": self.layout,
+             "slot_padding": ("writable: outputs zero-filled to their 128-byte line end "
+                              "(wg_gpu_ctx_set_slot_padding)") if self.pad else "untouched"}
+        if self.layout == "neptun":
+            d["layout_note"] = ("NepTUN's buffers: seal in place (plaintext at slot+16 overwritten by "
+                                "the datagram at slot+0, device/mod.rs:1297-1337), open into fresh "
+                                "slots at offset 0 (device/mod.rs:1140-1148)")
+        return d
 
     def close(self):
         self.ctx.close()
@@ -173,6 +215,7 @@ class DescWorkload:
         self.launch_bytes = {"seal": int((2 * P + 32).sum()) + key_bytes,
                              "open": int((2 * P + 32).sum()) + key_bytes}
         self.kernels = {"seal": "aead_desc_sync_kernel<true>", "open": "aead_desc_sync_kernel<false>"}
+        self.profile_tag = f"config{self.cfg}"
 
     def step(self, stream, evs=None):
         b, ctx = self.b, self.ctx
@@ -251,22 +294,34 @@ def host_cpus() -> dict:
             "logical_cpus": os.cpu_count() or 1, "allowed_cpus": allowed}
 
 
+def smi_index(local: int) -> int:
+    """amd-smi's index of this rank's GPU: HIP device `local` after any
+    *_VISIBLE_DEVICES remapping (one process per GPU, torchrun's LOCAL_RANK)."""
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            ids = [x.strip() for x in v.split(",") if x.strip()]
+            if local < len(ids) and ids[local].isdigit():
+                return int(ids[local])
+    return local
+
+
 class PowerSampler:
-    """Socket power / gfx clock / PPT state of GPU 0 (`amd-smi metric`, read-only)
+    """Socket power / gfx clock / PPT state of one GPU (`amd-smi metric -g`, read-only)
     sampled on a host thread while the supplementary sustained steps run: the
     kernels are power-bound, so the line says at what power and
     clock its sustained rate was reached.  Never fatal: no amd-smi -> an error note."""
 
-    def __init__(self, period: float = 0.05):
+    def __init__(self, period: float = 0.05, gpu: int = 0):
         import threading
-        self.period, self.samples, self.error = period, [], None
+        self.period, self.gpu, self.samples, self.error = period, gpu, [], None
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, daemon=True)
 
     def _run(self):
         from tools import power_probe
         while not self._stop.is_set():
-            s = power_probe.sample()
+            s = power_probe.sample(self.gpu)
             if "err" in s:
                 self.error = str(s["err"])[:120]
                 return
@@ -282,13 +337,35 @@ class PowerSampler:
         self._thread.join(timeout=30)
         if self.error and not self.samples:
             return {"error": self.error}
-        return dict(power_probe.summarize(self.samples), source="amd-smi metric during the sustained steps")
+        return dict(power_probe.summarize(self.samples), amd_smi_gpu=self.gpu,
+                    source="amd-smi metric during the sustained steps")
 
 
-def cpu_baseline(threads: int, cpus: dict) -> dict:
+# the package power limit of MI355X (amd-smi reports PPT 1400 W on the boxes);
+# a line is labelled power-limited only when its mean socket power reaches this
+PPT_LIMITED_W = 1390.0
+
+
+def power_limiter(pw: dict) -> str | None:
+    """The roofline.limiter label: 'package power' only when the sustained steps
+    drew the PPT limit (mean socket power >= PPT_LIMITED_W with PPT flagged),
+    else None -- a PPT flag at lower mean power does not make the time
+    power-set (config 4 at 1308-1328 W)."""
+    if "ACTIVE" in pw.get("ppt_violation", []) and pw.get("socket_power_W", 0) >= PPT_LIMITED_W:
+        # what holds the kernels below the HBM roofline (DESIGN.md 3.1)
+        return (f"package power: {pw['socket_power_W']} W with the PPT limit active at "
+                f"{pw['gfx_clock_MHz']} MHz during the sustained steps; time per launch = energy "
+                "per launch / power budget")
+    return None
+
+
+def cpu_baseline(threads: int, cpus: dict, curve=()) -> dict:
     """Config 1 on the host cores: oracle/build/cpu_baseline (NepTUN framing over
     OpenSSL EVP, the stand-in for ring's asm; see oracle/cpu_baseline.c), one
-    session per thread like packet_workers.rs:113-131 (num_cpus::get_physical())."""
+    session per thread like packet_workers.rs:113-131 (num_cpus::get_physical()).
+    Measured at `threads` (this job's CPU share) and at each count of `curve`
+    below it, so the per-core scaling behind the all-core figure is measured,
+    not assumed."""
     exe = os.path.join(ROOT, "oracle", "build", "cpu_baseline")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
@@ -301,7 +378,12 @@ def cpu_baseline(threads: int, cpus: dict) -> dict:
         return json.loads(out.stdout)
 
     one = run(1, 11)
+    pts = {1: one["gbps"]}
+    for t in sorted({int(c) for c in curve if 1 < int(c) < threads}):
+        pts[t] = run(t, 11)["gbps"]
     many = run(threads, 21)
+    pts[threads] = many["gbps"]
+    per_core_at_share = many["gbps"] / threads
     return {
         "value": round(many["gbps"], 3),
         "unit": "Gbit/s",
@@ -319,8 +401,15 @@ def cpu_baseline(threads: int, cpus: dict) -> dict:
                    f"{cpus['model']}); "
                    f"1 thread: {one['gbps']:.3f} Gbit/s"),
         "one_core_gbps": round(one["gbps"], 3),
-        # linear extrapolation of the 1-thread rate, labelled as such (not measured)
-        "all_physical_cores_extrapolated_gbps": round(one["gbps"] * cpus["physical_cores"], 1),
+        "threads_gbps": {str(k): round(v, 3) for k, v in sorted(pts.items())},
+        "scaling_efficiency_at_share": round(per_core_at_share / one["gbps"], 3),
+        # the GPU box grants one job `threads` CPUs (its share); the machine's other
+        # cores belong to other jobs, so the all-core figure is the measured
+        # per-core rate at the share times the physical cores -- labelled, not measured
+        "all_physical_cores_extrapolated_gbps": round(per_core_at_share * cpus["physical_cores"], 1),
+        "all_physical_cores_note": ("measured per-core rate at this job's CPU share x physical cores; "
+                                    "not run on all cores because the GPU box grants one job a "
+                                    f"{threads}-CPU share of the machine"),
     }
 
 
@@ -340,11 +429,11 @@ def evp_check(wl, k: int) -> dict:
     return {"checked": len(smp), "mismatches": bad}
 
 
-def load_pmc(kind: str, kernel: str, config: int) -> dict | None:
-    """Committed rocprofv3 PMC summary of one bench kernel for this config:
+def load_pmc(kind: str, kernel: str, tag: str) -> dict | None:
+    """Committed rocprofv3 PMC summary of one bench kernel for this workload:
     kind "traffic" (tools/pmc_traffic.py, HBM bytes per launch) or "valu"
     (tools/pmc_valu.py, clock + VALU instructions per wave)."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{kind}_config{config}.json")
+    path = os.path.join(ROOT, "profiles", f"pmc_{kind}_{tag}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -355,26 +444,39 @@ def load_pmc(kind: str, kernel: str, config: int) -> dict | None:
     return dict(k, source=os.path.relpath(path, ROOT), how=d.get("source", ""))
 
 
-def compute_roofline(wl, kernel: str, config: int, kernel_ms: float) -> dict:
-    """VALU-issue floor of the launch (tools/compute_roofline.py) at the clock the
-    PMC run measured for this kernel, against the live kernel time."""
+def compute_roofline(wl, kernel: str, kernel_ms: float, live_clock_ghz: float | None,
+                     sustained_ms: float | None = None) -> dict | None:
+    """VALU-issue floor of the launch (tools/compute_roofline.py), priced at the
+    live gfx clock (amd-smi during this run's sustained steps) against the live
+    kernel time; the PMC run's own clock and time only as frac_in_profiled_run."""
     from tools import compute_roofline as cr
     if not hasattr(wl, "size_hist"):
         return None
-    pmc = load_pmc("valu", kernel, config)
-    clock = pmc["clock_GHz"] if pmc else None
-    fl = cr.launch_floor(wl.size_hist(), clock)
+    keyed = getattr(wl, "cfg", 2) == 4  # per-lane keys: no SALU columns, no shared diagonal
+    fl = cr.launch_floor(wl.size_hist(), live_clock_ghz, per_lane_keys=keyed)
     out = {"bound": "valu-issue", "model": "tools/compute_roofline.py", **fl}
+    if live_clock_ghz:
+        out["clock_GHz_live"] = round(live_clock_ghz, 4)
+        out["clock_source"] = "amd-smi gfx clock, mean over the sustained steps of this run"
+        out["frac"] = round(fl["floor_ms_at_clock"] / kernel_ms, 4)
+        if sustained_ms:
+            out["frac_sustained"] = round(fl["floor_ms_at_clock"] / sustained_ms, 4)
+    pmc = load_pmc("valu", kernel, getattr(wl, "profile_tag", "config2"))
     if pmc:
         out.update({
             "clock_GHz_profiled": pmc["clock_GHz"],
-            "frac": round(fl["floor_ms_at_profiled_clock"] / kernel_ms, 4),
-            "frac_in_profiled_run": round(fl["floor_ms_at_profiled_clock"] / pmc["ms"], 4),
+            "frac_in_profiled_run": round(
+                cr.launch_floor(wl.size_hist(), pmc["clock_GHz"], per_lane_keys=keyed)["floor_ms_at_clock"]
+                / pmc["ms"], 4),
             "valu_instr_per_64_packets_measured": round(
                 pmc["valu_per_wave"] * pmc.get("waves", 0) * 64 / wl.packets, 1),
             "pmc_source": pmc["source"],
         })
     return out
+
+
+def mean(xs):
+    return sum(xs) / len(xs) if xs else 0.0
 
 
 def run(args, factory=None, device_fn=None, device_count=None):
@@ -423,6 +525,7 @@ def run(args, factory=None, device_fn=None, device_count=None):
         wl.step(stream, events[k])
     sync()
     elapsed = time.perf_counter() - t0
+    my_elapsed = elapsed
     totals = torch.tensor([wl.payload_bytes, wl.packets], dtype=torch.float64)
     if world > 1:
         dist.barrier()
@@ -447,30 +550,51 @@ def run(args, factory=None, device_fn=None, device_count=None):
         dist.all_reduce(f, op=dist.ReduceOp.MAX)
         ok = int(f.item()) == 0
     sustained = None
-    if ok and world == 1 and args.sustain_seconds > 0 and args.steps > 0:
+    if ok and args.sustain_seconds > 0 and args.steps > 0:
         # the kernels run at the package power limit (profiles/r02_power.json);
         # over the first tens of ms the clock is still settling, so the K-step
-        # line above and a seconds-long run can differ by a few %
-        per = max(elapsed / args.steps, 1e-4)
+        # line above and a seconds-long run can differ by a few %.  Every rank
+        # runs it at once (its own GPU's power and clock sampled), so an N-GPU
+        # line says what each package did while all of them were loaded.
+        per = max(my_elapsed / args.steps, 1e-4)
         k2 = max(1, int(args.sustain_seconds / per))
-        ev = [new_event(), new_event()]
-        sampler = PowerSampler() if device_fn is None else None
+        if world > 1:  # one count for all ranks: they start and end together
+            kt = torch.tensor([k2], dtype=torch.int64)
+            dist.all_reduce(kt, op=dist.ReduceOp.MIN)
+            k2 = int(kt.item())
+        evs = [[new_event() for _ in range(3)] for _ in range(k2)]
+        sampler = PowerSampler(gpu=smi_index(local)) if device_fn is None else None
         sync()
+        if world > 1:
+            dist.barrier()
         if sampler:
             sampler.start()  # samples while the steps run (idle samples are filtered out)
-        ev[0].record(stream)
-        for _ in range(k2):
-            wl.step(stream)
-        ev[1].record(stream)
+        for k in range(k2):
+            wl.step(stream, evs[k])
         sync()
-        ms = ev[0].elapsed_time(ev[1])
+        ms = evs[0][0].elapsed_time(evs[-1][2])
         sustained = {"steps": k2, "seconds": round(ms * 1e-3, 3),
                      "gbps": round(wl.payload_bytes * 8 * k2 / (ms * 1e-3) / 1e9, 2),
                      "ms_per_step": round(ms / k2, 4),
+                     "kernel_ms": {"seal": round(mean([e[0].elapsed_time(e[1]) for e in evs]), 4),
+                                   "open": round(mean([e[1].elapsed_time(e[2]) for e in evs]), 4)},
                      "note": "supplementary: steps run after the timed region and its "
                              "verification; not the headline value"}
         if sampler:
             sustained["power"] = sampler.stop()
+    avg = {"seal": mean(seal_ms), "open": mean(open_ms)}
+    mine = {"rank": rank, "local_rank": local, "elapsed_s": round(my_elapsed, 6),
+            "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+            "packets": wl.packets, "payload_bytes": wl.payload_bytes}
+    if sustained:
+        mine["sustained_gbps"] = sustained["gbps"]
+        mine["sustained_kernel_ms"] = sustained["kernel_ms"]
+        if "power" in sustained:
+            mine["power"] = sustained["power"]
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     line = None
     if not ok:
         line = {"error": "verification failed (statuses, round trip or EVP sample)", "rank": rank,
@@ -478,10 +602,12 @@ def run(args, factory=None, device_fn=None, device_count=None):
     elif rank == 0:
         total_payload, total_pkts = float(totals[0]), float(totals[1])
         gbps = total_payload * 8 * args.steps / elapsed / 1e9
-        avg = {"seal": sum(seal_ms) / len(seal_ms), "open": sum(open_ms) / len(open_ms)}
         dom = "seal" if avg["seal"] >= avg["open"] else "open"
         achieved = wl.launch_bytes[dom] / (avg[dom] * 1e-3) / 1e9
-        tr = load_pmc("traffic", wl.kernels[dom], args.config)
+        tag = getattr(wl, "profile_tag", f"config{args.config}")
+        tr = load_pmc("traffic", wl.kernels[dom], tag)
+        pw = (sustained or {}).get("power") or {}
+        live_clock = pw["gfx_clock_MHz"] / 1e3 if pw.get("gfx_clock_MHz") else None
         line = {
             "metric": METRIC if args.config == 2 else
             f"Gbit/s device-resident ChaCha20-Poly1305 seal+open, BASELINE config {args.config}",
@@ -511,7 +637,8 @@ def run(args, factory=None, device_fn=None, device_count=None):
                 "traffic_source": tr["source"] if tr else None,
                 "algorithmic_bytes_per_launch": wl.launch_bytes[dom],
                 # the bound that actually limits the kernel: VALU issue
-                "compute": compute_roofline(wl, wl.kernels[dom], args.config, avg[dom]),
+                "compute": compute_roofline(wl, wl.kernels[dom], avg[dom], live_clock,
+                                            ((sustained or {}).get("kernel_ms") or {}).get(dom)),
             },
             "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
             "seal_gbps": round(wl.payload_bytes * 8 / (avg["seal"] * 1e-3) / 1e9, 1),
@@ -525,22 +652,20 @@ def run(args, factory=None, device_fn=None, device_count=None):
             "evp_sample": evp,
             "sustained": sustained,
         }
-        pw = (sustained or {}).get("power") or {}
-        if "ACTIVE" in pw.get("ppt_violation", []):
-            # what actually holds the kernels below the HBM roofline
-            line["roofline"]["limiter"] = (
-                f"package power: {pw['socket_power_W']} W with the PPT limit active at "
-                f"{pw['gfx_clock_MHz']} MHz during the sustained steps; time per launch = energy "
-                "per launch / power budget, both energy terms (VALU instructions, HBM bytes) at "
-                "their floors")
+        if world > 1:
+            line["per_rank"] = per_rank
+        lim = power_limiter(pw)
+        if lim:
+            line["roofline"]["limiter"] = lim
         if world == 1 and not args.no_cpu_baseline and args.config == 2:
             cpus = host_cpus()
             # one thread per physical core this job may use: the GPU box grants a
             # job a CPU share (OMP_NUM_THREADS there) of a larger machine
             share = int(os.environ.get("OMP_NUM_THREADS") or cpus["allowed_cpus"])
             threads = args.cpu_threads or max(1, min(cpus["allowed_cpus"], cpus["physical_cores"], share))
+            curve = [int(x) for x in args.cpu_curve.split(",") if x.strip()] if args.cpu_curve else []
             try:
-                line["cpu_baseline"] = cpu_baseline(threads, cpus)
+                line["cpu_baseline"] = cpu_baseline(threads, cpus, curve)
             except Exception as e:  # reported, never fatal to the GPU number
                 line["cpu_baseline"] = {"error": str(e)[:200]}
     if line is not None:

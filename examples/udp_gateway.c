@@ -67,6 +67,8 @@ typedef struct {
   uint32_t *rx_len;
   _Atomic uint32_t n_rx;
   _Atomic int rx_done;
+  _Atomic int send_done;       /* the sender has sent (or given up on) all its datagrams */
+  _Atomic uint32_t n_written_off; /* datagrams the sender's flow control counts as lost */
   /* decrypt worker output */
   uint8_t **dst;
   uint32_t *dst_cap;
@@ -115,7 +117,7 @@ static void *sender(void *arg) {
   uint32_t *cap = calloc(B, sizeof *cap);
   struct mmsghdr *msgs = calloc(B, sizeof *msgs);
   struct iovec *iov = calloc(B, sizeof *iov);
-  for (uint32_t i0 = g->i0; i0 < n && !atomic_load(&g->failed); i0 += B) {
+  for (uint32_t i0 = g->i0; i0 < n && !atomic_load(&g->failed) && !atomic_load(&g->rx_done); i0 += B) {
     const uint32_t m = n - i0 < B ? n - i0 : B;
     for (uint32_t j = 0; j < m; ++j) cap[j] = g->slot;
     double t = now();
@@ -138,16 +140,31 @@ static void *sender(void *arg) {
       msgs[k].msg_hdr.msg_iovlen = 1;
       ++k;
     }
-    /* flow control: at most `window` datagrams in the receiver's socket queue */
+    /* flow control: at most `window` datagrams in the receiver's socket queue.
+       Lost datagrams never arrive, so a window that has not moved for 1 s is
+       written off (counted as lost) instead of waited for forever; the reader
+       ending (rx_done) or a failure stops the sender. */
     uint32_t done = 0;
+    double stall_since = -1.0;
+    uint32_t stall_rx = 0;
     while (done < k) {
-      const uint32_t inflight = atomic_load(&g->n_sent) - atomic_load(&g->n_rx);
+      if (atomic_load(&g->rx_done) || atomic_load(&g->failed)) break;
+      const uint32_t rx = atomic_load(&g->n_rx);
+      const uint32_t inflight = atomic_load(&g->n_sent) - rx - atomic_load(&g->n_written_off);
       if (inflight >= g->window) {
         t = now();
+        if (stall_since < 0 || rx != stall_rx) {
+          stall_since = t;
+          stall_rx = rx;
+        } else if (t - stall_since > 1.0) {
+          atomic_fetch_add(&g->n_written_off, inflight);
+          stall_since = -1.0;
+        }
         sched_yield();
         g->t_wait += now() - t;
         continue;
       }
+      stall_since = -1.0;
       uint32_t can = g->window - inflight;
       if (can > k - done) can = k - done;
       t = now();
@@ -162,6 +179,7 @@ static void *sender(void *arg) {
       atomic_fetch_add(&g->n_sent, (uint32_t)r);
     }
   }
+  atomic_store(&g->send_done, 1);
   free(res); free(cap); free(msgs); free(iov);
   return NULL;
 }
@@ -172,7 +190,10 @@ static void *reader(void *arg) {
   const uint32_t n = g->i1 - g->i0, B = g->batch;
   struct mmsghdr *msgs = calloc(B, sizeof *msgs);
   struct iovec *iov = calloc(B, sizeof *iov);
-  double idle_since = now();
+  /* idle clock: from the first datagram on (a slow first GPU batch is not
+     idleness), and only once the sender is done may 2 s of silence end the run */
+  double idle_since = -1.0;
+  const double t_start = now();
   while (atomic_load(&g->n_rx) < n && !atomic_load(&g->failed)) {
     const uint32_t base = atomic_load(&g->n_rx);
     const uint32_t m = n - base < B ? n - base : B;
@@ -188,8 +209,11 @@ static void *reader(void *arg) {
     const int r = recvmmsg(g->sb, msgs, m, MSG_WAITFORONE, &to);
     g->t_recv += now() - t;
     if (r <= 0) {
-      /* every datagram that was sent has arrived or is lost: stop after 2 s idle */
-      if (now() - idle_since > 2.0) break;
+      /* every datagram that was sent has arrived or is lost: stop after 2 s
+         idle once the sender is done; nothing at all for 60 s ends it too */
+      const double tn = now();
+      if (atomic_load(&g->send_done) && tn - (idle_since < 0 ? t_start : idle_since) > 2.0) break;
+      if (idle_since < 0 && tn - t_start > 60.0) break;
       continue;
     }
     idle_since = now();

@@ -247,7 +247,9 @@ int wg_gpu_handshake_anon_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32
  * Under load (RateLimiter::verify_packet, rate_limiter.rs:197-218):
  *   wg_gpu_mac2_check_batch: cookie = MAC(secret, LE64(counter) || addr) and the
  *     mac2 check of each handshake message (len 148 or 92); status 0 valid,
- *     1 = answer with a cookie reply; the cookie is returned.
+ *     1 = answer with a cookie reply; the cookie is returned.  Any other length
+ *     is not a handshake message (parse_incoming_packet rejects it): status
+ *     WG_STATUS_INVALID_PACKET, cookie zeroed, nothing of the message read.
  *   wg_gpu_cookie_reply_batch: format_cookie_reply (rate_limiter.rs:133-170):
  *     nonce = b2s_mac_24(nonce_key, LE64(nonce_ctr)) (the caller hands out
  *     nonce_ctr in reply order, :112-121), XChaCha20-Poly1305(cookie_key, nonce,

@@ -98,6 +98,12 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_OPAQUE_LANE_DESC 1
 #endif
 
+// descriptor kernels (per-lane keys): the shared first diagonal round too (the
+// two blocks' columns 1-3 are equal after the first column round whatever the key)
+#ifndef WG_SHARED_DIAG_DESC
+#define WG_SHARED_DIAG_DESC 0
+#endif
+
 #ifndef WG_HDR_NT
 #define WG_HDR_NT 0  // open's early header fetch with the streaming (nt) policy
 #endif
@@ -122,6 +128,16 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #endif
 #ifndef WG_STORE_CPOL
 #define WG_STORE_CPOL 2
+#endif
+// the text grid's loads (open into offset-0 destinations): each 128-byte run of
+// the datagram starts 16 bytes into a line, so every line is read by two rounds
+// (its head in round r, the rest in round r + 1).  As nt loads HBM served such
+// a line twice (PMC: 2.80 GB read per 1M x 1350 B open against 1.48 GB on the
+// wire grid, profiles/pmc_traffic_config2_neptun.json); with the default policy
+// the line stays in L2 for the second read: open 0.815 -> 0.758 ms
+// (profiles/r03_ab_text_grid.txt)
+#ifndef WG_TEXT_LOAD_CPOL
+#define WG_TEXT_LOAD_CPOL 0
 #endif
 // the owner-lane stores of a packet's partial last chunk (dword / short / byte,
 // no slot padding) keep the default policy: as nt stores their partial writes
@@ -539,6 +555,7 @@ template <bool kSeal, bool kText>
 __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &g, uint32_t lane,
                                          uint32_t r) {
   using R = Ranges<kSeal, kText>;
+  constexpr int kCpol = kText ? WG_TEXT_LOAD_CPOL : WG_LOAD_CPOL;
   const uint32_t stride = (uint32_t)g.in_stride;
   const uint32_t hi = R::in_hi(g.W);
   // num_records = the end of the wave's last packet's input, rounded up to its
@@ -570,12 +587,12 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &
 #pragma unroll
     for (uint32_t j = 0; j < kChunks; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, c.lds(j), 16, (j & 1u) ? v1 : v0, c.soff(j), 0,
-                                               WG_LOAD_CPOL);
+                                               kCpol);
 #else
 #pragma unroll
     for (uint32_t j = 0; j < kChunks; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16, (j & 1u) ? v1 : v0,
-                                               8u * j * stride + kRun * r, 0, WG_LOAD_CPOL);
+                                               8u * j * stride + kRun * r, 0, kCpol);
 #endif
     return;
   }
@@ -589,11 +606,11 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &
     const bool ok = w >= R::in_lo() && w < hi;
 #if WG_STAGE_CHAIN
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, c.lds(j), 16, ok ? y * stride + 16u * k : kNoAccess,
-                                             c.soff(j), 0, WG_LOAD_CPOL);
+                                             c.soff(j), 0, kCpol);
 #else
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16,
                                              ok ? y * stride + 16u * k : kNoAccess,
-                                             8u * j * stride + kRun * r, 0, WG_LOAD_CPOL);
+                                             8u * j * stride + kRun * r, 0, kCpol);
 #endif
   }
 }
@@ -981,7 +998,9 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       n2 = h.w;
       one_time_key();
     }
-    if constexpr (kUniform) g.dead = __ballot(job.status != WG_STATUS_OK);
+    // (the non-phase-locked loop calls this in a divergent branch: it takes the
+    // ballot itself, outside it)
+    if constexpr (kUniform && kSync) g.dead = __ballot(job.status != WG_STATUS_OK);
   };
   // open: collect the received tag before the slots are decrypted in place.
   // It is bytes [q, q + 16) of the 32 raw bytes [wt, wt + 32), which sit in
@@ -1166,7 +1185,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // the keystream lives only inside this branch (kept out of phis, the
         // compiler would otherwise carry it as a register tuple and spill it)
         uint32_t ka[16], kb[16];
-        chacha20_block2_sync<WG_SHARED_DIAG && kUniform>(ka, kb, key, 2u * r + 1u, n1, n2);
+        chacha20_block2_sync<WG_SHARED_DIAG && (kUniform || WG_SHARED_DIAG_DESC)>(ka, kb, key, 2u * r + 1u, n1, n2);
         WG_STAMP_AT(kSeal, r, 2);
         landed();
         if (my_runs) {
@@ -1213,6 +1232,14 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
           crypt_round<kSeal>(run, lane, r, P, key, n1, n2, poly, ks_save);
           if (kSeal) seal_tail(run, r);
         }
+      }
+      if constexpr (kUniform && !kSeal) {
+        if (r == 0) g.dead = __ballot(job.status != WG_STATUS_OK);
+      }
+      // (uniform geometry built with WG_SYNC=0: slot padding writes whole lines
+      // here too, so the stage chunks outside the output are zeroed first)
+      if constexpr (kUniform) {
+        if (WG_FULL_LINES && g.pad) zero_outside(run, lane, r);
       }
 #if !WG_ABLATE_NO_MEM
       stage_out<kSeal>(run, g, lane, r);
@@ -1300,7 +1327,8 @@ __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams 
       return;
     }
 #endif
-    run_wave<kSeal, true, WG_SYNC != 0>(stage, g, lane, job, prm.keys, prm.key_index, st, sk);
+    // (the text grid exists only in the phase-locked form)
+    run_wave<kSeal, true, WG_SYNC != 0 || kText>(stage, g, lane, job, prm.keys, prm.key_index, st, sk);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
     LdsGeom g{stage};

@@ -295,8 +295,133 @@ __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_
 }
 
 // ---------------------------------------------------------------------------
-// Poly1305 (RFC 8439 2.5), radix 2^32: h = h0..h3 (32-bit) + h4 (< 8)
+// Poly1305 (RFC 8439 2.5) -- two limb schemes, same results bit for bit:
+//  * radix 2^32 (default): 4 x 32-bit limbs + a 3-bit top limb, 21
+//    v_mad_u64_u32 on full 32-bit operands, 39 VALU per 16-byte block;
+//  * radix 2^26 (-DWG_POLY_RADIX26=1): 5 x 26-bit limbs (poly1305-donna-32),
+//    25 v_mad_u64_u32 whose operands carry <= 27 / 29 significant bits, 54
+//    VALU per block.  More instructions, narrower multiplies: built to measure
+//    energy per block at the package power limit, where time
+//    follows energy, not issue slots.
 // ---------------------------------------------------------------------------
+#ifndef WG_POLY_RADIX26
+#define WG_POLY_RADIX26 0
+#endif
+
+#if WG_POLY_RADIX26
+struct Poly {
+  uint32_t h0, h1, h2, h3, h4;  // 26-bit limbs (h1 may carry a few bits more between blocks)
+  uint32_t r0, r1, r2, r3, r4;  // clamped r, 26-bit limbs
+  uint32_t s1, s2, s3, s4;      // 5 * r_i (2^130 == 5)
+};
+
+__device__ __forceinline__ void poly_init(Poly &p, const uint32_t ks0[8]) {
+  const uint32_t w0 = ks0[0] & 0x0fffffffu, w1 = ks0[1] & 0x0ffffffcu, w2 = ks0[2] & 0x0ffffffcu,
+                 w3 = ks0[3] & 0x0ffffffcu;
+  p.r0 = w0 & 0x3ffffffu;
+  p.r1 = ((w0 >> 26) | (w1 << 6)) & 0x3ffffffu;
+  p.r2 = ((w1 >> 20) | (w2 << 12)) & 0x3ffffffu;
+  p.r3 = ((w2 >> 14) | (w3 << 18)) & 0x3ffffffu;
+  p.r4 = w3 >> 8;
+  p.s1 = 5u * p.r1;
+  p.s2 = 5u * p.r2;
+  p.s3 = 5u * p.r3;
+  p.s4 = 5u * p.r4;
+  p.h0 = p.h1 = p.h2 = p.h3 = p.h4 = 0;
+}
+
+// h = (h + m + 2^128) * r, partially reduced.  Bounds: h_i < 2^27 after the
+// add, s_i < 2^29, so each product < 2^56 and each 5-term chain + seed < 2^59;
+// d4 (no s terms) < 2^55.4, so its carry fits 32 bits and 5 * it fits too.
+__device__ __forceinline__ void poly_block(Poly &p, uint32_t m0, uint32_t m1, uint32_t m2,
+                                           uint32_t m3) {
+  // m + 2^128 in 26-bit limbs (funnel shifts), added to h
+  const uint32_t a0 = p.h0 + (m0 & 0x3ffffffu);
+  const uint32_t a1 = p.h1 + (__builtin_amdgcn_alignbit(m1, m0, 26) & 0x3ffffffu);
+  const uint32_t a2 = p.h2 + (__builtin_amdgcn_alignbit(m2, m1, 20) & 0x3ffffffu);
+  const uint32_t a3 = p.h3 + (__builtin_amdgcn_alignbit(m3, m2, 14) & 0x3ffffffu);
+  const uint32_t a4 = p.h4 + ((m3 >> 8) | (1u << 24));
+  uint64_t d0, d1, d2, d3, d4, seed, sc;
+  asm volatile(
+      // d0 = h0 r0 + h1 s4 + h2 s3 + h3 s2 + h4 s1
+      "v_mad_u64_u32 %[d0], %[sc], %[a0], %[r0], 0\n\t"
+      "v_mad_u64_u32 %[d0], %[sc], %[a1], %[s4], %[d0]\n\t"
+      "v_mad_u64_u32 %[d0], %[sc], %[a2], %[s3], %[d0]\n\t"
+      "v_mad_u64_u32 %[d0], %[sc], %[a3], %[s2], %[d0]\n\t"
+      "v_mad_u64_u32 %[d0], %[sc], %[a4], %[s1], %[d0]\n\t"
+      // d1 = (d0 >> 26) + h0 r1 + h1 r0 + h2 s4 + h3 s3 + h4 s2
+      "v_lshrrev_b64 %[seed], 26, %[d0]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a0], %[r1], %[seed]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a1], %[r0], %[d1]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a2], %[s4], %[d1]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a3], %[s3], %[d1]\n\t"
+      "v_mad_u64_u32 %[d1], %[sc], %[a4], %[s2], %[d1]\n\t"
+      // d2 = (d1 >> 26) + h0 r2 + h1 r1 + h2 r0 + h3 s4 + h4 s3
+      "v_lshrrev_b64 %[seed], 26, %[d1]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a0], %[r2], %[seed]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a1], %[r1], %[d2]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a2], %[r0], %[d2]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a3], %[s4], %[d2]\n\t"
+      "v_mad_u64_u32 %[d2], %[sc], %[a4], %[s3], %[d2]\n\t"
+      // d3 = (d2 >> 26) + h0 r3 + h1 r2 + h2 r1 + h3 r0 + h4 s4
+      "v_lshrrev_b64 %[seed], 26, %[d2]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a0], %[r3], %[seed]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a1], %[r2], %[d3]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a2], %[r1], %[d3]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a3], %[r0], %[d3]\n\t"
+      "v_mad_u64_u32 %[d3], %[sc], %[a4], %[s4], %[d3]\n\t"
+      // d4 = (d3 >> 26) + h0 r4 + h1 r3 + h2 r2 + h3 r1 + h4 r0
+      "v_lshrrev_b64 %[seed], 26, %[d3]\n\t"
+      "v_mad_u64_u32 %[d4], %[sc], %[a0], %[r4], %[seed]\n\t"
+      "v_mad_u64_u32 %[d4], %[sc], %[a1], %[r3], %[d4]\n\t"
+      "v_mad_u64_u32 %[d4], %[sc], %[a2], %[r2], %[d4]\n\t"
+      "v_mad_u64_u32 %[d4], %[sc], %[a3], %[r1], %[d4]\n\t"
+      "v_mad_u64_u32 %[d4], %[sc], %[a4], %[r0], %[d4]"
+      : [d0] "=&v"(d0), [d1] "=&v"(d1), [d2] "=&v"(d2), [d3] "=&v"(d3), [d4] "=&v"(d4),
+        [seed] "=&v"(seed), [sc] "=&s"(sc)
+      : [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [a4] "v"(a4),
+        [r0] "v"(p.r0), [r1] "v"(p.r1), [r2] "v"(p.r2), [r3] "v"(p.r3), [r4] "v"(p.r4),
+        [s1] "v"(p.s1), [s2] "v"(p.s2), [s3] "v"(p.s3), [s4] "v"(p.s4));
+  // bits >= 130: c = d4 >> 26 (< 2^30), folded as 5c into limb 0, one carry into limb 1
+  const uint32_t c = __builtin_amdgcn_alignbit((uint32_t)(d4 >> 32), (uint32_t)d4, 26);
+  const uint32_t h0 = ((uint32_t)d0 & 0x3ffffffu) + 5u * c;
+  p.h0 = h0 & 0x3ffffffu;
+  p.h1 = ((uint32_t)d1 & 0x3ffffffu) + (h0 >> 26);
+  p.h2 = (uint32_t)d2 & 0x3ffffffu;
+  p.h3 = (uint32_t)d3 & 0x3ffffffu;
+  p.h4 = (uint32_t)d4 & 0x3ffffffu;
+}
+
+// tag = (h mod p) + s mod 2^128 (full carry, h + 5 >= 2^130 <=> h >= p)
+__device__ __forceinline__ void poly_finish(const Poly &p, const uint32_t s[4], uint32_t tag[4]) {
+  uint32_t h0 = p.h0, h1 = p.h1, h2 = p.h2, h3 = p.h3, h4 = p.h4, c;
+  c = h1 >> 26; h1 &= 0x3ffffffu; h2 += c;
+  c = h2 >> 26; h2 &= 0x3ffffffu; h3 += c;
+  c = h3 >> 26; h3 &= 0x3ffffffu; h4 += c;
+  c = h4 >> 26; h4 &= 0x3ffffffu; h0 += 5u * c;
+  c = h0 >> 26; h0 &= 0x3ffffffu; h1 += c;
+  // g = h + 5 - 2^130
+  uint32_t g0 = h0 + 5u; c = g0 >> 26; g0 &= 0x3ffffffu;
+  uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= 0x3ffffffu;
+  uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= 0x3ffffffu;
+  uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= 0x3ffffffu;
+  const uint32_t g4 = h4 + c - (1u << 26);
+  const bool ge = (g4 >> 31) == 0u;  // no borrow: h >= p
+  if (ge) { h0 = g0; h1 = g1; h2 = g2; h3 = g3; h4 = g4; }
+  const uint32_t f0 = h0 | (h1 << 26), f1 = (h1 >> 6) | (h2 << 20), f2 = (h2 >> 12) | (h3 << 14),
+                 f3 = (h3 >> 18) | (h4 << 8);
+  uint64_t t = (uint64_t)f0 + s[0];
+  tag[0] = (uint32_t)t;
+  t = (uint64_t)f1 + s[1] + (t >> 32);
+  tag[1] = (uint32_t)t;
+  t = (uint64_t)f2 + s[2] + (t >> 32);
+  tag[2] = (uint32_t)t;
+  tag[3] = f3 + s[3] + (uint32_t)(t >> 32);
+}
+
+#else  // radix 2^32
+
+// radix 2^32: h = h0..h3 (32-bit) + h4 (< 8)
 struct Poly {
   uint32_t h0, h1, h2, h3, h4;
   uint32_t r0, r1, r2, r3;  // clamped r
@@ -495,6 +620,8 @@ __device__ __forceinline__ void poly_finish(const Poly &p, const uint32_t s[4], 
   tag[2] = (uint32_t)t;
   tag[3] = f3 + s[3] + (uint32_t)(t >> 32);
 }
+
+#endif  // WG_POLY_RADIX26
 
 // ---------------------------------------------------------------------------
 // byte-granular helpers for the packet tail (run once per packet)

@@ -335,6 +335,16 @@ __global__ __launch_bounds__(256) void mac2_check_kernel(Mac2CheckParams prm) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= prm.n) return;
   const uint32_t len = prm.lens[i];
+  // only what parse_incoming_packet hands to verify_packet reaches the check:
+  // a 148-byte initiation or a 92-byte response (noise/mod.rs:139-199); any
+  // other length is rejected there, and here, before anything is read
+  // (the host guarantees stride >= 148, so both lengths fit their slot)
+  if (len != 148u && len != 92u) {
+    prm.status[i] = WG_STATUS_INVALID_PACKET;
+    const uint32_t z[4] = {0u, 0u, 0u, 0u};
+    st_words(prm.cookies + 16ull * i, z, 4);
+    return;
+  }
   uint32_t w[37];
   const uint32_t *q = reinterpret_cast<const uint32_t *>(prm.msgs + prm.stride * i);
 #pragma unroll

@@ -502,14 +502,14 @@ void make_chunks(Engine &E, SizeFn size, size_t limit = 0) {
   if (k0 < E.k1) E.chunks.push_back(Chunk{k0, E.k1, bytes});
 }
 
-// Split the selected packets [0, n) into contiguous engine ranges of about
-// equal staging bytes (size(k) per packet).
+// Split the selected packets [a, b) (default: all of them) into contiguous
+// engine ranges of about equal staging bytes (size(k) per packet).
 template <class SizeFn>
-void split(wg_tunn *t, SizeFn size) {
-  const size_t n = t->sel.size(), E = t->eng.size();
+void split(wg_tunn *t, SizeFn size, size_t a = 0, size_t b = ~size_t(0)) {
+  const size_t n = std::min(b, t->sel.size()), E = t->eng.size();
   uint64_t total = 0;
-  for (size_t k = 0; k < n; ++k) total += size(k);
-  size_t k = 0;
+  for (size_t k = a; k < n; ++k) total += size(k);
+  size_t k = a;
   uint64_t acc = 0;
   for (size_t e = 0; e < E; ++e) {
     t->eng[e]->k0 = k;
@@ -720,15 +720,18 @@ void validate(wg_tunn *t, const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
 // the plaintext on a tag mismatch); the copies then run on the pools.
 //  * one engine: a double-buffered chunk pipeline; each chunk is decided as it
 //    returns while the next runs on the GPU;
-//  * several engines: every engine opens its whole share at once (one chunk,
-//    in parallel on its own GPU and NUMA node); then the caller decides all
-//    packets in order; then every engine copies its share out.
+//  * several engines: the selection is cut into rounds of about
+//    engines x chunk_bytes() staging bytes; in each round every engine opens
+//    its share as one chunk (in parallel on its own GPU and NUMA node), then
+//    the caller decides the round's packets in order, then every engine copies
+//    its share out.  Pinned staging per engine stays one chunk whatever the
+//    batch size (a 16M-packet batch over 2 GPUs needs no more than 1 GPU does).
 template <class Decide>
 int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *len,
                   uint8_t *const *dst, Decide decide) {
   const bool multi = t->eng.size() > 1;
   auto size = [&](size_t k) { return round128(len[t->sel[k]]); };
-  split(t, size);
+  if (!multi) split(t, size);
   auto copy_out = [&](Engine &E, const Chunk &ch, Staging &S, const std::vector<uint8_t> &action) {
     E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
       for (size_t kk = lo; kk < hi; ++kk) {
@@ -779,17 +782,31 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     };
     return run_chunks(E, false, pack, unpack, direct, false);
   };
-  int rc = for_engines(t, engine_job);
-  if (rc || !multi) return rc;
-  // several engines: one chunk each, its results still in staging set 0
-  for (Engine *E : t->eng) {
-    if (E->chunks.empty()) continue;
-    for (size_t k = E->k0; k < E->k1; ++k) action[k] = decide(k, E->st[0], k - E->k0);
+  if (!multi) return for_engines(t, engine_job);
+  // several engines: rounds of about engines x chunk_bytes() staging bytes
+  const size_t n = t->sel.size();
+  const uint64_t cap = (uint64_t)chunk_bytes() * t->eng.size();
+  for (size_t a = 0; a < n;) {
+    size_t b = a;
+    uint64_t acc = 0;
+    while (b < n && (b == a || acc + size(b) <= cap)) acc += size(b++);
+    split(t, size, a, b);
+    const int rc = for_engines(t, engine_job);
+    if (rc) return rc;
+    // one chunk per engine, its results still in staging set 0; decided in
+    // packet order (engine ranges are contiguous and ordered)
+    for (Engine *E : t->eng) {
+      if (E->chunks.empty()) continue;
+      for (size_t k = E->k0; k < E->k1; ++k) action[k] = decide(k, E->st[0], k - E->k0);
+    }
+    const int rc2 = for_engines(t, [&](Engine &E) -> int {
+      if (!E.chunks.empty()) copy_out(E, E.chunks[0], E.st[0], action);
+      return WG_RC_OK;
+    });
+    if (rc2) return rc2;
+    a = b;
   }
-  return for_engines(t, [&](Engine &E) -> int {
-    if (!E.chunks.empty()) copy_out(E, E.chunks[0], E.st[0], action);
-    return WG_RC_OK;
-  });
+  return WG_RC_OK;
 }
 
 void destroy_engine(Engine *E) {

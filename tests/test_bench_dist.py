@@ -69,7 +69,7 @@ def _worker(rank, world, port, outdir, fail_rank, device_count=None):
     if fail_rank is not None:
         os.environ["FAKE_FAIL_RANK"] = str(fail_rank)
     import bench
-    args = bench.parse(["--steps", "5", "--warmup", "1", "--no-cpu-baseline"])
+    args = bench.parse(["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--sustain-seconds", "0.05"])
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
         rc = bench.run(args, factory=FakeWorkload, device_fn=cpu_device,
@@ -106,6 +106,16 @@ def test_two_ranks_aggregate_max_time_and_sum_payload(tmp_path, world):
     want = total_payload * 8 / (line["ms_per_step"] * 1e-3) / 1e9
     assert abs(line["value"] - want) / want < 1e-3
     assert line["config"]["parallelism"] == "2 shard(s), no collective"
+    # every rank's own numbers travel with the line, so a sub-linear N-GPU result
+    # can be attributed to a rank (its kernel times, its sustained rate and, on
+    # GPUs, its own package's power / clock / PPT state)
+    pr = line["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1] and [r["local_rank"] for r in pr] == [0, 1]
+    assert pr[1]["kernel_ms"]["seal"] >= 1.9 and pr[0]["kernel_ms"]["seal"] < pr[1]["kernel_ms"]["seal"]
+    assert [r["packets"] for r in pr] == [1000, 2000]
+    assert max(r["elapsed_s"] for r in pr) * 1e3 / 5 == pytest.approx(line["ms_per_step"], rel=1e-3)
+    assert all(r["sustained_gbps"] > 0 and r["sustained_kernel_ms"]["seal"] > 0 for r in pr)
+    assert line["sustained"]["steps"] >= 1
 
 
 def test_failed_verification_on_any_rank_fails_the_run(tmp_path):
@@ -131,14 +141,34 @@ def test_power_sampler_never_fails_the_bench(monkeypatch):
     from tools import power_probe
     calls = []
 
-    def fake_sample():
-        calls.append(1)
+    def fake_sample(gpu=0):
+        calls.append(gpu)
         return {"err": "amd-smi: no GPU"} if len(calls) > 2 else {"gpu_data": []}
 
     monkeypatch.setattr(power_probe, "sample", fake_sample)
-    s = bench.PowerSampler(period=0.01)
+    s = bench.PowerSampler(period=0.01, gpu=3)
     s.start()
     time.sleep(0.2)
     out = s.stop()
     assert out.get("busy_samples") == 0 or "error" in out
-    assert len(calls) == 3  # stops sampling at the first error
+    assert calls == [3, 3, 3]  # its own GPU; stops sampling at the first error
+
+
+def test_smi_index_follows_visible_devices(monkeypatch):
+    import bench
+    for v in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.smi_index(5) == 5
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "6,7")
+    assert bench.smi_index(1) == 7
+
+
+def test_limiter_label_needs_the_power_limit():
+    """roofline.limiter says 'package power' only when the mean socket power
+    reaches the PPT limit (>= 1390 W), not whenever a sample flags PPT."""
+    import bench
+    pw = {"socket_power_W": 1397.0, "gfx_clock_MHz": 1963.8, "ppt_violation": ["ACTIVE"]}
+    assert bench.power_limiter(pw).startswith("package power: 1397.0 W")
+    assert bench.power_limiter(dict(pw, socket_power_W=1323.0)) is None
+    assert bench.power_limiter(dict(pw, ppt_violation=["NOT ACTIVE"])) is None
+    assert bench.power_limiter({}) is None

@@ -252,3 +252,35 @@ def test_cookie_mac2_check_and_reply_match_oracle(torch_cuda, gpu):
         assert got == want, k
         assert H.xchacha20poly1305_open(cookie_key, got[8:32], msgs[i][-32:-16], got[32:]) == \
             jobs[k]["cookie"].tobytes()
+
+
+def test_mac2_check_rejects_non_handshake_lengths(torch_cuda, gpu):
+    """Only 148- and 92-byte messages reach the mac2 check (parse_incoming_packet,
+    noise/mod.rs:139-199); any other length -- 0, 16 (len - 16 would wrap), 91,
+    147, 200 (past the slot) -- gets WG_STATUS_INVALID_PACKET and a zero cookie,
+    without the kernel reading the message, while valid neighbours still check."""
+    torch = torch_cuda
+    from neptun_amd import gpu as G
+    rng = random.Random(41)
+    secret = rng.randbytes(16)
+    counter = rng.getrandbits(40)
+    lens = [0, 16, 148, 91, 147, 200, 92, 0xFFFFFFF0]
+    n = len(lens)
+    stride = 148
+    d_m = to_dev(torch, rng.randbytes(stride * n))
+    d_l = to_dev(torch, np.array(lens, np.uint32).tobytes())
+    addrs = [rng.randbytes(16) for _ in range(n)]
+    d_a = to_dev(torch, b"".join(addrs))
+    d_c = torch.full((16 * n,), 0xAB, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.mac2_check_batch(secret, counter, n, d_m, stride, d_l, d_a, d_c, d_st)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    cookies = d_c.cpu().numpy().tobytes()
+    for i, ln in enumerate(lens):
+        if ln in (148, 92):
+            assert st[i] in (0, 1)
+            assert cookies[16 * i:16 * i + 16] == H.current_cookie(secret, counter, addrs[i])
+        else:
+            assert G.STATUS[int(st[i])] == "InvalidPacket", (i, ln)
+            assert cookies[16 * i:16 * i + 16] == bytes(16)

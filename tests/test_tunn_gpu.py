@@ -416,12 +416,18 @@ def test_registered_direct_batches_match_sequential_tunn(gpu, seed):
     tg.close()
 
 
-def test_multi_engine_split_matches_sequential_tunn(torch_cuda):
+@pytest.mark.parametrize("chunk_kb", [None, "64"])
+def test_multi_engine_split_matches_sequential_tunn(torch_cuda, monkeypatch, chunk_kb):
     """wg_tunn_create_multi over two contexts on device 0 (the 1-GPU stand-in for
     one context per GPU): every batch is split into two byte-balanced shares that
     run concurrently on their own driver threads, streams and pinned staging, after
     ONE counter reservation (session.rs:219).  Results, destination bytes,
-    counters, replay windows and stats equal N sequential calls of the model."""
+    counters, replay windows and stats equal N sequential calls of the model.
+    With 64 KiB chunks (WG_TUNN_CHUNK_KB) a batch is far larger than one chunk per
+    engine: decapsulate then runs in rounds of 2 x 64 KiB, decided in packet order
+    across rounds and engines, with no more pinned staging than one chunk."""
+    if chunk_kb:
+        monkeypatch.setenv("WG_TUNN_CHUNK_KB", chunk_kb)
     from neptun_amd import GpuContext
     from neptun_amd.tunn import Tunn
     rng = random.Random(51)

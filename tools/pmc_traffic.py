@@ -11,7 +11,8 @@ quotes as roofline.traffic.
 
     python tools/pmc_traffic.py OUT.json [--config N] [bench args...]
 
-bench.py reads profiles/pmc_traffic_config{N}.json.
+bench.py reads profiles/pmc_traffic_config{N}.json (config 2 with --layout neptun:
+profiles/pmc_traffic_config2_neptun.json).
 """
 import csv
 import glob
@@ -44,6 +45,7 @@ def pmc_pass(counter, outdir, bench_args):
 
 def short(name):
     for tag in ("aead_strided_kernel<true, false>", "aead_strided_kernel<false, false>",
+                "aead_strided_open_text_kernel",
                 "aead_desc_sync_kernel<true>", "aead_desc_sync_kernel<false>",
                 "aead_desc_kernel<true>", "aead_desc_kernel<false>"):
         if tag in name:

@@ -17,9 +17,10 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def sample():
+def sample(gpu: int = 0):
+    """One `amd-smi metric` reading of GPU `gpu` (amd-smi's index), read-only."""
     try:
-        out = subprocess.run(["amd-smi", "metric", "-g", "0", "--json"], capture_output=True,
+        out = subprocess.run(["amd-smi", "metric", "-g", str(gpu), "--json"], capture_output=True,
                              text=True, timeout=20)
         return json.loads(out.stdout) if out.returncode == 0 else {"err": out.stderr[-300:]}
     except Exception as e:  # noqa: BLE001
