@@ -302,15 +302,18 @@ struct DescGeom {
   uint64_t in_ref, out_ref;      // src - 16, dst - 16
   uint32_t *wg_rounds;           // [waves] round counts of the workgroup's waves
   uint32_t wave, alive;          // this wave, waves of the workgroup with packets
-  // Fast addressing (per group, wave-uniform; set by set()): when the wave's
-  // packets span < 2 GiB on each side, in16 / out16 hold BYTE offsets from the
-  // wave's lowest packet (kNoAccess for packets not staged) and the rounds in
-  // [r_in0, r_in1) / [r_out0, r_out1) -- where every staged packet moves a full
-  // 128-byte run -- go through one buffer resource with 1 VALU op per piece
-  // (stage_in / stage_out overloads below) instead of per-lane 64-bit addresses.
+  // Fast addressing (per group, wave-uniform; set by set()): when every staged
+  // packet of the wave lies within +-1 GiB of the wave's first staged packet on
+  // each side, in16 / out16 hold BYTE offsets from that anchor - 1 GiB
+  // (kNoAccess for packets not staged) and every round goes through one buffer
+  // resource per side with 32-bit offsets: the rounds in [r_in0, r_in1) /
+  // [r_out0, r_out1), where every staged packet moves a full 128-byte run, with
+  // 1 VALU op per piece; the edge rounds with per-piece range masks (offset
+  // kNoAccess = no access) and owner-lane stores of each packet's partial last
+  // chunk (stage_in / stage_out overloads below).  Otherwise per-lane 64-bit
+  // addresses (the generic path).
   bool fast = false;
   uint64_t in_wave = 0, out_wave = 0;
-  uint32_t in_rec = 0, out_rec = 0;
   uint32_t r_in0 = 0, r_in1 = 0, r_out0 = 0, r_out1 = 0;
   __device__ bool live(uint32_t p, uint32_t r) const { return kRun * r < S.wlen[p]; }
   __device__ uint32_t wlen(uint32_t p) const { return S.wlen[p]; }
@@ -322,30 +325,42 @@ struct DescGeom {
     if (fast) return out_wave + S.out16[p];
     return out_ref + 16ull * (((uint64_t)S.out_hi[p] << 32) | S.out16[p]);
   }
+  // the anchor of the fast offsets: the first staged lane's origin - 1 GiB
+  __device__ static uint64_t anchor(uint64_t x, int l0) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l0);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l0);
+    const uint64_t a = ((uint64_t)hi << 32) | lo;
+    return a > (1ull << 30) ? a - (1ull << 30) : 0ull;
+  }
   // (host side: src and dst are non-null, so offsets stay below 2^44 bytes)
   template <bool kSeal>
   __device__ void set(uint32_t lane, uint64_t in_base, uint64_t out_base, uint32_t W, bool ok) {
     const uint32_t ihi = ok ? (kSeal ? W - 16u : W) : 0u;   // Ranges<kSeal>::in_hi
     const uint32_t ohi = ok ? (kSeal ? W : W - 16u) : 0u;   // Ranges<kSeal>::out_hi
-    const uint64_t imin = wave_min64(ok ? in_base : ~0ull), omin = wave_min64(ok ? out_base : ~0ull);
-    const uint64_t imax = wave_max64(ok ? in_base + ihi : 0ull);
-    const uint64_t omax = wave_max64(ok ? out_base + ohi : 0ull);
-    const uint32_t any = __builtin_amdgcn_readfirstlane(__ballot(ok) != 0ull ? 1u : 0u);
-    const uint64_t ispan = imax - imin, ospan = omax - omin;
-    fast = any && ispan + 16u < kNoAccessOffset - 1024u && ospan + 16u < kNoAccessOffset - 1024u;
+    const uint64_t live_lanes = __ballot(ok);
+    fast = live_lanes != 0ull;
     if (fast) {
-      in_wave = imin;
-      out_wave = omin;
-      in_rec = (uint32_t)((ispan + 15u) & ~15ull);
-      out_rec = (uint32_t)((ospan + 15u) & ~15ull);
-      // full-run rounds: 128 r >= lo and 128 (r + 1) <= hi for every staged packet
-      r_in0 = kSeal ? 1u : 0u;
-      r_out0 = kSeal ? 0u : 1u;
-      r_in1 = wave_min32(ok ? ihi / kRun : 0xffffffffu);
-      r_out1 = wave_min32(ok ? ohi / kRun : 0xffffffffu);
-      S.in16[lane] = ok ? (uint32_t)(in_base - imin) : kNoAccessOffset;
-      S.out16[lane] = ok ? (uint32_t)(out_base - omin) : kNoAccessOffset;
-    } else {
+      const int l0 = (int)__builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(live_lanes));
+      const uint64_t ia = anchor(in_base, l0), oa = anchor(out_base, l0);
+      const uint64_t io = in_base - ia, oo = out_base - oa;
+      // every byte a staged packet moves (its extent + a 16-byte tail chunk)
+      // stays below kNoAccess, and kNoAccess + 128 r never wraps
+      const bool far = ok && (io + ihi + 16u >= kNoAccessOffset - 1024u ||
+                              oo + ohi + 16u >= kNoAccessOffset - 1024u);
+      fast = __ballot(far) == 0ull;
+      if (fast) {
+        in_wave = ia;
+        out_wave = oa;
+        // full-run rounds: 128 r >= lo and 128 (r + 1) <= hi for every staged packet
+        r_in0 = kSeal ? 1u : 0u;
+        r_out0 = kSeal ? 0u : 1u;
+        r_in1 = wave_min32(ok ? ihi / kRun : 0xffffffffu);
+        r_out1 = wave_min32(ok ? ohi / kRun : 0xffffffffu);
+        S.in16[lane] = ok ? (uint32_t)io : kNoAccessOffset;
+        S.out16[lane] = ok ? (uint32_t)oo : kNoAccessOffset;
+      }
+    }
+    if (!fast) {
       const uint64_t i16 = (in_base - in_ref) >> 4, o16 = (out_base - out_ref) >> 4;
       S.in16[lane] = (uint32_t)i16;
       S.in_hi[lane] = (uint8_t)(i16 >> 32);
@@ -696,24 +711,40 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
   }
 }
 
-// Descriptor-batch forms (DescGeom): rounds where every staged packet of the
-// wave moves a full 128-byte run use one wave-uniform buffer resource over the
-// wave's packets (base = its lowest packet, records = its span) and the 32-bit
-// per-packet offsets from LDS -- one v_add per piece, no range checks (packets
-// not staged carry offset kNoAccess); the other rounds (the first / last ones,
-// ragged lengths) take the generic per-lane path.  The 8 offsets are read before
-// the 8 DMAs: an LDS read after a builtin LDS-DMA makes the compiler drain it.
+// Descriptor-batch forms (DescGeom, fast waves): one wave-uniform buffer
+// resource per side (base = the anchor, num_records = kNoAccess) and the 32-bit
+// per-packet offsets from LDS.  Rounds where every staged packet moves a full
+// 128-byte run: one v_add per piece, no range checks (packets not staged carry
+// offset kNoAccess).  Edge rounds (the first / last ones, ragged lengths): each
+// piece masked by its packet's range (kNoAccess = no access), full chunks only
+// on the store side, then each packet's partial last chunk stored by its owner
+// lane (dword / short / byte, masked the same way) -- no per-lane 64-bit
+// addresses and no divergent branches.  The 8 offsets are read before the 8
+// DMAs: an LDS read after a builtin LDS-DMA makes the compiler drain it.
+#ifndef WG_DESC_MASKED_EDGES
+#define WG_DESC_MASKED_EDGES 1
+#endif
 template <bool kSeal>
 __device__ __forceinline__ void stage_in(uint4 *run, const DescGeom &g, uint32_t lane, uint32_t r) {
-  if (!(g.fast && r >= g.r_in0 && r < g.r_in1)) {
+  const bool interior = r >= g.r_in0 && r < g.r_in1;
+  if (!g.fast || (!WG_DESC_MASKED_EDGES && !interior)) {
     stage_in<kSeal, DescGeom>(run, g, lane, r);
     return;
   }
   const uint32_t y = lane >> 3, k0 = 16u * ((lane & 7u) ^ swz(y)), k1 = k0 ^ 64u;
-  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in_wave, g.in_rec);
+  const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.in_wave, kNoAccessOffset);
   uint32_t off[kChunks];
+  if (interior) {
 #pragma unroll
-  for (uint32_t j = 0; j < kChunks; ++j) off[j] = g.S.in16[8u * j + y] + ((j & 1u) ? k1 : k0);
+    for (uint32_t j = 0; j < kChunks; ++j) off[j] = g.S.in16[8u * j + y] + ((j & 1u) ? k1 : k0);
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j) {
+      const uint32_t p = 8u * j + y, kb = (j & 1u) ? k1 : k0, w = kRun * r + kb;
+      const bool ok = w >= Ranges<kSeal>::in_lo() && w < Ranges<kSeal>::in_hi(g.S.wlen[p]);
+      off[j] = ok ? g.S.in16[p] + kb : kNoAccessOffset;
+    }
+  }
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, &run[64u * j], 16, off[j], kRun * r, 0, WG_LOAD_CPOL);
@@ -721,22 +752,60 @@ __device__ __forceinline__ void stage_in(uint4 *run, const DescGeom &g, uint32_t
 
 template <bool kSeal>
 __device__ __forceinline__ void stage_out(uint4 *run, const DescGeom &g, uint32_t lane, uint32_t r) {
-  if (!(g.fast && r >= g.r_out0 && r < g.r_out1)) {
+  const bool interior = r >= g.r_out0 && r < g.r_out1;
+  if (!g.fast || (!WG_DESC_MASKED_EDGES && !interior)) {
     stage_out<kSeal, DescGeom>(run, g, lane, r);
     return;
   }
   const uint32_t y = lane >> 3, k0 = 16u * ((lane & 7u) ^ swz(y)), k1 = k0 ^ 64u;
   uint32_t off[kChunks];
   uint4 v[kChunks];
+  if (interior) {
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j) {
+      off[j] = g.S.out16[8u * j + y] + ((j & 1u) ? k1 : k0);
+      v[j] = run[64u * j + lane];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kChunks; ++j) {
+      const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
+      store16(vv, g.out_wave, kNoAccessOffset, off[j], kRun * r);
+    }
+    return;
+  }
+  // edge round: whole 16-byte chunks of the output (lines partly written: the
+  // default cache policy, as the uniform kernels' unpadded edges)
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
-    off[j] = g.S.out16[8u * j + y] + ((j & 1u) ? k1 : k0);
+    const uint32_t p = 8u * j + y, kb = (j & 1u) ? k1 : k0, w = kRun * r + kb;
+    const bool ok = w >= Ranges<kSeal>::out_lo() && w + 16u <= Ranges<kSeal>::out_hi(g.S.wlen[p]);
+    off[j] = ok ? g.S.out16[p] + kb : kNoAccessOffset;
     v[j] = run[64u * j + lane];
   }
 #pragma unroll
   for (uint32_t j = 0; j < kChunks; ++j) {
     const u32x4 vv = {v[j].x, v[j].y, v[j].z, v[j].w};
-    store16(vv, g.out_wave, g.out_rec, off[j], kRun * r);
+    store16<WG_EDGE_STORE_NT != 0>(vv, g.out_wave, kNoAccessOffset, off[j], kRun * r);
+  }
+  // the packet's partial last chunk (q = hi % 16 bytes at wire offset wp), by its
+  // owner lane straight from its LDS row, when it falls in this round
+  const uint32_t W = g.S.wlen[lane];
+  const uint32_t hi = Ranges<kSeal>::out_hi(W), q = hi & 15u, wp = hi & ~15u;
+  const bool mine = W != 0u && q != 0u && (wp >> 7) == r && wp >= Ranges<kSeal>::out_lo();
+  if (__ballot(mine) != 0ull) {  // (wave-uniform)
+    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(g.out_wave, kNoAccessOffset);
+    const uint4 c = run[8u * lane + (((wp >> 4) & 7u) ^ swz(lane))];
+    const uint32_t base = mine ? g.S.out16[lane] + wp : kNoAccessOffset;
+    const uint32_t nd = q >> 2, rem = q & 3u;
+    const uint32_t last = nd == 0 ? c.x : nd == 1 ? c.y : nd == 2 ? c.z : c.w;
+    __builtin_amdgcn_raw_buffer_store_b32(c.x, rs, q >= 4u ? base : kNoAccessOffset, 0, WG_PARTIAL_STORE_CPOL);
+    __builtin_amdgcn_raw_buffer_store_b32(c.y, rs, q >= 8u ? base + 4u : kNoAccessOffset, 0, WG_PARTIAL_STORE_CPOL);
+    __builtin_amdgcn_raw_buffer_store_b32(c.z, rs, q >= 12u ? base + 8u : kNoAccessOffset, 0, WG_PARTIAL_STORE_CPOL);
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)last, rs, rem >= 2u ? base + 4u * nd : kNoAccessOffset,
+                                          0, WG_PARTIAL_STORE_CPOL);
+    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(last >> (8u * (rem & 2u))), rs,
+                                         (rem & 1u) ? base + 4u * nd + (rem & 2u) : kNoAccessOffset, 0,
+                                         WG_PARTIAL_STORE_CPOL);
   }
 }
 

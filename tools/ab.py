@@ -118,7 +118,8 @@ def main():
         return main_desc(paths, int(os.environ["AB_CONFIG"]))
     n, P, S = 1 << 20, int(os.environ.get("AB_SIZE", 1350)), 0
     oo = int(os.environ.get("AB_OPEN_OFF", 16))  # open's plaintext offset in its output slot
-    S = synth.round_up(P + 32, 128)
+    wo = int(os.environ.get("AB_WIRE_OFF", 0))   # seal's datagram offset in its wire slot
+    S = int(os.environ.get("AB_STRIDE", 0)) or synth.round_up(P + 32, 128)
     rounds = int(os.environ.get("AB_ROUNDS", 15))
     dev = torch.device("cuda", 0)
     pt = synth.device_payloads(n, P, S, dev, offset=16)
@@ -139,11 +140,11 @@ def main():
         libs.append((os.path.basename(p), L, h))
 
     def seal(L, h):
-        assert L.wg_gpu_seal_strided(h, n, P, 0, 0, pt.data_ptr() + 16, S, wire.data_ptr(), S,
+        assert L.wg_gpu_seal_strided(h, n, P, 0, 0, pt.data_ptr() + 16, S, wire.data_ptr() + wo, S,
                                      st.data_ptr(), stream) == 0
 
     def open_(L, h):
-        assert L.wg_gpu_open_strided(h, n, P + 32, 0, wire.data_ptr(), S, back.data_ptr() + oo, S,
+        assert L.wg_gpu_open_strided(h, n, P + 32, 0, wire.data_ptr() + wo, S, back.data_ptr() + oo, S,
                                      st.data_ptr(), stream) == 0
 
     ref_wire = None
@@ -152,7 +153,7 @@ def main():
         seal(L, h); open_(L, h)
         torch.cuda.synchronize()
         ok = torch.equal(back.view(n, S)[:, oo:oo + P], pt.view(n, S)[:, 16:16 + P]) and int(st.abs().sum()) == 0
-        w = wire.view(n, S)[:, :P + 32]
+        w = wire.view(n, S)[:, wo:wo + P + 32]
         if ref_wire is None:
             ref_wire = w.clone()
         same = torch.equal(w, ref_wire)

@@ -43,4 +43,11 @@ fi
 if [ -n "$PROBE_C4_BENCH" ]; then
   step bench_config4 600 python bench.py --config 4 --steps 10 --warmup 3 --sustain-seconds 6
 fi
+if [ -n "$PROBE_C4_SHAPE" ]; then  # what makes config 4 slower: footprint, per-lane keys or the kernel
+  step c2_1m 200 env AB_PAD=0 AB_OPEN_OFF=16 AB_BURST=100 AB_ROUNDS=4 python tools/ab.py "${libs[0]}"
+  step c4_1m_1peer 300 env AB_CONFIG=4 AB_PEERS=1 AB_PER_PEER=1048576 AB_BURST=40 AB_ROUNDS=5 python tools/ab.py "${libs[0]}"
+  step c4_1m_4096peers 300 env AB_CONFIG=4 AB_PEERS=4096 AB_PER_PEER=256 AB_BURST=40 AB_ROUNDS=5 python tools/ab.py "${libs[0]}"
+  step c4_16m_1peer 600 env AB_CONFIG=4 AB_PEERS=1 AB_PER_PEER=16777216 AB_BURST=3 AB_ROUNDS=4 python tools/ab.py "${libs[0]}"
+  step c2_16m 400 python bench.py --packets 16777216 --steps 5 --warmup 2 --sustain-seconds 3 --no-cpu-baseline --evp-sample 0
+fi
 echo "== done"
