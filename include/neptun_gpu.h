@@ -314,6 +314,87 @@ int wg_gpu_cookie_reply_batch(wg_gpu_ctx *ctx, const uint8_t cookie_key[32],
                               const wg_cookie_reply_job *jobs, uint8_t *out, void *stream);
 
 /*
+ * Initiator side, batched.  The reference's sequential
+ * per-peer state stays with the caller: inc_index() for each initiation, the
+ * InitSent / previous-state match of a response by its receiver index
+ * (handshake.rs:619-624, else UnexpectedPacket), and cookies.index /
+ * last_mac1 for cookie replies (:701-709, else UnexpectedPacket / WrongIndex).
+ *   wg_gpu_handshake_initiate_batch: format_handshake_initiation
+ *     (noise/handshake.rs:769-851) + append_mac1_and_mac2 (:732-765) with the
+ *     caller's random ephemeral key and TAI64N stamp: the 148-byte message and
+ *     the InitSent state (chaining key, hash; the ephemeral key stays with the
+ *     caller) and mac1 (cookies.last_mac1).
+ *   wg_gpu_handshake_receive_response_batch: receive_handshake_response
+ *     (:615-695) for n 92-byte responses (`stride` apart, stride % 4 == 0),
+ *     after the mac1 check of RateLimiter::verify_packet (rate_limiter.rs:182-195,
+ *     when check_mac1 != 0; the key is derived from static_private).  out[i]:
+ *     the session keys -- Session::new(local, peer, temp3, temp2): sending =
+ *     temp2, receiving = temp3 -- and the responder's sender index, or a status
+ *     (WRONG_PACKET_TYPE, INVALID_MAC, INVALID_AEAD_TAG; keys zeroed).
+ *     static_private (32 bytes) is HOST memory.
+ *   wg_gpu_cookie_reply_open_batch: the decryption of receive_cookie_reply
+ *     (:711-724): XChaCha20-Poly1305 open of the cookie with key
+ *     HASH(LABEL_COOKIE || responder static public), aad = last mac1.  out[i]:
+ *     the cookie (cookies.write_cookie) or WRONG_PACKET_TYPE / INVALID_AEAD_TAG.
+ * Device pointers for the arrays.
+ */
+typedef struct wg_initiation_job {
+  uint8_t ephemeral_private[32];   /* DH_GENERATE() (random, from the caller) */
+  uint8_t static_public[32];       /* NoiseParams::static_public */
+  uint8_t peer_static_public[32];
+  uint8_t static_shared[32];       /* NoiseParams::static_shared = DH(static_private, peer_static_public) */
+  uint8_t mac1_key[32];            /* sending_mac1_key = HASH(LABEL_MAC1 || peer_static_public) */
+  uint8_t cookie[16];              /* cookies.write_cookie, when has_cookie */
+  uint8_t timestamp[12];           /* TAI64N stamp: big-endian seconds then nanoseconds */
+  uint32_t local_index;            /* inc_index() */
+  uint32_t has_cookie;
+  uint8_t pad[12];
+} wg_initiation_job;               /* 208 bytes */
+
+typedef struct wg_init_sent {      /* HandshakeState::InitSent (+ the message and last mac1) */
+  uint8_t message[148];            /* HANDSHAKE_INIT incl. mac1 / mac2 */
+  uint32_t local_index;
+  uint8_t chaining_key[32];
+  uint8_t hash[32];
+  uint8_t mac1[16];                /* cookies.last_mac1 */
+} wg_init_sent;                    /* 232 bytes */
+
+typedef struct wg_response_received_job {
+  uint8_t chaining_key[32];        /* the matched InitSent state */
+  uint8_t hash[32];
+  uint8_t ephemeral_private[32];
+  uint8_t preshared_key[32];       /* zeros when the peer has none (handshake.rs:657-661) */
+} wg_response_received_job;        /* 128 bytes */
+
+typedef struct wg_session_keys {
+  int32_t status;
+  uint32_t peer_index;             /* the response's sender index */
+  uint8_t sending_key[32];         /* temp2 */
+  uint8_t receiving_key[32];       /* temp3 */
+} wg_session_keys;                 /* 72 bytes */
+
+typedef struct wg_cookie_open_job {
+  uint8_t message[64];             /* COOKIE_REPLY */
+  uint8_t cookie_key[32];          /* HASH(LABEL_COOKIE || responder static public) */
+  uint8_t mac1[16];                /* cookies.last_mac1 */
+} wg_cookie_open_job;              /* 112 bytes */
+
+typedef struct wg_cookie_open_out {
+  int32_t status;
+  uint32_t receiver_idx;           /* the reply's receiver index (the caller compares cookies.index) */
+  uint8_t cookie[16];
+} wg_cookie_open_out;              /* 24 bytes */
+
+int wg_gpu_handshake_initiate_batch(wg_gpu_ctx *ctx, uint32_t n, const wg_initiation_job *jobs,
+                                    wg_init_sent *out, void *stream);
+int wg_gpu_handshake_receive_response_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32],
+                                            uint32_t n, const uint8_t *msgs, uint64_t stride,
+                                            int check_mac1, const wg_response_received_job *jobs,
+                                            wg_session_keys *out, void *stream);
+int wg_gpu_cookie_reply_open_batch(wg_gpu_ctx *ctx, uint32_t n, const wg_cookie_open_job *jobs,
+                                   wg_cookie_open_out *out, void *stream);
+
+/*
  * Host memory registration (hipHostRegister, mapped) for copy-free batches:
  * the kernels can then address the caller's buffers directly (absolute
  * device addresses in descriptors with NULL src / dst bases, or the Tunn

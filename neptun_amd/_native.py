@@ -62,6 +62,9 @@ def load() -> ctypes.CDLL:
     L.wg_gpu_handshake_respond_batch.argtypes = [vp, u32, vp, vp, vp, vp]
     L.wg_gpu_mac2_check_batch.argtypes = [vp, c.c_char_p, u64, u32, vp, u64, vp, vp, vp, vp, vp]
     L.wg_gpu_cookie_reply_batch.argtypes = [vp, c.c_char_p, c.c_char_p, u32, vp, vp, vp]
+    L.wg_gpu_handshake_initiate_batch.argtypes = [vp, u32, vp, vp, vp]
+    L.wg_gpu_handshake_receive_response_batch.argtypes = [vp, c.c_char_p, u32, vp, u64, c.c_int, vp, vp, vp]
+    L.wg_gpu_cookie_reply_open_batch.argtypes = [vp, u32, vp, vp, vp]
     L.wg_gpu_route_set.argtypes = [vp, u32, vp, vp]
     L.wg_gpu_route_batch.argtypes = [vp, vp, u32, vp, vp]
     L.wg_gpu_pipe_create.argtypes = [vp, u64, u32, c.POINTER(vp)]

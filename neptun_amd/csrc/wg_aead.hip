@@ -991,7 +991,9 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   if constexpr (kUniform) {
     rounds = my_runs;  // uniform: job.len is a kernel argument
   } else if constexpr (kSync) {
-    g.template set<kSeal>(lane, job.in_base, job.out_base, W, my_runs != 0u);
+    uint32_t ls = lane;  // (opaque: no kernel-lifetime LDS addresses to hold and spill)
+    if constexpr (WG_OPAQUE_LANE_DESC) asm volatile("" : "+v"(ls));
+    g.template set<kSeal>(ls, job.in_base, job.out_base, W, my_runs != 0u);
     rounds = g.wg_max(wave_max(my_runs));
   } else {
     S.in_base[lane] = job.in_base;
@@ -1207,7 +1209,12 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
           hdr = make_uint4(h.x, h.y, h.z, h.w);
         }
 #if !WG_ABLATE_NO_MEM
-        stage_in<kSeal>(run, g, lane, 0);
+        // (descriptor batches: the lane opaque here as in do_round -- else the
+        // compiler computes round 0's lane-derived offsets once per kernel, holds
+        // them through every group and spills them: ~40 scratch reloads per group)
+        uint32_t ln0 = lane;
+        if constexpr (!kUniform && WG_OPAQUE_LANE_DESC) asm volatile("" : "+v"(ln0));
+        stage_in<kSeal>(run, g, ln0, 0);
 #endif
       }
       if (kSeal && !WG_ABLATE_NO_KEYBLOCK) one_time_key();  // while round 0's DMA is in flight (every wave: phase-locked)

@@ -126,8 +126,30 @@ struct CookieReplyParams {
   uint32_t n;
   uint32_t cookie_key[8], nonce_key[8];
 };
+struct HandshakeInitiateParams {
+  const wg_initiation_job *jobs;
+  wg_init_sent *out;
+  uint32_t n;
+};
+struct HandshakeResponseParams {
+  const uint8_t *msgs;  // n handshake responses, 92 bytes each at `stride`
+  uint64_t stride;
+  const wg_response_received_job *jobs;
+  wg_session_keys *out;
+  uint32_t n, check_mac1;
+  uint32_t static_private[8];  // the initiator's static key (wave-uniform)
+  uint32_t mac1_key[8];        // HASH(LABEL_MAC1 || static_public)
+};
+struct CookieOpenParams {
+  const wg_cookie_open_job *jobs;
+  wg_cookie_open_out *out;
+  uint32_t n;
+};
 __global__ void x25519_kernel(uint32_t n, const uint8_t *scalars, const uint8_t *points,
                               uint8_t *out);
+__global__ void handshake_initiate_kernel(HandshakeInitiateParams prm);
+__global__ void handshake_response_kernel(HandshakeResponseParams prm);
+__global__ void cookie_open_kernel(CookieOpenParams prm);
 __global__ void handshake_anon_kernel(HandshakeAnonParams prm);
 __global__ void handshake_consume_kernel(HandshakeConsumeParams prm);
 __global__ void handshake_respond_kernel(HandshakeRespondParams prm);

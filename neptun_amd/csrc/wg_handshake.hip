@@ -416,4 +416,211 @@ __global__ __launch_bounds__(256) void cookie_reply_kernel(CookieReplyParams prm
   st_words(prm.out + 64ull * i, m, 16);
 }
 
+// ---------------------------------------------------------------------------
+// Initiator side: format_handshake_initiation (handshake.rs:769-851)
+// + append_mac1_and_mac2 (:732-765), receive_handshake_response (:615-695) and
+// receive_cookie_reply (:697-727).  The per-peer sequential state (inc_index,
+// the InitSent / previous state match by receiver index, cookies.index /
+// last_mac1) stays with the caller; the device does the crypto.
+// ---------------------------------------------------------------------------
+// INITIAL_CHAIN_HASH = HASH(INITIAL_CHAIN_KEY || IDENTIFIER) (handshake.rs:34-39)
+__constant__ uint32_t kChainHash0[8] = {0x61b31122u, 0x66c51a08u, 0xdb431269u, 0x32d58a45u,
+                                        0x666c9c2du, 0xb7e89322u, 0x659ce10eu, 0xf39e07bau};
+
+// aead_chacha20_seal (handshake.rs:101-117) of <= 32 plaintext bytes under a
+// 32-byte AAD with nonce 0: ct = pt ^ keystream block 1, tag over AAD || ct
+__device__ __forceinline__ void seal_aad32(uint32_t ct[8], uint32_t tag[4], const uint32_t key[8],
+                                           const uint32_t aad[8], const uint32_t pt[8], uint32_t len) {
+  uint32_t ks[16];
+  chacha20_block(ks, key, 1u, 0u, 0u);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ct[j] = 4u * j < len ? pt[j] ^ ks[j] : 0u;
+  tag_aad32(tag, key, aad, ct, len);
+}
+
+__global__ __launch_bounds__(256) void handshake_initiate_kernel(HandshakeInitiateParams prm) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= prm.n) return;
+  const wg_initiation_job &job = prm.jobs[i];
+  uint32_t e[8], epub[8], pst[8], h[8], t[8], ck[8], dh[8], key[8], d[16];
+  ld_words(e, job.ephemeral_private, 8);
+  ld_words(pst, job.peer_static_public, 8);
+  uint32_t base[8], c0[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    base[j] = kBasePoint[j];
+    c0[j] = kChainHash0[j];
+  }
+  // hash = HASH(INITIAL_CHAIN_HASH || responder.static_public)
+  b2s::hash64(h, c0, pst);
+  // msg.unencrypted_ephemeral = DH_PUBKEY(ephemeral_private); hash = HASH(hash || it)
+  x25519::scalarmult(epub, e, base);
+  b2s::hash64(d, h, epub);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = d[j];
+    c0[j] = kChainKey0[j];
+  }
+  // chaining_key = HMAC(HMAC(INITIAL_CHAIN_KEY, ephemeral), 0x1)
+  hmac_32(t, c0, epub);
+  hmac_1(ck, t, 1u);
+  // temp = HMAC(ck, DH(ephemeral, responder static)); ck = HMAC(temp, 1); key = HMAC(temp, ck || 2)
+  x25519::scalarmult(dh, e, pst);
+  hmac_32(t, ck, dh);
+  hmac_1(ck, t, 1u);
+  hmac_33(key, t, ck, 2u);
+  // msg.encrypted_static = AEAD(key, 0, static_public, hash); hash = HASH(hash || it)
+  uint32_t spub[8], es[8], tag_s[4];
+  ld_words(spub, job.static_public, 8);
+  seal_aad32(es, tag_s, key, h, spub, 32u);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d[j] = j < 8 ? es[j] : (j < 12 ? tag_s[j - 8] : 0u);
+  uint32_t h2[8];
+  b2s::hash_cat(h2, h, d, 48);
+  // temp = HMAC(ck, static_shared); ck = HMAC(temp, 1); key = HMAC(temp, ck || 2)
+  uint32_t ss[8];
+  ld_words(ss, job.static_shared, 8);
+  hmac_32(t, ck, ss);
+  hmac_1(ck, t, 1u);
+  hmac_33(key, t, ck, 2u);
+  // msg.encrypted_timestamp = AEAD(key, 0, TAI64N, hash); hash = HASH(hash || it)
+  uint32_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0}, et[8], tag_t[4];
+  ld_words(ts, job.timestamp, 3);
+  seal_aad32(et, tag_t, key, h2, ts, 12u);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) d[j] = j < 3 ? et[j] : (j < 7 ? tag_t[j - 3] : 0u);
+  b2s::hash_cat(h, h2, d, 28);
+  // message: type 1 | sender (local index) | eph_pub | enc_static | enc_ts | mac1 | mac2
+  uint32_t m[37];
+  m[0] = 1u;  // HANDSHAKE_INIT
+  m[1] = job.local_index;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[2 + j] = epub[j];
+    m[10 + j] = es[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[18 + j] = tag_s[j];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) m[22 + j] = et[j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[25 + j] = tag_t[j];
+  uint32_t mk[8], mac1[4], mac2[4] = {0, 0, 0, 0};
+  ld_words(mk, job.mac1_key, 8);
+  b2s::mac16_116(mac1, mk, m);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[29 + j] = mac1[j];
+  if (job.has_cookie) {  // mac2 = MAC(cookie, msg[..mac2_off]) (132 bytes)
+    uint32_t ckey[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    ld_words(ckey, job.cookie, 4);
+    b2s::keyed_mac(mac2, 16, ckey, 16, m, 132);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[33 + j] = mac2[j];
+  wg_init_sent &o = prm.out[i];
+  st_words(o.message, m, 37);
+  o.local_index = job.local_index;
+  st_words(o.chaining_key, ck, 8);
+  st_words(o.hash, h, 8);
+  st_words(o.mac1, mac1, 4);
+}
+
+__global__ __launch_bounds__(256) void handshake_response_kernel(HandshakeResponseParams prm) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= prm.n) return;
+  uint32_t w[23];
+  ld_words(w, prm.msgs + prm.stride * i, 23);
+  const wg_response_received_job &job = prm.jobs[i];
+  wg_session_keys &o = prm.out[i];
+  int32_t status = w[0] == 2u ? WG_STATUS_OK : WG_STATUS_WRONG_PACKET_TYPE;  // HANDSHAKE_RESP
+  if (status == WG_STATUS_OK && prm.check_mac1) {  // verify_packet (rate_limiter.rs:182-195)
+    uint32_t mac[4];
+    b2s::keyed_mac(mac, 16, prm.mac1_key, 32, w, 60);
+    if ((mac[0] ^ w[15]) | (mac[1] ^ w[16]) | (mac[2] ^ w[17]) | (mac[3] ^ w[18]))
+      status = WG_STATUS_INVALID_MAC;
+  }
+  uint32_t ck[8], h[8], e[8], peph[8], t[8], dh[8], d[16];
+  ld_words(ck, job.chaining_key, 8);
+  ld_words(h, job.hash, 8);
+  ld_words(e, job.ephemeral_private, 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) peph[j] = w[3 + j];
+  // hash = HASH(hash || unencrypted_ephemeral); temp = HMAC(ck, it); ck = HMAC(temp, 1)
+  b2s::hash64(d, h, peph);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) h[j] = d[j];
+  hmac_32(t, ck, peph);
+  hmac_1(ck, t, 1u);
+  // DH(ephemeral, responder ephemeral), then DH(static, responder ephemeral)
+  x25519::scalarmult(dh, e, peph);
+  hmac_32(t, ck, dh);
+  hmac_1(ck, t, 1u);
+  x25519::scalarmult(dh, prm.static_private, peph);
+  hmac_32(t, ck, dh);
+  hmac_1(ck, t, 1u);
+  // psk (zeros when none, handshake.rs:657-661): temp2 / key / hash
+  uint32_t psk[8], temp2[8], key[8];
+  ld_words(psk, job.preshared_key, 8);
+  hmac_32(t, ck, psk);
+  hmac_1(ck, t, 1u);
+  hmac_33(temp2, t, ck, 2u);
+  hmac_33(key, t, temp2, 3u);
+  b2s::hash64(d, h, temp2);
+  // encrypted_nothing: AEAD-open of the empty plaintext (AAD = hash)
+  uint32_t tag[4], none[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  tag_aad32(tag, key, d, none, 0);
+  if (status == WG_STATUS_OK && ((tag[0] ^ w[11]) | (tag[1] ^ w[12]) | (tag[2] ^ w[13]) | (tag[3] ^ w[14])))
+    status = WG_STATUS_INVALID_AEAD_TAG;
+  // temp1 = HMAC(ck, []), temp2 = HMAC(temp1, 1), temp3 = HMAC(temp1, temp2 || 2)
+  uint32_t t1[8], t2[8], t3[8], empty[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) empty[j] = 0u;
+  b2s::hmac(t1, ck, empty, 0);
+  hmac_1(t2, t1, 1u);
+  hmac_33(t3, t1, t2, 2u);
+  const bool ok = status == WG_STATUS_OK;
+  uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  o.status = status;
+  o.peer_index = status == WG_STATUS_WRONG_PACKET_TYPE ? 0u : w[1];
+  // Session::new(local_index, peer_index, temp3, temp2): sending = temp2, receiving = temp3
+  st_words(o.sending_key, ok ? t2 : z, 8);
+  st_words(o.receiving_key, ok ? t3 : z, 8);
+}
+
+// receive_cookie_reply's decryption (handshake.rs:711-724): XChaCha20-Poly1305
+// open of the 16-byte cookie with key HASH(LABEL_COOKIE || responder static
+// public), the message's 24-byte nonce and aad = the last mac1 sent
+__global__ __launch_bounds__(256) void cookie_open_kernel(CookieOpenParams prm) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= prm.n) return;
+  const wg_cookie_open_job &job = prm.jobs[i];
+  uint32_t m[16], key[8], mac1[4], sub[8];
+  ld_words(m, job.message, 16);
+  ld_words(key, job.cookie_key, 8);
+  ld_words(mac1, job.mac1, 4);
+  // m: type 3 | receiver | nonce (6 words) | encrypted cookie (4) | tag (4)
+  int32_t status = m[0] == 3u ? WG_STATUS_OK : WG_STATUS_WRONG_PACKET_TYPE;  // COOKIE_REPLY
+  hchacha20(sub, key, m + 2);
+  uint32_t ks[16];
+  chacha20_block(ks, sub, 0u, m[6], m[7]);
+  Poly poly;
+  poly_init(poly, ks);
+  const uint32_t s[4] = {ks[4], ks[5], ks[6], ks[7]};
+  poly_block(poly, mac1[0], mac1[1], mac1[2], mac1[3]);  // AAD (16 bytes)
+  poly_block(poly, m[8], m[9], m[10], m[11]);
+  poly_block(poly, 16u, 0u, 16u, 0u);
+  uint32_t tag[4];
+  poly_finish(poly, s, tag);
+  if (status == WG_STATUS_OK && ((tag[0] ^ m[12]) | (tag[1] ^ m[13]) | (tag[2] ^ m[14]) | (tag[3] ^ m[15])))
+    status = WG_STATUS_INVALID_AEAD_TAG;
+  chacha20_block(ks, sub, 1u, m[6], m[7]);
+  uint32_t cookie[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cookie[j] = status == WG_STATUS_OK ? m[8 + j] ^ ks[j] : 0u;
+  wg_cookie_open_out &o = prm.out[i];
+  o.status = status;
+  o.receiver_idx = m[1];
+  st_words(o.cookie, cookie, 4);
+}
+
 }  // namespace wg

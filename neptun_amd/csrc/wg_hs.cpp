@@ -194,4 +194,72 @@ int wg_gpu_cookie_reply_batch(wg_gpu_ctx *ctx, const uint8_t cookie_key[32],
   return e == hipSuccess ? WG_RC_OK : wg_pipe_fail(WG_RC_HIP_ERROR, "cookie_reply_batch: launch", e);
 }
 
+int wg_gpu_handshake_initiate_batch(wg_gpu_ctx *ctx, uint32_t n, const wg_initiation_job *jobs,
+                                    wg_init_sent *out, void *stream) {
+  if (!ctx || (n && (!jobs || !out)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "handshake_initiate_batch: null argument", hipSuccess);
+  if (((uintptr_t)jobs | (uintptr_t)out) & 7u)
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "handshake_initiate_batch: 8-byte alignment required",
+                        hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  wg::HandshakeInitiateParams prm{jobs, out, n};
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::handshake_initiate_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), prm);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK
+                         : wg_pipe_fail(WG_RC_HIP_ERROR, "handshake_initiate_batch: launch", e);
+}
+
+int wg_gpu_handshake_receive_response_batch(wg_gpu_ctx *ctx, const uint8_t static_private[32],
+                                            uint32_t n, const uint8_t *msgs, uint64_t stride,
+                                            int check_mac1, const wg_response_received_job *jobs,
+                                            wg_session_keys *out, void *stream) {
+  if (!ctx || !static_private || (n && (!msgs || !jobs || !out)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "handshake_receive_response_batch: null argument",
+                        hipSuccess);
+  if (stride < 92 || (stride & 3u) || (((uintptr_t)msgs | (uintptr_t)jobs | (uintptr_t)out) & 3u))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT,
+                        "handshake_receive_response_batch: stride >= 92 and 4-byte alignment required",
+                        hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  wg::HandshakeResponseParams prm{};
+  prm.msgs = msgs;
+  prm.stride = stride;
+  prm.jobs = jobs;
+  prm.out = out;
+  prm.n = n;
+  prm.check_mac1 = check_mac1 ? 1u : 0u;
+  std::memcpy(prm.static_private, static_private, 32);
+  // mac1_key = HASH(LABEL_MAC1 || static_public) (rate_limiter.rs:67), static_public = X25519(k, 9)
+  uint32_t base[8] = {9, 0, 0, 0, 0, 0, 0, 0}, pub[8];
+  wg::x25519::scalarmult(pub, prm.static_private, base);
+  uint32_t m[16] = {0};
+  std::memcpy(m, "mac1----", 8);
+  std::memcpy(reinterpret_cast<uint8_t *>(m) + 8, pub, 32);
+  wg::b2s::hash_block(prm.mac1_key, m, 40);
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::handshake_response_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), prm);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK
+                         : wg_pipe_fail(WG_RC_HIP_ERROR, "handshake_receive_response_batch: launch", e);
+}
+
+int wg_gpu_cookie_reply_open_batch(wg_gpu_ctx *ctx, uint32_t n, const wg_cookie_open_job *jobs,
+                                   wg_cookie_open_out *out, void *stream) {
+  if (!ctx || (n && (!jobs || !out)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "cookie_reply_open_batch: null argument", hipSuccess);
+  if (((uintptr_t)jobs | (uintptr_t)out) & 7u)
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "cookie_reply_open_batch: 8-byte alignment required",
+                        hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  wg::CookieOpenParams prm{jobs, out, n};
+  DevGuard g(wg_ctx_device(ctx));
+  hipLaunchKernelGGL(wg::cookie_open_kernel, dim3((n + 255u) / 256u), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), prm);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? WG_RC_OK : wg_pipe_fail(WG_RC_HIP_ERROR, "cookie_reply_open_batch: launch", e);
+}
+
 }  // extern "C"

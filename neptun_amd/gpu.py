@@ -44,6 +44,22 @@ COOKIE_REPLY_JOB_DTYPE = np.dtype([("cookie", "u1", 16), ("mac1", "u1", 16), ("n
                                    ("receiver_idx", "<u4"), ("pad", "<u4")])
 assert (RESPONDER_PEER_DTYPE.itemsize, INIT_RECEIVED_DTYPE.itemsize, RESPONSE_JOB_DTYPE.itemsize,
         RESPONSE_OUT_DTYPE.itemsize, COOKIE_REPLY_JOB_DTYPE.itemsize) == (64, 128, 160, 176, 48)
+# initiator side (include/neptun_gpu.h)
+INITIATION_JOB_DTYPE = np.dtype([("ephemeral_private", "u1", 32), ("static_public", "u1", 32),
+                                 ("peer_static_public", "u1", 32), ("static_shared", "u1", 32),
+                                 ("mac1_key", "u1", 32), ("cookie", "u1", 16), ("timestamp", "u1", 12),
+                                 ("local_index", "<u4"), ("has_cookie", "<u4"), ("pad", "u1", 12)])
+INIT_SENT_DTYPE = np.dtype([("message", "u1", 148), ("local_index", "<u4"), ("chaining_key", "u1", 32),
+                            ("hash", "u1", 32), ("mac1", "u1", 16)])
+RESPONSE_RECEIVED_JOB_DTYPE = np.dtype([("chaining_key", "u1", 32), ("hash", "u1", 32),
+                                        ("ephemeral_private", "u1", 32), ("preshared_key", "u1", 32)])
+SESSION_KEYS_DTYPE = np.dtype([("status", "<i4"), ("peer_index", "<u4"), ("sending_key", "u1", 32),
+                               ("receiving_key", "u1", 32)])
+COOKIE_OPEN_JOB_DTYPE = np.dtype([("message", "u1", 64), ("cookie_key", "u1", 32), ("mac1", "u1", 16)])
+COOKIE_OPEN_OUT_DTYPE = np.dtype([("status", "<i4"), ("receiver_idx", "<u4"), ("cookie", "u1", 16)])
+assert (INITIATION_JOB_DTYPE.itemsize, INIT_SENT_DTYPE.itemsize, RESPONSE_RECEIVED_JOB_DTYPE.itemsize,
+        SESSION_KEYS_DTYPE.itemsize, COOKIE_OPEN_JOB_DTYPE.itemsize,
+        COOKIE_OPEN_OUT_DTYPE.itemsize) == (208, 232, 128, 72, 112, 24)
 
 STATUS = {
     0: "Ok", 1: "DestinationBufferTooSmall", 2: "IncorrectPacketLength", 3: "UnexpectedPacket",
@@ -181,6 +197,26 @@ class GpuContext:
                                                 stride, _ptr(lens), _ptr(addrs), _ptr(cookies),
                                                 _ptr(status), _stream(stream)),
               "wg_gpu_mac2_check_batch")
+
+    def handshake_initiate_batch(self, n: int, jobs, out, stream=None) -> None:
+        """format_handshake_initiation + mac1/mac2 (device): jobs INITIATION_JOB_DTYPE,
+        out INIT_SENT_DTYPE."""
+        check(self._lib.wg_gpu_handshake_initiate_batch(self._h, n, _ptr(jobs), _ptr(out), _stream(stream)),
+              "wg_gpu_handshake_initiate_batch")
+
+    def handshake_receive_response_batch(self, static_private: bytes, n: int, msgs, stride: int,
+                                         jobs, out, check_mac1: bool = True, stream=None) -> None:
+        """receive_handshake_response crypto (device): jobs RESPONSE_RECEIVED_JOB_DTYPE,
+        out SESSION_KEYS_DTYPE."""
+        check(self._lib.wg_gpu_handshake_receive_response_batch(
+            self._h, bytes(static_private), n, _ptr(msgs), stride, 1 if check_mac1 else 0, _ptr(jobs),
+            _ptr(out), _stream(stream)), "wg_gpu_handshake_receive_response_batch")
+
+    def cookie_reply_open_batch(self, n: int, jobs, out, stream=None) -> None:
+        """receive_cookie_reply's XChaCha20-Poly1305 open (device): jobs COOKIE_OPEN_JOB_DTYPE,
+        out COOKIE_OPEN_OUT_DTYPE."""
+        check(self._lib.wg_gpu_cookie_reply_open_batch(self._h, n, _ptr(jobs), _ptr(out), _stream(stream)),
+              "wg_gpu_cookie_reply_open_batch")
 
     def cookie_reply_batch(self, cookie_key: bytes, nonce_key: bytes, n: int, jobs, out,
                            stream=None) -> None:

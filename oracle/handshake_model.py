@@ -9,8 +9,10 @@ The checker for the GPU handshake kernels (neptun_amd/csrc/wg_handshake.hip):
   parse_handshake_anon        handshake.rs:367-412
   mac1 check                  rate_limiter.rs:172-195 (mac1_key = HASH(LABEL_MAC1 || pub))
   format_handshake_initiation handshake.rs:769-830 + append_mac1_and_mac2 :732-765
-                              (initiator side, used to build test messages; the
-                              ephemeral key and timestamp come from the caller)
+                              (initiator side: builds test messages and checks the
+                              device initiator; the ephemeral key and timestamp
+                              come from the caller)
+  receive_response            handshake.rs:615-695 (checks the device initiator)
 Pinned by RFC 7748's test vectors, OpenSSL's X25519 (oracle/openssl_ref.c) and the
 reference's own INITIAL_CHAIN_KEY / INITIAL_CHAIN_HASH constants (handshake.rs:29-39),
 which are BLAKE2s outputs (tests/test_handshake_cpu.py).

@@ -317,6 +317,60 @@ def test_config2_full_size_round_trip(torch_cuda, gpu):
         assert w[:P + 32].tobytes() == want
 
 
+@pytest.mark.parametrize("layout", ["slots_padded", "neptun"])
+def test_config2_full_size_bench_layouts(torch_cuda, gpu, layout):
+    """1M x 1350 B in bench.py's two config-2 layouts, full size:
+    slots_padded -- plaintext at slot+16 sealed to a separate wire buffer and opened
+      back to slot+16 with slot padding on (the headline line's layout): every
+      seal output zero-filled from byte 1382 to its slot's line end (1408), every
+      open output's 16 head bytes and bytes 1366..1407 zeroed, nothing else;
+    neptun -- seal in place (device/mod.rs:1297-1337), open into fresh slots at
+      offset 0 (device/mod.rs:1140-1148, the text grid), no padding: the bytes of
+      the open slots past the plaintext untouched.
+    Both: all statuses Ok, open(seal(x)) == x, every 1021st datagram equal to the
+    oracle's format_packet_data."""
+    torch = torch_cuda
+    n, P, S = 1 << 20, 1350, 1408
+    keys = synth.keys(1)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    pt = synth.device_payloads(n, P, S, "cuda", offset=16)
+    st_s = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    st_o = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    back = torch.full((n * S,), 0xCD, dtype=torch.uint8, device="cuda")
+    if layout == "slots_padded":
+        wire = torch.full((n * S,), 0xAB, dtype=torch.uint8, device="cuda")
+        gpu.set_slot_padding(True)
+        try:
+            gpu.seal_strided(n, P, 0, 0, pt.data_ptr() + 16, S, wire, S, st_s)
+            gpu.open_strided(n, P + 32, 0, wire, S, back.data_ptr() + 16, S, st_o)
+            torch.cuda.synchronize()
+        finally:
+            gpu.set_slot_padding(False)
+        o_off = 16
+        w2, b2 = wire.view(n, S), back.view(n, S)
+        assert bool((w2[:, P + 32:] == 0).all()), "seal: slot padding past the datagram"
+        assert bool((b2[:, :16] == 0).all()) and bool((b2[:, 16 + P:] == 0).all()), "open: slot padding"
+    else:
+        wire = pt.clone()  # the TUN buffers, sealed in place
+        gpu.seal_strided(n, P, 0, 0, wire.data_ptr() + 16, S, wire, S, st_s)
+        gpu.open_strided(n, P + 32, 0, wire, S, back, S, st_o)
+        torch.cuda.synchronize()
+        o_off = 0
+        b2 = back.view(n, S)
+        assert bool((b2[:, P:] == 0xCD).all()), "open: bytes past the plaintext written"
+        assert bool((wire.view(n, S)[:, P + 32:] == pt.view(n, S)[:, P + 32:]).all()), \
+            "in-place seal: bytes past the datagram written"
+    assert int((st_s != 0).sum()) == 0 and int((st_o != 0).sum()) == 0
+    assert torch.equal(back.view(n, S)[:, o_off:o_off + P], pt.view(n, S)[:, 16:16 + P])
+    rows = np.arange(0, n, 1021)
+    idx = torch.from_numpy(rows).cuda()
+    wire_rows = wire.view(n, S)[idx].cpu().numpy()
+    pt_rows = pt.view(n, S)[idx].cpu().numpy()
+    for r, w, p in zip(rows, wire_rows, pt_rows):
+        want = o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, int(r), p[16:16 + P].tobytes())
+        assert w[:P + 32].tobytes() == want
+
+
 # ---------------------------------------------------------------------------
 # mixed-length scheduling (BASELINE config 3) and per-peer keys (config 4)
 # ---------------------------------------------------------------------------

@@ -284,3 +284,184 @@ def test_mac2_check_rejects_non_handshake_lengths(torch_cuda, gpu):
         else:
             assert G.STATUS[int(st[i])] == "InvalidPacket", (i, ln)
             assert cookies[16 * i:16 * i + 16] == bytes(16)
+
+
+def test_initiator_handshake_on_gpu_end_to_end(torch_cuda, gpu):
+    """Initiator side: format_handshake_initiation + mac1/mac2
+    (handshake.rs:769-851, :732-765) on the device equals the oracle's initiation
+    (message, InitSent chaining key / hash, last mac1); the device responder
+    (consume + respond) answers; receive_handshake_response (:615-695) on the
+    device equals the oracle's receive_response and yields the responder's keys
+    crossed (initiator sending = responder receiving = temp2).  Damaged responses
+    fail as the reference fails them: InvalidMac (mac1 checked), InvalidAeadTag
+    (mac1 not checked), WrongPacketType."""
+    from neptun_amd import gpu as G
+    torch = torch_cuda
+    rng = random.Random(61)
+    resp_priv = rng.randbytes(32)
+    resp_pub = H.public_key(resp_priv)
+    n = 260
+    jobs = np.zeros(n, G.INITIATION_JOB_DTYPE)
+    want = []
+    for i in range(n):
+        si, ei, ts = rng.randbytes(32), rng.randbytes(32), rng.randbytes(12)
+        cookie = rng.randbytes(16) if i % 3 == 0 else None
+        idx = rng.getrandbits(32)
+        jobs[i]["ephemeral_private"] = np.frombuffer(ei, np.uint8)
+        jobs[i]["static_public"] = np.frombuffer(H.public_key(si), np.uint8)
+        jobs[i]["peer_static_public"] = np.frombuffer(resp_pub, np.uint8)
+        jobs[i]["static_shared"] = np.frombuffer(H.x25519(si, resp_pub), np.uint8)
+        jobs[i]["mac1_key"] = np.frombuffer(H.b2s_hash(H.LABEL_MAC1, resp_pub), np.uint8)
+        jobs[i]["timestamp"] = np.frombuffer(ts, np.uint8)
+        jobs[i]["local_index"] = idx
+        jobs[i]["has_cookie"] = 1 if cookie else 0
+        jobs[i]["cookie"] = np.frombuffer(cookie or bytes(16), np.uint8)
+        want.append((si, ei, idx) + H.initiation(si, resp_pub, ei, idx, ts, cookie))
+    d_j = to_dev(torch, jobs.tobytes())
+    d_o = torch.zeros(n * G.INIT_SENT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    gpu.handshake_initiate_batch(n, d_j, d_o)
+    torch.cuda.synchronize()
+    sent = d_o.cpu().numpy().view(G.INIT_SENT_DTYPE)
+    for i, (si, ei, idx, msg, ck, h) in enumerate(want):
+        assert sent[i]["message"].tobytes() == msg, i
+        assert int(sent[i]["local_index"]) == idx
+        assert sent[i]["chaining_key"].tobytes() == ck and sent[i]["hash"].tobytes() == h
+        assert sent[i]["mac1"].tobytes() == msg[116:132]
+    # the device responder answers the device initiations
+    msgs = b"".join(sent[i]["message"].tobytes() for i in range(n))
+    peers = np.zeros(n, G.RESPONDER_PEER_DTYPE)
+    for i, (si, *_rest) in enumerate(want):
+        pi = H.public_key(si)
+        peers[i]["peer_static_public"] = np.frombuffer(pi, np.uint8)
+        peers[i]["static_shared"] = np.frombuffer(H.x25519(resp_priv, pi), np.uint8)
+    d_s = torch.zeros(n * G.INIT_RECEIVED_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    gpu.handshake_consume_batch(resp_priv, n, to_dev(torch, msgs), 148, to_dev(torch, peers.tobytes()), d_s)
+    rjobs = np.zeros(n, G.RESPONSE_JOB_DTYPE)
+    psks = []
+    for i, (si, *_rest) in enumerate(want):
+        psk = rng.randbytes(32) if i % 4 == 1 else bytes(32)
+        psks.append(psk)
+        rjobs[i]["ephemeral_private"] = np.frombuffer(rng.randbytes(32), np.uint8)
+        rjobs[i]["peer_static_public"] = peers[i]["peer_static_public"]
+        rjobs[i]["preshared_key"] = np.frombuffer(psk, np.uint8)
+        rjobs[i]["mac1_key"] = np.frombuffer(H.b2s_hash(H.LABEL_MAC1, H.public_key(si)), np.uint8)
+        rjobs[i]["local_index"] = 0x0A000000 + i
+    d_r = torch.zeros(n * G.RESPONSE_OUT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    gpu.handshake_respond_batch(n, d_s, to_dev(torch, rjobs.tobytes()), d_r)
+    torch.cuda.synchronize()
+    resp = d_r.cpu().numpy().view(G.RESPONSE_OUT_DTYPE)
+    assert (d_s.cpu().numpy().view(G.INIT_RECEIVED_DTYPE)["status"] == 0).all()
+    # damage some responses: mac1-checked batch sees InvalidMac, unchecked InvalidAeadTag
+    rmsgs, kind = [], []
+    for i in range(n):
+        m = bytearray(resp[i]["message"].tobytes())
+        r = i % 10
+        if r == 7:
+            m[rng.randrange(44, 60)] ^= 0x20   # encrypted nothing (its tag)
+            kind.append("tag")
+        elif r == 8:
+            m[0] = 1
+            kind.append("type")
+        else:
+            kind.append("ok")
+        rmsgs.append(bytes(m))
+    stride = 96
+    d_m = to_dev(torch, b"".join(m + bytes(stride - 92) for m in rmsgs))
+    ijobs = np.zeros(n, G.RESPONSE_RECEIVED_JOB_DTYPE)
+    for i, (si, ei, idx, msg, ck, h) in enumerate(want):
+        ijobs[i]["chaining_key"] = np.frombuffer(ck, np.uint8)
+        ijobs[i]["hash"] = np.frombuffer(h, np.uint8)
+        ijobs[i]["ephemeral_private"] = np.frombuffer(ei, np.uint8)
+        ijobs[i]["preshared_key"] = np.frombuffer(psks[i], np.uint8)
+    d_ij = to_dev(torch, ijobs.tobytes())
+    for check_mac1 in (True, False):
+        out = torch.zeros(n * G.SESSION_KEYS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        res = np.zeros(n, G.SESSION_KEYS_DTYPE)
+        # the initiator's static key is one per call (wave-uniform) and every
+        # initiation above has its own: one single-entry call each for a sample,
+        # plus one whole-batch call with the first initiator's key below
+        for i in range(0, n, 13):
+            si = want[i][0]
+            o1 = torch.zeros(G.SESSION_KEYS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+            gpu.handshake_receive_response_batch(si, 1, d_m[stride * i:], stride,
+                                                 d_ij[G.RESPONSE_RECEIVED_JOB_DTYPE.itemsize * i:], o1,
+                                                 check_mac1=check_mac1)
+            torch.cuda.synchronize()
+            res[i] = o1.cpu().numpy().view(G.SESSION_KEYS_DTYPE)[0]
+        for i in range(0, n, 13):
+            si, ei, idx, msg, ck, h = want[i]
+            st = int(res[i]["status"])
+            if kind[i] == "type":
+                assert st == H.WRONG_PACKET_TYPE, i
+                continue
+            if kind[i] == "tag":
+                assert st == (H.INVALID_MAC if check_mac1 else H.INVALID_AEAD_TAG), (i, st)
+                continue
+            exp = H.receive_response(ck, h, ei, si, rmsgs[i], psks[i])
+            assert st == exp[0] == 0, (i, st)
+            assert int(res[i]["peer_index"]) == 0x0A000000 + i
+            assert res[i]["sending_key"].tobytes() == exp[1] == resp[i]["receiving_key"].tobytes()
+            assert res[i]["receiving_key"].tobytes() == exp[2] == resp[i]["sending_key"].tobytes()
+        # whole batch under initiator 0's key: only entry 0 (and any other entry of
+        # that key) derives the right keys; the rest fail their AEAD tag
+        gpu.handshake_receive_response_batch(want[0][0], n, d_m, stride, d_ij, out, check_mac1=False)
+        torch.cuda.synchronize()
+        allres = out.cpu().numpy().view(G.SESSION_KEYS_DTYPE)
+        assert int(allres[0]["status"]) == 0
+        assert all(int(allres[i]["status"]) in (H.INVALID_AEAD_TAG, H.WRONG_PACKET_TYPE) for i in range(1, n))
+
+
+def test_cookie_reply_open_matches_oracle(torch_cuda, gpu):
+    """receive_cookie_reply (handshake.rs:697-727): the device responder's COOKIE_REPLY
+    messages (cookie_reply_batch) opened on the device give back the cookies;
+    a damaged tag or ciphertext -> InvalidAeadTag (cookie zeroed), a wrong type ->
+    WrongPacketType; the receiver index comes back for the caller's cookies.index check."""
+    from neptun_amd import gpu as G
+    torch = torch_cuda
+    rng = random.Random(67)
+    resp_pub = H.public_key(rng.randbytes(32))
+    cookie_key = H.b2s_hash(H.LABEL_COOKIE, resp_pub)
+    nonce_key = rng.randbytes(32)
+    n = 300
+    rj = np.zeros(n, G.COOKIE_REPLY_JOB_DTYPE)
+    for i in range(n):
+        rj[i]["cookie"] = np.frombuffer(rng.randbytes(16), np.uint8)
+        rj[i]["mac1"] = np.frombuffer(rng.randbytes(16), np.uint8)
+        rj[i]["nonce_ctr"] = 1000 + i
+        rj[i]["receiver_idx"] = rng.getrandbits(32)
+    d_o = torch.zeros(64 * n, dtype=torch.uint8, device="cuda")
+    gpu.cookie_reply_batch(cookie_key, nonce_key, n, to_dev(torch, rj.tobytes()), d_o)
+    torch.cuda.synchronize()
+    replies = d_o.cpu().numpy().tobytes()
+    oj = np.zeros(n, G.COOKIE_OPEN_JOB_DTYPE)
+    kinds = []
+    for i in range(n):
+        m = bytearray(replies[64 * i:64 * i + 64])
+        assert bytes(m) == H.format_cookie_reply(cookie_key, int(rj[i]["receiver_idx"]), rj[i]["cookie"].tobytes(),
+                                                 rj[i]["mac1"].tobytes(), H.cookie_nonce(nonce_key, 1000 + i))
+        k = i % 8
+        if k == 5:
+            m[rng.randrange(32, 64)] ^= 4
+        elif k == 6:
+            m[0] = 2
+        kinds.append(k)
+        oj[i]["message"] = np.frombuffer(bytes(m), np.uint8)
+        oj[i]["cookie_key"] = np.frombuffer(cookie_key, np.uint8)
+        mac1 = rj[i]["mac1"].tobytes() if k != 7 else rng.randbytes(16)  # wrong AAD
+        oj[i]["mac1"] = np.frombuffer(mac1, np.uint8)
+    d_res = torch.zeros(n * G.COOKIE_OPEN_OUT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    gpu.cookie_reply_open_batch(n, to_dev(torch, oj.tobytes()), d_res)
+    torch.cuda.synchronize()
+    res = d_res.cpu().numpy().view(G.COOKIE_OPEN_OUT_DTYPE)
+    for i in range(n):
+        st, k = int(res[i]["status"]), kinds[i]
+        assert int(res[i]["receiver_idx"]) == (int(rj[i]["receiver_idx"]) if k != 6 else
+                                                int.from_bytes(oj[i]["message"][4:8].tobytes(), "little"))
+        if k == 6:
+            assert st == H.WRONG_PACKET_TYPE
+        elif k in (5, 7):
+            assert st == H.INVALID_AEAD_TAG and res[i]["cookie"].tobytes() == bytes(16), i
+        else:
+            m = oj[i]["message"].tobytes()
+            want = H.xchacha20poly1305_open(cookie_key, m[8:32], rj[i]["mac1"].tobytes(), m[32:])
+            assert st == 0 and res[i]["cookie"].tobytes() == want == rj[i]["cookie"].tobytes(), i

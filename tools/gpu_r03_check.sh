@@ -40,4 +40,9 @@ if [ -n "$CHECK_DESC" ]; then  # descriptor-kernel variants ($CHECK_DESC), confi
   step desc_config4 400 env AB_CONFIG=4 AB_PER_PEER=1024 AB_BURST=6 AB_ROUNDS=6 python tools/ab.py "${libs[@]}"
   step desc_config3 400 env AB_CONFIG=3 AB_BURST=6 AB_ROUNDS=6 python tools/ab.py "${libs[@]}"
 fi
+if [ -n "$CHECK_PMC" ]; then  # HBM traffic of the descriptor configs with the current build
+  for c in $CHECK_PMC; do
+    step pmc_traffic_config$c 500 python tools/pmc_traffic.py "$OUT/pmc_traffic_config$c.json" --config $c
+  done
+fi
 echo "== done"
