@@ -46,6 +46,8 @@ def parse(argv=None):
                          "seal in place (device/mod.rs:1297-1337), open into a fresh buffer at offset 0 "
                          "(device/mod.rs:1140-1148), no slot padding")
     ap.add_argument("--per-size", type=int, default=1 << 18, help="config 3: packets per size")
+    ap.add_argument("--mixed-sizes", default="64,256,576,1350,8900",
+                    help="config 3: the payload sizes mixed (diagnostics; BASELINE's set by default)")
     ap.add_argument("--peers", type=int, default=4096, help="config 4")
     ap.add_argument("--per-peer", type=int, default=4096, help="config 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -122,7 +124,11 @@ class StridedWorkload:
         self.kernels = {"seal": "aead_strided_kernel<true, false>",
                         "open": "aead_strided_open_text_kernel" if self.layout == "neptun"
                         else "aead_strided_kernel<false, false>"}
-        self.profile_tag = "config2_neptun" if self.layout == "neptun" else "config2"
+        # the committed PMC summaries were profiled on the default shape only
+        default_shape = n == 1 << 20 and P == 1350 and S == synth.round_up(P + 32, 128) and (
+            self.layout == "neptun" or self.pad)
+        self.profile_tag = (("config2_neptun" if self.layout == "neptun" else "config2")
+                            if default_shape else None)
 
     def _seal_src(self):
         return (self.wire if self.layout == "neptun" else self.pt).data_ptr() + 16
@@ -196,7 +202,8 @@ class DescWorkload:
         from tools import synth, workloads
         self.cfg = args.config
         if self.cfg == 3:
-            self.b = workloads.config3(args.per_size, dev, seed=synth.SEED + rank)
+            sizes = tuple(int(x) for x in args.mixed_sizes.split(","))
+            self.b = workloads.config3(args.per_size, dev, seed=synth.SEED + rank, sizes=sizes)
             nkeys = 1
         else:
             self.b = workloads.config4(args.peers, args.per_peer, args.size, dev,
@@ -215,7 +222,10 @@ class DescWorkload:
         self.launch_bytes = {"seal": int((2 * P + 32).sum()) + key_bytes,
                              "open": int((2 * P + 32).sum()) + key_bytes}
         self.kernels = {"seal": "aead_desc_sync_kernel<true>", "open": "aead_desc_sync_kernel<false>"}
-        self.profile_tag = f"config{self.cfg}"
+        default_shape = (args.per_size == 1 << 18 and args.mixed_sizes == "64,256,576,1350,8900") \
+            if self.cfg == 3 else (
+            args.peers == 4096 and args.per_peer == 4096 and args.size == 1350)
+        self.profile_tag = f"config{self.cfg}" if default_shape else None
 
     def step(self, stream, evs=None):
         b, ctx = self.b, self.ctx
@@ -249,10 +259,12 @@ class DescWorkload:
         return {int(a): int(b) for a, b in zip(u, c)}
 
     def describe(self, world):
+        import numpy as np
         b = self.b
         if self.cfg == 3:
-            w = (f"BASELINE config 3: mixed MTU {{64,256,576,1350,8900}} x {b.n // 5} each, seeded "
-                 "interleave, single session, device-side length scheduling included")
+            k = len(np.unique(b.sizes))
+            w = (f"BASELINE config 3: mixed MTU {{{','.join(str(int(x)) for x in np.unique(b.sizes))}}} x "
+                 f"{b.n // k} each, seeded interleave, single session, device-side length scheduling included")
         else:
             w = (f"BASELINE config 4: {b.n} x {int(b.sizes[0])} B packets over "
                  f"{self.ctx.key_slots} peers (per-lane key lookup from HBM)")
@@ -325,7 +337,7 @@ class PowerSampler:
             if "err" in s:
                 self.error = str(s["err"])[:120]
                 return
-            self.samples.append({"m": s})
+            self.samples.append({"t": time.time(), "m": s})
             self._stop.wait(self.period)
 
     def start(self):
@@ -429,10 +441,13 @@ def evp_check(wl, k: int) -> dict:
     return {"checked": len(smp), "mismatches": bad}
 
 
-def load_pmc(kind: str, kernel: str, tag: str) -> dict | None:
+def load_pmc(kind: str, kernel: str, tag: str | None) -> dict | None:
     """Committed rocprofv3 PMC summary of one bench kernel for this workload:
     kind "traffic" (tools/pmc_traffic.py, HBM bytes per launch) or "valu"
-    (tools/pmc_valu.py, clock + VALU instructions per wave)."""
+    (tools/pmc_valu.py, clock + VALU instructions per wave).  None when the
+    workload is not the shape those summaries were profiled on."""
+    if tag is None:
+        return None
     path = os.path.join(ROOT, "profiles", f"pmc_{kind}_{tag}.json")
     if not os.path.exists(path):
         return None
@@ -604,7 +619,7 @@ def run(args, factory=None, device_fn=None, device_count=None):
         gbps = total_payload * 8 * args.steps / elapsed / 1e9
         dom = "seal" if avg["seal"] >= avg["open"] else "open"
         achieved = wl.launch_bytes[dom] / (avg[dom] * 1e-3) / 1e9
-        tag = getattr(wl, "profile_tag", f"config{args.config}")
+        tag = getattr(wl, "profile_tag", f"config{args.config}")  # (None: non-default shape)
         tr = load_pmc("traffic", wl.kernels[dom], tag)
         pw = (sustained or {}).get("power") or {}
         live_clock = pw["gfx_clock_MHz"] / 1e3 if pw.get("gfx_clock_MHz") else None

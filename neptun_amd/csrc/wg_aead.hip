@@ -104,6 +104,13 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_SHARED_DIAG_DESC 0
 #endif
 
+#ifndef WG_DESC_UNIFORM_KEY
+#define WG_DESC_UNIFORM_KEY 0  // descriptor kernels: SGPR-key form for single-key waves
+#endif
+#ifndef WG_DESC_FULL_ROUNDS
+#define WG_DESC_FULL_ROUNDS 1  // descriptor kernels: the full-round fast path (run_wave)
+#endif
+
 #ifndef WG_HDR_NT
 #define WG_HDR_NT 0  // open's early header fetch with the streaming (nt) policy
 #endif
@@ -721,8 +728,10 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
 // lane (dword / short / byte, masked the same way) -- no per-lane 64-bit
 // addresses and no divergent branches.  The 8 offsets are read before the 8
 // DMAs: an LDS read after a builtin LDS-DMA makes the compiler drain it.
+// (measured: config 3 -1.2 %, config 4 +-0.2 % against the generic edge rounds,
+// profiles/r03_ab_desc_addressing.txt -- off by default)
 #ifndef WG_DESC_MASKED_EDGES
-#define WG_DESC_MASKED_EDGES 1
+#define WG_DESC_MASKED_EDGES 0
 #endif
 template <bool kSeal>
 __device__ __forceinline__ void stage_in(uint4 *run, const DescGeom &g, uint32_t lane, uint32_t r) {
@@ -811,7 +820,8 @@ __device__ __forceinline__ void stage_out(uint4 *run, const DescGeom &g, uint32_
 
 // One lane's chunk of ciphertext work.  m = plaintext/ciphertext byte index of
 // the chunk (wire w - 16); `ks` = its 4 keystream words.  Returns via LDS.
-template <bool kSeal>
+// kFull: the caller knows the chunk is a whole one (no tail mask)
+template <bool kSeal, bool kFull = false>
 __device__ __forceinline__ void crypt_chunk(uint4 &slot, Poly &p, int m, uint32_t P,
                                             uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 #if WG_ABLATE_NO_LDS_CRYPT
@@ -822,7 +832,7 @@ __device__ __forceinline__ void crypt_chunk(uint4 &slot, Poly &p, int m, uint32_
 #endif
   uint32_t o0 = i0 ^ a, o1 = i1 ^ b, o2 = i2 ^ c, o3 = i3 ^ d;
   const int valid = (int)P - m;
-  if (valid < 16) {  // the packet's last, partial chunk: AEAD pad16 zero-fills it
+  if (!kFull && valid < 16) {  // the packet's last, partial chunk: AEAD pad16 zero-fills it
     const uint32_t m0 = byte_mask(valid, 0), m1 = byte_mask(valid, 1), m2 = byte_mask(valid, 2),
                    m3 = byte_mask(valid, 3);
     i0 &= m0; i1 &= m1; i2 &= m2; i3 &= m3;
@@ -884,17 +894,20 @@ __device__ __forceinline__ void crypt_round(uint4 *run, uint32_t lane, uint32_t 
 // from the previous round), then chunks 1-7.
 // (text grid: chunk k of round r is text 128r + 16k -- blocks 2r + 1 and
 // 2r + 2 cover the round exactly, nothing is carried between rounds)
-template <bool kSeal, bool kText = false>
+// kFull (descriptor batches): every live packet of the wave has ciphertext
+// through the end of the round (128 r + 112 <= the wave's shortest P), so no
+// per-chunk length test and no tail mask (wave-uniform, decided per round)
+template <bool kSeal, bool kText = false, bool kFull = false>
 __device__ __forceinline__ void apply_chunk0(uint4 *run, uint32_t lane, uint32_t r, uint32_t P,
                                              Poly &p, const uint32_t ks_save[4]) {
   if constexpr (kText) return;
   const int m0 = (int)(kRun * r) - 16;
-  if (r > 0 && m0 < (int)P)
-    crypt_chunk<kSeal>(run[8u * lane + (0u ^ swz(lane))], p, m0, P, ks_save[0], ks_save[1],
-                       ks_save[2], ks_save[3]);
+  if (r > 0 && (kFull || m0 < (int)P))
+    crypt_chunk<kSeal, kFull>(run[8u * lane + (0u ^ swz(lane))], p, m0, P, ks_save[0], ks_save[1],
+                              ks_save[2], ks_save[3]);
 }
 
-template <bool kSeal, bool kText = false>
+template <bool kSeal, bool kText = false, bool kFull = false>
 __device__ __forceinline__ void apply_blocks(uint4 *run, uint32_t lane, uint32_t r, uint32_t P,
                                              const uint32_t (&ka)[16], const uint32_t (&kb)[16],
                                              Poly &p, uint32_t ks_save[4]) {
@@ -921,16 +934,16 @@ __device__ __forceinline__ void apply_blocks(uint4 *run, uint32_t lane, uint32_t
 #pragma unroll
   for (int k = 1; k <= 4; ++k) {
     const int m = m0 + 16 * k;
-    if (m < (int)P)
-      crypt_chunk<kSeal>(run[row + ((uint32_t)k ^ sw)], p, m, P, ka[4 * k - 4], ka[4 * k - 3],
-                         ka[4 * k - 2], ka[4 * k - 1]);
+    if (kFull || m < (int)P)
+      crypt_chunk<kSeal, kFull>(run[row + ((uint32_t)k ^ sw)], p, m, P, ka[4 * k - 4], ka[4 * k - 3],
+                                ka[4 * k - 2], ka[4 * k - 1]);
   }
 #pragma unroll
   for (int k = 5; k <= 7; ++k) {
     const int m = m0 + 16 * k;
-    if (m < (int)P)
-      crypt_chunk<kSeal>(run[row + ((uint32_t)k ^ sw)], p, m, P, kb[4 * k - 20], kb[4 * k - 19],
-                         kb[4 * k - 18], kb[4 * k - 17]);
+    if (kFull || m < (int)P)
+      crypt_chunk<kSeal, kFull>(run[row + ((uint32_t)k ^ sw)], p, m, P, kb[4 * k - 20], kb[4 * k - 19],
+                                kb[4 * k - 18], kb[4 * k - 17]);
   }
   ks_save[0] = kb[12]; ks_save[1] = kb[13]; ks_save[2] = kb[14]; ks_save[3] = kb[15];
 }
@@ -962,7 +975,10 @@ struct PacketJob {
 // The owner lane's side of a packet: everything but the cooperative memory
 // moves.  kUniform = every lane of the wave is live with the same length
 // (strided batches); then P, W and the round count are wave-uniform.
-template <bool kSeal, bool kUniform, bool kSync, class Stage, class Geom>
+// kUKey (descriptor batches, phase-locked): every live packet of the wave uses
+// the key slot `pre` carries, loaded once into SGPRs -- the keystream then runs
+// as for uniform batches (wave-uniform columns on the SALU, shared diagonal)
+template <bool kSeal, bool kUniform, bool kSync, bool kUKey = false, class Stage, class Geom>
 __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
                                          int32_t *status_out, const SessionKey *pre = nullptr) {
@@ -988,9 +1004,11 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   // runs covering the grid span of the datagram (text grid: without its header)
   uint32_t my_runs = job.status == WG_STATUS_OK ? (W - (16u - kG) + kRun - 1) / kRun : 0u;
   uint32_t rounds;
+  uint32_t p_min = 0u;  // descriptor batches, phase-locked: the wave's shortest live payload
   if constexpr (kUniform) {
     rounds = my_runs;  // uniform: job.len is a kernel argument
   } else if constexpr (kSync) {
+    p_min = wave_min32(my_runs ? P : 0xffffffffu);
     uint32_t ls = lane;  // (opaque: no kernel-lifetime LDS addresses to hold and spill)
     if constexpr (WG_OPAQUE_LANE_DESC) asm volatile("" : "+v"(ls));
     g.template set<kSeal>(ls, job.in_base, job.out_base, W, my_runs != 0u);
@@ -1005,7 +1023,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 
   uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t sidx = 0;
-  if (kUniform && pre) {
+  if ((kUniform || kUKey) && pre) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) key[j] = pre->k[j];
     sidx = pre->sidx;
@@ -1245,13 +1263,17 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       if (r > 0) stage_in<kSeal>(run, g, ln, r);
 #endif
       WG_STAMP_AT(kSeal, r, 1);
+      // descriptor batches: a round every live packet fills with ciphertext
+      // (wave-uniform) runs without per-chunk length tests, tail masks or tag work
+      const bool full = !kUniform && WG_DESC_FULL_ROUNDS && kRun * r + 112u <= p_min;
       auto landed = [&]() {
 #if WG_MEM_PRIO && !WG_MEM_PRIO_AT
         __builtin_amdgcn_s_setprio(WG_MEM_PRIO);
 #endif
         lds_wait_dma();
         WG_STAMP_AT(kSeal, r, 3);
-        if (!kSeal && my_runs) open_keep_tail(run, r);
+        // (no tag byte lies in a full round: the tag starts past 128 r + 128)
+        if (!kSeal && my_runs && !full) open_keep_tail(run, r);
         if (kSeal && r == 0)  // header: LE32 4 | LE32 sending_index | LE64 counter (session.rs:221-227)
           run[8u * ln + (0u ^ swz(ln))] = make_uint4(WG_MSG_DATA, sidx, n1, n2);
       };
@@ -1261,10 +1283,15 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // the keystream lives only inside this branch (kept out of phis, the
         // compiler would otherwise carry it as a register tuple and spill it)
         uint32_t ka[16], kb[16];
-        chacha20_block2_sync<WG_SHARED_DIAG && (kUniform || WG_SHARED_DIAG_DESC)>(ka, kb, key, 2u * r + 1u, n1, n2);
+        chacha20_block2_sync<WG_SHARED_DIAG && (kUniform || kUKey || WG_SHARED_DIAG_DESC)>(ka, kb, key, 2u * r + 1u, n1, n2);
         WG_STAMP_AT(kSeal, r, 2);
         landed();
-        if (my_runs) {
+        if (full) {
+          if (my_runs) {
+            apply_chunk0<kSeal, kText, true>(run, ln, r, Pr, poly, ks_save);
+            apply_blocks<kSeal, kText, true>(run, ln, r, Pr, ka, kb, poly, ks_save);
+          }
+        } else if (my_runs) {
           apply_chunk0<kSeal, kText>(run, ln, r, Pr, poly, ks_save);
           apply_blocks<kSeal, kText>(run, ln, r, Pr, ka, kb, poly, ks_save);
           if (kSeal) seal_tail(run, r);
@@ -1541,8 +1568,28 @@ __global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_s
     }
     DescGeom g{stage[wave], reinterpret_cast<uint64_t>(prm.src) - 16u,
                reinterpret_cast<uint64_t>(prm.dst) - 16u, wg_rounds, wave, alive};
-    run_wave<kSeal, false, true>(stage[wave], g, lane, job, prm.keys, prm.key_index,
-                                 i < prm.n ? prm.status + idx : nullptr);
+    int32_t *st = i < prm.n ? prm.status + idx : nullptr;
+#if WG_DESC_UNIFORM_KEY
+    // a wave whose live packets all use one key slot (single-session batches:
+    // config 3, a Tunn's batches) takes the SGPR-key form; the two forms run
+    // the same barrier sequence, so the waves of a workgroup may mix them
+    const uint64_t live = __ballot(job.status == WG_STATUS_OK);
+    if (live) {
+      const int l0 = (int)__builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(live));
+      const uint32_t us = (uint32_t)__builtin_amdgcn_readlane((int)job.slot, l0);
+      if (__ballot(job.status == WG_STATUS_OK && job.slot != us) == 0ull) {
+        SessionKey sk;
+        const uint4 a = ld16(prm.keys + 32u * us), b = ld16(prm.keys + 32u * us + 16u);
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sk.k[j] = __builtin_amdgcn_readfirstlane(w[j]);
+        sk.sidx = __builtin_amdgcn_readfirstlane(prm.key_index[us]);
+        run_wave<kSeal, false, true, true>(stage[wave], g, lane, job, prm.keys, prm.key_index, st, &sk);
+        continue;
+      }
+    }
+#endif
+    run_wave<kSeal, false, true>(stage[wave], g, lane, job, prm.keys, prm.key_index, st);
   }
 }
 

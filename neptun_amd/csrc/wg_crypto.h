@@ -96,6 +96,33 @@ __device__ __forceinline__ void hchacha20(uint32_t out[8], const uint32_t k[8], 
 #ifndef WG_CHACHA_PRIO
 #define WG_CHACHA_PRIO 3  // wave priority during the phase-locked steps (0: unchanged)
 #endif
+// One rotate of a phase-locked step: v_alignbit_b32 (x, x, SH) = rotl(x, 32 - SH);
+// with WG_STEP_PERM the byte rotations (SH 16: rotl 16, SH 24: rotl 8) are
+// v_perm_b32 byte selects whose selector sits in an SGPR operand (%SEL; VOP3
+// takes no literal on gfx950) -- the same issue cost, measured for energy.
+#ifndef WG_STEP_PERM
+#define WG_STEP_PERM 0
+#endif
+#define WG_ROT_A(R, SH) "v_alignbit_b32 %" #R ", %" #R ", %" #R ", " #SH "\n\t"
+#define WG_ROT_P(R, SEL) "v_perm_b32 %" #R ", %" #R ", %" #R ", %" #SEL "\n\t"
+#if WG_STEP_PERM
+#define WG_ROT_16(R, SEL) WG_ROT_P(R, SEL)
+#define WG_ROT_24(R, SEL) WG_ROT_P(R, SEL)
+#else
+#define WG_ROT_16(R, SEL) WG_ROT_A(R, 16)
+#define WG_ROT_24(R, SEL) WG_ROT_A(R, 24)
+#endif
+#define WG_ROT_20(R, SEL) WG_ROT_A(R, 20)
+#define WG_ROT_25(R, SEL) WG_ROT_A(R, 25)
+#define WG_ROT(R, SH, SEL) WG_ROT_##SH(R, SEL)
+// the selector operand of the byte rotations (unused by the other steps)
+constexpr uint32_t kPermRotl16 = 0x01000302u, kPermRotl8 = 0x02010003u;
+__device__ __forceinline__ uint32_t perm_sel(int sh) { return sh == 16 ? kPermRotl16 : kPermRotl8; }
+#if WG_STEP_PERM
+#define WG_PERM_SEL(SH) , "s"(perm_sel(SH))
+#else
+#define WG_PERM_SEL(SH)
+#endif
 #define WG_STEP8_ASM(SH)                                                                  \
   "v_add_u32 %0, %0, %16\n\tv_add_u32 %1, %1, %17\n\tv_add_u32 %2, %2, %18\n\t"           \
   "v_add_u32 %3, %3, %19\n\tv_add_u32 %4, %4, %20\n\tv_add_u32 %5, %5, %21\n\t"           \
@@ -103,10 +130,8 @@ __device__ __forceinline__ void hchacha20(uint32_t out[8], const uint32_t k[8], 
   "v_xor_b32 %8, %8, %0\n\tv_xor_b32 %9, %9, %1\n\tv_xor_b32 %10, %10, %2\n\t"            \
   "v_xor_b32 %11, %11, %3\n\tv_xor_b32 %12, %12, %4\n\tv_xor_b32 %13, %13, %5\n\t"        \
   "v_xor_b32 %14, %14, %6\n\tv_xor_b32 %15, %15, %7\n\t"                                  \
-  "v_alignbit_b32 %8, %8, %8, " #SH "\n\tv_alignbit_b32 %9, %9, %9, " #SH "\n\t"          \
-  "v_alignbit_b32 %10, %10, %10, " #SH "\n\tv_alignbit_b32 %11, %11, %11, " #SH "\n\t"    \
-  "v_alignbit_b32 %12, %12, %12, " #SH "\n\tv_alignbit_b32 %13, %13, %13, " #SH "\n\t"    \
-  "v_alignbit_b32 %14, %14, %14, " #SH "\n\tv_alignbit_b32 %15, %15, %15, " #SH "\n\t"    \
+  WG_ROT(8, SH, 24) WG_ROT(9, SH, 24) WG_ROT(10, SH, 24) WG_ROT(11, SH, 24)                 \
+  WG_ROT(12, SH, 24) WG_ROT(13, SH, 24) WG_ROT(14, SH, 24) WG_ROT(15, SH, 24)                 \
   "s_barrier"
 // Single-block form of the phase-locked steps (4 quarter-rounds per step:
 // 4 v_add + 4 v_xor + 4 v_alignbit + s_barrier), for the Poly1305 key block.
@@ -115,19 +140,18 @@ __device__ __forceinline__ void hchacha20(uint32_t out[8], const uint32_t k[8], 
   "v_add_u32 %3, %3, %11\n\t"                                                            \
   "v_xor_b32 %4, %4, %0\n\tv_xor_b32 %5, %5, %1\n\tv_xor_b32 %6, %6, %2\n\t"              \
   "v_xor_b32 %7, %7, %3\n\t"                                                             \
-  "v_alignbit_b32 %4, %4, %4, " #SH "\n\tv_alignbit_b32 %5, %5, %5, " #SH "\n\t"          \
-  "v_alignbit_b32 %6, %6, %6, " #SH "\n\tv_alignbit_b32 %7, %7, %7, " #SH "\n\t"          \
+  WG_ROT(4, SH, 12) WG_ROT(5, SH, 12) WG_ROT(6, SH, 12) WG_ROT(7, SH, 12)                     \
   "s_barrier"
 #define WG_COLUMN_ROUND1 \
-  asm volatile(WG_STEP4_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7)); \
-  asm volatile(WG_STEP4_ASM(20) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15)); \
-  asm volatile(WG_STEP4_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7)); \
-  asm volatile(WG_STEP4_ASM(25) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15));
+  asm volatile(WG_STEP4_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7) WG_PERM_SEL(16)); \
+  asm volatile(WG_STEP4_ASM(20) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15) WG_PERM_SEL(20)); \
+  asm volatile(WG_STEP4_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7) WG_PERM_SEL(24)); \
+  asm volatile(WG_STEP4_ASM(25) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15) WG_PERM_SEL(25));
 #define WG_DIAGONAL_ROUND1 \
-  asm volatile(WG_STEP4_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4)); \
-  asm volatile(WG_STEP4_ASM(20) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14)); \
-  asm volatile(WG_STEP4_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4)); \
-  asm volatile(WG_STEP4_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14));
+  asm volatile(WG_STEP4_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4) WG_PERM_SEL(16)); \
+  asm volatile(WG_STEP4_ASM(20) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14) WG_PERM_SEL(20)); \
+  asm volatile(WG_STEP4_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4) WG_PERM_SEL(24)); \
+  asm volatile(WG_STEP4_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14) WG_PERM_SEL(25));
 
 // Keystream block blk, phase-locked (same barrier contract as chacha20_block2_sync).
 __device__ __forceinline__ void chacha20_block_sync(uint32_t (&ks)[16], const uint32_t k[8],
@@ -160,15 +184,15 @@ __device__ __forceinline__ void chacha20_block_sync(uint32_t (&ks)[16], const ui
 // scalars, not arrays: the compiler keeps arrays that are addressed through
 // pointers in register tuples and spills them whole.
 #define WG_COLUMN_ROUND2 \
-  asm volatile(WG_STEP8_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15), "+v"(q12), "+v"(q13), "+v"(q14), "+v"(q15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7), "v"(q4), "v"(q5), "v"(q6), "v"(q7)); \
-  asm volatile(WG_STEP8_ASM(20) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(q8), "+v"(q9), "+v"(q10), "+v"(q11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15), "v"(q12), "v"(q13), "v"(q14), "v"(q15)); \
-  asm volatile(WG_STEP8_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15), "+v"(q12), "+v"(q13), "+v"(q14), "+v"(q15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7), "v"(q4), "v"(q5), "v"(q6), "v"(q7)); \
-  asm volatile(WG_STEP8_ASM(25) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(q8), "+v"(q9), "+v"(q10), "+v"(q11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15), "v"(q12), "v"(q13), "v"(q14), "v"(q15));
+  asm volatile(WG_STEP8_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15), "+v"(q12), "+v"(q13), "+v"(q14), "+v"(q15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7), "v"(q4), "v"(q5), "v"(q6), "v"(q7) WG_PERM_SEL(16)); \
+  asm volatile(WG_STEP8_ASM(20) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(q8), "+v"(q9), "+v"(q10), "+v"(q11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15), "v"(q12), "v"(q13), "v"(q14), "v"(q15) WG_PERM_SEL(20)); \
+  asm volatile(WG_STEP8_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(p15), "+v"(q12), "+v"(q13), "+v"(q14), "+v"(q15) : "v"(p4), "v"(p5), "v"(p6), "v"(p7), "v"(q4), "v"(q5), "v"(q6), "v"(q7) WG_PERM_SEL(24)); \
+  asm volatile(WG_STEP8_ASM(25) : "+v"(p8), "+v"(p9), "+v"(p10), "+v"(p11), "+v"(q8), "+v"(q9), "+v"(q10), "+v"(q11), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7) : "v"(p12), "v"(p13), "v"(p14), "v"(p15), "v"(q12), "v"(q13), "v"(q14), "v"(q15) WG_PERM_SEL(25));
 #define WG_DIAGONAL_ROUND2 \
-  asm volatile(WG_STEP8_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(q15), "+v"(q12), "+v"(q13), "+v"(q14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4), "v"(q5), "v"(q6), "v"(q7), "v"(q4)); \
-  asm volatile(WG_STEP8_ASM(20) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14)); \
-  asm volatile(WG_STEP8_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(q15), "+v"(q12), "+v"(q13), "+v"(q14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4), "v"(q5), "v"(q6), "v"(q7), "v"(q4)); \
-  asm volatile(WG_STEP8_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14));
+  asm volatile(WG_STEP8_ASM(16) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(q15), "+v"(q12), "+v"(q13), "+v"(q14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4), "v"(q5), "v"(q6), "v"(q7), "v"(q4) WG_PERM_SEL(16)); \
+  asm volatile(WG_STEP8_ASM(20) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14) WG_PERM_SEL(20)); \
+  asm volatile(WG_STEP8_ASM(24) : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(p15), "+v"(p12), "+v"(p13), "+v"(p14), "+v"(q15), "+v"(q12), "+v"(q13), "+v"(q14) : "v"(p5), "v"(p6), "v"(p7), "v"(p4), "v"(q5), "v"(q6), "v"(q7), "v"(q4) WG_PERM_SEL(24)); \
+  asm volatile(WG_STEP8_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14) WG_PERM_SEL(25));
 
 #ifndef WG_SHARED_DIAG
 #define WG_SHARED_DIAG 1  // first diagonal round with the two blocks' common words shared
@@ -272,7 +296,7 @@ __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_
         : [p5] "v"(p5), [q5] "v"(q5), [a1] "v"(a1), [p6] "v"(p6), [q6] "v"(q6), [a2] "v"(a2),
           [p7] "v"(p7), [q7] "v"(q7), [d13] "v"(d13), [p4] "v"(p4), [q4] "v"(q4));
     // step 4: the ordinary in-place step (no common words left)
-    asm volatile(WG_STEP8_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14));
+    asm volatile(WG_STEP8_ASM(25) : "+v"(p10), "+v"(p11), "+v"(p8), "+v"(p9), "+v"(q10), "+v"(q11), "+v"(q8), "+v"(q9), "+v"(p5), "+v"(p6), "+v"(p7), "+v"(p4), "+v"(q5), "+v"(q6), "+v"(q7), "+v"(q4) : "v"(p15), "v"(p12), "v"(p13), "v"(p14), "v"(q15), "v"(q12), "v"(q13), "v"(q14) WG_PERM_SEL(25));
   } else {
     WG_DIAGONAL_ROUND2
   }

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Throughput of the batched handshake kernels, one JSON line each:
-X25519 operations per second (per-lane scalar and point) and handshake initiations
-per second through mac1 + parse_handshake_anon, next to OpenSSL's X25519 on the host
+X25519 operations per second (per-lane scalar and point), handshake initiations
+per second through mac1 + parse_handshake_anon, the responder's consume / respond,
+the cookie path and the initiator's initiate / receive-response, next to OpenSSL's X25519 on the host
 cores (oracle/build/cpu_x25519, 16 threads; the reference's x25519-dalek cannot be
 built here).  Inputs are device-resident; every output of the timed run is checked
 on a sample against oracle/handshake_model.py."""
@@ -157,6 +158,60 @@ def main():
              for i in rng.sample(range(m), 16))
     print(json.dumps({"op": "cookie_reply (XChaCha20-Poly1305)", "n": m, "ms": round(t * 1e3, 3),
                       "msgs_per_s": round(m / t, 1), "verified_sample": ok}), flush=True)
+    # initiator side: format_handshake_initiation for m peers, then receive_handshake_response
+    # of the device responder's answers (one local static key, as on one interface)
+    init_priv = rng.randbytes(32)
+    init_pub = H.public_key(init_priv)
+    peer_privs = [rng.randbytes(32) for _ in range(len(base))]
+    peer_pubs = [H.public_key(k) for k in peer_privs]
+    ij = np.zeros(m, G.INITIATION_JOB_DTYPE)
+    ij["ephemeral_private"] = np.frombuffer(rng.randbytes(32 * m), np.uint8).reshape(m, 32)
+    ij["static_public"] = np.frombuffer(init_pub, np.uint8)
+    pp = np.stack([np.frombuffer(x, np.uint8) for x in peer_pubs])
+    ss = np.stack([np.frombuffer(H.x25519(init_priv, x), np.uint8) for x in peer_pubs])
+    mk = np.stack([np.frombuffer(H.b2s_hash(H.LABEL_MAC1, x), np.uint8) for x in peer_pubs])
+    reps = m // len(base)
+    ij["peer_static_public"] = np.tile(pp, (reps, 1))
+    ij["static_shared"] = np.tile(ss, (reps, 1))
+    ij["mac1_key"] = np.tile(mk, (reps, 1))
+    ij["timestamp"] = np.frombuffer(rng.randbytes(12), np.uint8)
+    ij["local_index"] = np.arange(m, dtype=np.uint32)
+    d_ij = torch.from_numpy(ij.view(np.uint8).copy()).cuda()
+    sent = torch.zeros(m * G.INIT_SENT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    t = timed(lambda: ctx.handshake_initiate_batch(m, d_ij, sent))
+    sn = sent.cpu().numpy().view(G.INIT_SENT_DTYPE)
+    ok = True
+    for i in rng.sample(range(m), 8):
+        want = H.initiation(init_priv, peer_pubs[i % len(base)], ij[i]["ephemeral_private"].tobytes(), i,
+                            ij[i]["timestamp"].tobytes())
+        ok = ok and sn[i]["message"].tobytes() == want[0] and sn[i]["hash"].tobytes() == want[2]
+    print(json.dumps({"op": "handshake_initiate (format_handshake_initiation + mac1)", "n": m,
+                      "ms": round(t * 1e3, 3), "msgs_per_s": round(m / t, 1),
+                      "verified_sample": ok}), flush=True)
+    # responses to time receive_response on: the oracle answers a tile, repeated (the
+    # kernel's work does not depend on which response it opens)
+    tile_r, rj_tile = [], np.zeros(len(base), G.RESPONSE_RECEIVED_JOB_DTYPE)
+    for i in range(len(base)):
+        _, idx, _ts, ck, h, eph = H.consume_initiation(peer_privs[i], init_pub, H.x25519(peer_privs[i], init_pub),
+                                                        sn[i]["message"].tobytes())
+        tile_r.append(H.format_response(ck, h, eph, idx, 7 + i, rng.randbytes(32), init_pub)[0])
+        rj_tile[i]["chaining_key"] = sn[i]["chaining_key"]
+        rj_tile[i]["hash"] = sn[i]["hash"]
+        rj_tile[i]["ephemeral_private"] = ij[i]["ephemeral_private"]
+    d_rm = torch.from_numpy(np.frombuffer(b"".join(tile_r) * reps, np.uint8).copy()).cuda()
+    d_rj = torch.from_numpy(np.tile(rj_tile, reps).view(np.uint8).copy()).cuda()
+    keys_out = torch.zeros(m * G.SESSION_KEYS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    t = timed(lambda: ctx.handshake_receive_response_batch(init_priv, m, d_rm, 92, d_rj, keys_out))
+    ko = keys_out.cpu().numpy().view(G.SESSION_KEYS_DTYPE)
+    ok = bool((ko["status"] == 0).all())
+    for i in rng.sample(range(m), 8):
+        j = i % len(base)
+        want = H.receive_response(sn[j]["chaining_key"].tobytes(), sn[j]["hash"].tobytes(),
+                                  ij[j]["ephemeral_private"].tobytes(), init_priv, tile_r[j])
+        ok = ok and ko[i]["sending_key"].tobytes() == want[1]
+    print(json.dumps({"op": "handshake_receive_response (mac1 + receive_handshake_response)", "n": m,
+                      "ms": round(t * 1e3, 3), "msgs_per_s": round(m / t, 1),
+                      "verified_sample": ok}), flush=True)
     exe = os.path.join(ROOT, "oracle", "build", "cpu_x25519")
     if os.path.exists(exe):
         threads = min(16, len(os.sched_getaffinity(0)))

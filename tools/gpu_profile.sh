@@ -17,6 +17,11 @@ for c in $CONFIGS; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
   python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --sustain-seconds 0 > "$OUT/trace_bench_config2.json"
+# NepTUN's own buffer layouts (seal in place, open to offset 0: the text grid)
+timeout -k 10 300 python3 bench.py --layout neptun --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench_config2_neptun.json"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_neptun" -o run -- \
+  python3 bench.py --layout neptun --steps 20 --warmup 5 --no-cpu-baseline --sustain-seconds 0 > "$OUT/trace_bench_config2_neptun.json"
+timeout -k 10 400 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_config2_neptun.json" --layout neptun > /dev/null
 for c in $CONFIGS; do
   timeout -k 10 400 python3 tools/pmc_traffic.py "$OUT/pmc_traffic_config$c.json" --config "$c" > /dev/null
   timeout -k 10 400 python3 tools/pmc_valu.py "$OUT/pmc_valu_config$c.json" --config "$c" > /dev/null

@@ -43,10 +43,31 @@ def summarize(samples):
     if not busy:
         return {"busy_samples": 0}
     n = len(busy)
-    return {"busy_samples": n, "socket_power_W": round(sum(r[0] for r in busy) / n, 1),
-            "gfx_clock_MHz": round(sum(r[1] for r in busy) / n, 1),
-            "umc_activity_pct": round(sum(r[3] for r in busy) / n, 1),
-            "ppt_violation": sorted({str(r[4]) for r in busy})}
+    out = {"busy_samples": n, "socket_power_W": round(sum(r[0] for r in busy) / n, 1),
+           "gfx_clock_MHz": round(sum(r[1] for r in busy) / n, 1),
+           "umc_activity_pct": round(sum(r[3] for r in busy) / n, 1),
+           "ppt_violation": sorted({str(r[4]) for r in busy})}
+    # the package's energy accumulator between the first and the last busy sample:
+    # mean power over that window (not a few instantaneous readings), and the
+    # share of it the PPT controller was throttling
+    acc = []
+    for s in samples:
+        try:
+            g = s["m"]["gpu_data"][0]
+            if g["usage"]["gfx_activity"]["value"] < 90 or "t" not in s:
+                continue
+            th = g.get("throttle", {})
+            acc.append((s["t"], float(g["energy"]["total_energy_consumption"]["value"]),
+                        th.get("ppt_accumulated"), th.get("accumulation_counter")))
+        except (KeyError, IndexError, TypeError, ValueError):
+            continue
+    if len(acc) >= 2 and acc[-1][0] > acc[0][0]:
+        (t0, e0, p0, c0), (t1, e1, p1, c1) = acc[0], acc[-1]
+        out["energy_window_s"] = round(t1 - t0, 3)
+        out["socket_power_from_energy_W"] = round((e1 - e0) / (t1 - t0), 1)
+        if isinstance(p0, (int, float)) and isinstance(c1, (int, float)) and c1 > c0:
+            out["ppt_throttled_fraction"] = round((p1 - p0) / (c1 - c0), 3)
+    return out
 
 
 def main():
@@ -63,7 +84,7 @@ def main():
     t0 = time.time()
     while child.poll() is None:
         s = sample()
-        samples.append({"t": round(time.time() - t0, 2), "m": s})
+        samples.append({"t": round(time.time() - t0, 3), "m": s})
         time.sleep(0.1)
     lines = child.stdout.read().strip().splitlines()
     try:

@@ -85,10 +85,10 @@ class DescBatch:
         return out
 
 
-def config3(per_size: int, device, seed: int = synth.SEED) -> DescBatch:
+def config3(per_size: int, device, seed: int = synth.SEED, sizes=MIXED_SIZES) -> DescBatch:
     """{64,256,576,1350,8900} x per_size, seeded interleave, one session (counters 0..n-1)."""
     rng = np.random.default_rng(seed)
-    sizes = np.repeat(np.array(MIXED_SIZES, np.uint32), per_size)
+    sizes = np.repeat(np.array(sizes, np.uint32), per_size)
     sizes = sizes[rng.permutation(len(sizes))]
     n = len(sizes)
     return DescBatch(sizes, np.arange(n, dtype=np.uint64), np.zeros(n, np.uint32), device, seed)
