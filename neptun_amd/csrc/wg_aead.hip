@@ -104,11 +104,18 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_SHARED_DIAG_DESC 0
 #endif
 
+// descriptor kernels: the SGPR-key form for waves whose live packets share one
+// key slot.  Measured -0.5 % on config 3 (its only single-key config) and -0.3 %
+// on config 4: off (profiles/r03_ab_desc_forms.txt)
 #ifndef WG_DESC_UNIFORM_KEY
-#define WG_DESC_UNIFORM_KEY 0  // descriptor kernels: SGPR-key form for single-key waves
+#define WG_DESC_UNIFORM_KEY 0
 #endif
+// descriptor kernels: the full-round fast path (run_wave).  Measured +0.3 % on
+// config 4 and +0.1 % on config 3 (noise level), but its register pressure spills
+// 6-7 VGPRs per group (+1.5 % config-4 HBM traffic): off
+// (profiles/r03_ab_desc_forms.txt)
 #ifndef WG_DESC_FULL_ROUNDS
-#define WG_DESC_FULL_ROUNDS 1  // descriptor kernels: the full-round fast path (run_wave)
+#define WG_DESC_FULL_ROUNDS 0
 #endif
 
 #ifndef WG_HDR_NT
@@ -1097,8 +1104,15 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   // other half read as zero) and the parts are OR-ed together.
   // With an LDS tag slot (uniform stage) the parts go there instead of
   // registers: 4 fewer VGPRs through every round measured +3 % on open.
+  // (descriptor batches: the lane made opaque in the tail helpers too -- else its
+  // row / swizzle are computed once per kernel, held, and spilled)
+  auto tail_lane = [&]() {
+    uint32_t l = lane;
+    if constexpr (!kUniform && WG_OPAQUE_LANE_DESC) asm volatile("" : "+v"(l));
+    return l;
+  };
   auto open_keep_tail = [&](uint4 *run, uint32_t r) {
-    const uint32_t row = 8u * lane, sw = swz(lane);
+    const uint32_t tl = tail_lane(), row = 8u * tl, sw = swz(tl);
     const uint32_t ra = wt >> 7, rb = (wt + 16u) >> 7;
     uint32_t t[4] = {0u, 0u, 0u, 0u};
     if (ra == r) {
@@ -1127,7 +1141,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   };
   // seal: place the tag (and the tag bytes that spill into the next round)
   auto seal_tail = [&](uint4 *run, uint32_t r) {
-    const uint32_t row = 8u * lane, sw = swz(lane);
+    const uint32_t tl = tail_lane(), row = 8u * tl, sw = swz(tl);
     if (r > 0 && ((wt + 16u) >> 7) == r && (wt >> 7) == r - 1u && q) {
       // tag remainder spilled into this round's first chunk
       run[row + (0u ^ sw)] = make_uint4(tailB[0], tailB[1], tailB[2], tailB[3]);
@@ -1136,7 +1150,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       // all ciphertext is MACed: LE64(aad_len=0) | LE64(ct_len), then the tag
       poly_block(poly, 0u, 0u, P, 0u);
       uint32_t tag[4];
-      const uint4 sp = S.park[lane];
+      const uint4 sp = S.park[tl];
       const uint32_t s[4] = {sp.x, sp.y, sp.z, sp.w};
       poly_finish(poly, s, tag);
       const uint32_t ka = (wt >> 4) & 7u;

@@ -888,3 +888,84 @@ def test_one_context_from_two_threads(torch_cuda, gpu):
             row = pt.view(n, S)[i, 16:16 + P].cpu().numpy().tobytes()
             want = o.format_packet_data(keys[t].tobytes(), int(idx[t]), 1000 * t + i, row)
             assert wire.view(n, S)[i, :P + 32].cpu().numpy().tobytes() == want
+
+
+def test_descriptor_wave_shapes_match_oracle(torch_cuda, gpu):
+    """The descriptor kernels' wave-level forms -- waves whose live packets share one
+    key slot (the SGPR-key form when built with WG_DESC_UNIFORM_KEY) or not, rounds
+    every live packet fills (the full-round form) and rounds near that boundary
+    (P = 128 r + 112 +- 1), waves with failed lanes (bad key slot, misaligned) beside
+    live ones -- sealed and opened bit-exact against the oracle, with tampered
+    datagrams rejected and zeroed."""
+    torch = torch_cuda
+    rng = np.random.default_rng(97)
+    n_keys = 16
+    keys = rng.integers(0, 256, (n_keys, 32), dtype=np.uint8)
+    kidx = rng.integers(0, 2**32, n_keys, dtype=np.uint64).astype(np.uint32)
+    gpu.set_keys(0, keys, kidx)
+    waves = 24  # 3 workgroups of 8 waves
+    n = 64 * waves
+    sizes = np.zeros(n, np.int64)
+    slots = np.zeros(n, np.uint32)
+    bound = [111, 112, 113, 239, 240, 241, 367, 368, 369, 1391, 1392, 1393]
+    for w in range(waves):
+        lo, kind = 64 * w, w % 4
+        if kind == 0:      # one key, one length
+            sizes[lo:lo + 64], slots[lo:lo + 64] = 1350, w % n_keys
+        elif kind == 1:    # one key, lengths around the full-round boundaries
+            sizes[lo:lo + 64] = rng.choice(bound, 64)
+            slots[lo:lo + 64] = (w * 7) % n_keys
+        elif kind == 2:    # mixed keys, long packets plus one empty and one tiny one
+            sizes[lo:lo + 64] = rng.choice([1350, 8900, 2000], 64)
+            sizes[lo + 5], sizes[lo + 40] = 0, 16
+            slots[lo:lo + 64] = rng.integers(0, n_keys, 64)
+        else:              # one key, but some lanes fail before the crypto
+            sizes[lo:lo + 64] = rng.integers(0, 3000, 64)
+            slots[lo:lo + 64] = 3
+    payloads = synth.host_payloads(sizes, seed=98)
+    src, soffs = pack(payloads)
+    doffs, pos = [], 0
+    for s in sizes:
+        doffs.append(pos)
+        pos = synth.round_up(pos + int(s) + 32, 16)
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = soffs
+    descs["dst_off"] = doffs
+    descs["counter"] = rng.integers(0, 2**62, n, dtype=np.uint64)
+    descs["len"] = sizes
+    descs["key_slot"] = slots
+    bad_slot = [64 * 3 + 2, 64 * 7 + 63, 64 * 11]
+    misaligned = [64 * 3 + 9, 64 * 15 + 1]
+    descs["key_slot"][bad_slot] = gpu.key_slots + 5  # past the context's key table
+    descs["src_off"][misaligned] += 4
+    valid = np.ones(n, bool)
+    valid[bad_slot + misaligned] = False
+    out, st = run_desc(torch, gpu, True, descs, src, pos + 64)
+    assert (st[bad_slot] == 101).all() and (st[misaligned] == 100).all()
+    want = np.zeros(pos + 64, np.uint8)
+    wst = o.seal_batch(descs[valid], keys, kidx, src, want)
+    assert (wst == 0).all() and (st[valid] == 0).all()
+    assert np.array_equal(out, want), "sealed bytes differ from the oracle"
+    # open the valid datagrams back, a few of them tampered
+    vi = np.nonzero(valid)[0]
+    d2 = np.zeros(len(vi), DESC)
+    d2["src_off"] = np.array(doffs)[vi]
+    d2["dst_off"] = np.array(soffs)[vi]
+    d2["len"] = sizes[vi] + 32
+    d2["key_slot"] = slots[vi]
+    wire = out.copy()
+    tampered = rng.choice(len(vi), 12, replace=False)
+    for t in tampered:
+        L = int(sizes[vi[t]]) + 32
+        wire[int(d2["src_off"][t]) + int(rng.integers(16, L))] ^= 0x40
+    back, st2 = run_desc(torch, gpu, False, d2, wire, len(src))
+    want2 = np.zeros(len(src), np.uint8)
+    wst2 = o.open_batch(d2, keys, kidx, wire, want2)
+    assert (st2 == wst2).all(), (st2[tampered], wst2[tampered])
+    assert (st2[tampered] == 10).all()
+    for t in range(len(vi)):  # plaintext bytes (tampered ones zeroed, like ring)
+        a, P = int(d2["dst_off"][t]), int(sizes[vi[t]])
+        if t in set(tampered.tolist()):
+            assert not back[a:a + P].any()
+        else:
+            assert np.array_equal(back[a:a + P], want2[a:a + P]) and np.array_equal(back[a:a + P], src[a:a + P])
