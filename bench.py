@@ -221,7 +221,11 @@ class DescWorkload:
         key_bytes = 32 * b.n if self.cfg == 4 else 0  # per-lane key reads
         self.launch_bytes = {"seal": int((2 * P + 32).sum()) + key_bytes,
                              "open": int((2 * P + 32).sum()) + key_bytes}
-        self.kernels = {"seal": "aead_desc_sync_kernel<true>", "open": "aead_desc_sync_kernel<false>"}
+        # config 3 runs the plan's ordered launches; config 4's unordered ones go to
+        # the affine-capable kernel (wg_gpu.cpp, WG_DESC_AFFINE)
+        # (config 3's context has one key slot: the SGPR-key form)
+        k = "aead_desc_sync_key1_kernel" if self.cfg == 3 else "aead_desc_affine_kernel"
+        self.kernels = {"seal": f"{k}<true>", "open": f"{k}<false>"}
         default_shape = (args.per_size == 1 << 18 and args.mixed_sizes == "64,256,576,1350,8900") \
             if self.cfg == 3 else (
             args.peers == 4096 and args.per_peer == 4096 and args.size == 1350)

@@ -235,6 +235,11 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
   return x;
 }
 
+__device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
@@ -737,6 +742,11 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
 // DMAs: an LDS read after a builtin LDS-DMA makes the compiler drain it.
 // (measured: config 3 -1.2 %, config 4 +-0.2 % against the generic edge rounds,
 // profiles/r03_ab_desc_addressing.txt -- off by default)
+// aead_desc_affine_kernel (WG_DESC_AFFINE, wg_aead_kernels.h): the shared first
+// diagonal round with the affine groups' per-lane keys
+#ifndef WG_AFFINE_SHARED_DIAG
+#define WG_AFFINE_SHARED_DIAG 0
+#endif
 #ifndef WG_DESC_MASKED_EDGES
 #define WG_DESC_MASKED_EDGES 0
 #endif
@@ -985,13 +995,20 @@ struct PacketJob {
 // kUKey (descriptor batches, phase-locked): every live packet of the wave uses
 // the key slot `pre` carries, loaded once into SGPRs -- the keystream then runs
 // as for uniform batches (wave-uniform columns on the SALU, shared diagonal)
-template <bool kSeal, bool kUniform, bool kSync, bool kUKey = false, class Stage, class Geom>
+// kLaneKeys (uniform geometry, descriptor batches): a key per packet in VGPRs
+// (pre unused) -- the keystream keeps the in-place first diagonal round.
+// kInDesc: uniform geometry inside a descriptor kernel (the affine groups).
+template <bool kSeal, bool kUniform, bool kSync, bool kUKey = false, bool kLaneKeys = false,
+          bool kInDesc = false, class Stage, class Geom>
 __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
                                          int32_t *status_out, const SessionKey *pre = nullptr) {
   // run grid (Ranges): kG = grid coordinate of text byte 0
   constexpr bool kText = Geom::kTextGrid;
   constexpr uint32_t kG = kText ? 0u : 16u;
+  // the descriptor kernel's forms: the lane made opaque where its derived
+  // offsets would otherwise be hoisted across groups and spilled
+  constexpr bool kOpaqueDesc = (!kUniform || kLaneKeys || kInDesc) && WG_OPAQUE_LANE_DESC;
   static_assert(!kText || (kSync && kUniform && !kSeal), "text grid: uniform phase-locked open only");
   // phase-locked: every wave of the workgroup runs the same number of rounds
   // (uniform batches by construction, descriptor batches via DescGeom::wg_max)
@@ -1030,7 +1047,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 
   uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t sidx = 0;
-  if ((kUniform || kUKey) && pre) {
+  if ((kUniform || kUKey) && !kLaneKeys && pre) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) key[j] = pre->k[j];
     sidx = pre->sidx;
@@ -1108,7 +1125,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   // row / swizzle are computed once per kernel, held, and spilled)
   auto tail_lane = [&]() {
     uint32_t l = lane;
-    if constexpr (!kUniform && WG_OPAQUE_LANE_DESC) asm volatile("" : "+v"(l));
+    if constexpr (kOpaqueDesc) asm volatile("" : "+v"(l));
     return l;
   };
   auto open_keep_tail = [&](uint4 *run, uint32_t r) {
@@ -1245,7 +1262,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // compiler computes round 0's lane-derived offsets once per kernel, holds
         // them through every group and spills them: ~40 scratch reloads per group)
         uint32_t ln0 = lane;
-        if constexpr (!kUniform && WG_OPAQUE_LANE_DESC) asm volatile("" : "+v"(ln0));
+        if constexpr (kOpaqueDesc) asm volatile("" : "+v"(ln0));
         stage_in<kSeal>(run, g, ln0, 0);
 #endif
       }
@@ -1270,6 +1287,10 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       if constexpr (!kUniform) {
         asm volatile("" : "+v"(ln));
         asm volatile("" : "+v"(Pr));
+      } else if constexpr (kLaneKeys || kInDesc) {
+        asm volatile("" : "+v"(ln));
+        Pr = __builtin_amdgcn_readfirstlane(P);
+        asm volatile("" : "+s"(Pr));
       }
 #endif
       WG_STAMP_AT(kSeal, r, 0);
@@ -1297,7 +1318,8 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // the keystream lives only inside this branch (kept out of phis, the
         // compiler would otherwise carry it as a register tuple and spill it)
         uint32_t ka[16], kb[16];
-        chacha20_block2_sync<WG_SHARED_DIAG && (kUniform || kUKey || WG_SHARED_DIAG_DESC)>(ka, kb, key, 2u * r + 1u, n1, n2);
+        chacha20_block2_sync<WG_SHARED_DIAG && ((kUniform && (!kLaneKeys || WG_AFFINE_SHARED_DIAG)) ||
+                                                kUKey || WG_SHARED_DIAG_DESC)>(ka, kb, key, 2u * r + 1u, n1, n2);
         WG_STAMP_AT(kSeal, r, 2);
         landed();
         if (full) {
@@ -1541,15 +1563,41 @@ __global__ __launch_bounds__(kBlockThreads, WG_WAVES_PER_SIMD) void aead_desc_ke
 // workgroups like the strided kernel; each group of 512 descriptors runs the
 // workgroup's longest packet's rounds (the length-sorted plan,
 // wg_gpu_plan_batch, keeps a group's packets alike).
-template <bool kSeal>
-__global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_sync_kernel(
-    DescParams prm) {
+// kAffine (aead_desc_affine_kernel, unordered launches): workgroups whose packets
+// are affine take the uniform geometry (below).  A separate kernel, so that the
+// ordered launches of mixed batches (whose groups gather packets from all over
+// the batch and are never affine) keep the plain form's register allocation.
+// kOneKey (the *_key1 kernels, contexts with one key slot -- a single session,
+// BASELINE config 3): the key is loaded once per kernel into SGPRs as in the
+// strided kernels, and every group runs the SGPR-key forms (wave-uniform first
+// column on the SALU, shared first diagonal round).  Packets naming any other
+// slot fail with BAD_KEY_SLOT before the crypto, so no lane needs another key.
+template <bool kSeal, bool kAffine, bool kOneKey>
+__device__ __forceinline__ void desc_sync_body(const DescParams &prm) {
   constexpr uint32_t kWaves = kStridedThreads / 64u;
-  __shared__ WaveStageDesc stage[kWaves];
-  __shared__ uint32_t wg_rounds[kWaves];
+  // The descriptor stages and, with kAffine, the uniform stages of the affine
+  // groups share the LDS; the workgroup's round / vote slots sit in the
+  // descriptor layout's slack (the last wave's uniform tag park: 2 workgroups x
+  // 80 KiB = the whole LDS).
+  static_assert(kWaves * sizeof(WaveStageDesc) + 4u * kWaves <= kWaves * sizeof(WaveStageUniform),
+                "vote slots in the slack");
+  constexpr uint32_t kLdsBytes =
+      kAffine ? kWaves * sizeof(WaveStageUniform) : (kWaves * sizeof(WaveStageDesc) + 4u * kWaves + 15u) & ~15u;
+  __shared__ uint4 lds_raw[kLdsBytes / 16u];
+  auto stage_d = [&](uint32_t w) { return reinterpret_cast<WaveStageDesc *>(lds_raw) + w; };
+  auto stage_u = [&](uint32_t w) { return reinterpret_cast<WaveStageUniform *>(lds_raw) + w; };
+  uint32_t *wg_rounds = reinterpret_cast<uint32_t *>(stage_d(kWaves));
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t groups = (prm.n + 64u * kWaves - 1u) / (64u * kWaves);
+  SessionKey sk;
+  if constexpr (kOneKey) {
+    const uint4 a = ld16(prm.keys), b = ld16(prm.keys + 16u);
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sk.k[j] = __builtin_amdgcn_readfirstlane(w[j]);
+    sk.sidx = __builtin_amdgcn_readfirstlane(prm.key_index[0]);
+  }
   for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
     const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
     // only the last group can lack waves; it is this workgroup's last iteration
@@ -1580,9 +1628,53 @@ __global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_s
       else if (((d.src_off | d.dst_off) & 15u) != 0u) job.status = WG_STATUS_MISALIGNED;
       else job.status = WG_STATUS_OK;
     }
-    DescGeom g{stage[wave], reinterpret_cast<uint64_t>(prm.src) - 16u,
-               reinterpret_cast<uint64_t>(prm.dst) - 16u, wg_rounds, wave, alive};
     int32_t *st = i < prm.n ? prm.status + idx : nullptr;
+    // Affine groups: when every wave of the workgroup holds 64 live packets of one
+    // length in slots at a constant stride on each side (MTU-sized traffic in
+    // fixed receive / send slots: config 4, a Tunn's bulk batches), the group runs
+    // the strided kernels' uniform geometry -- SGPR addressing, wave-uniform
+    // lengths and branches -- with the keys still per packet.  The vote is
+    // workgroup-wide because the two forms run different barrier sequences.
+    if constexpr (kAffine) {
+      const uint32_t Wl = kSeal ? job.len + WG_DATA_OVERHEAD_SZ : job.len;
+      const uint32_t W0 = __builtin_amdgcn_readfirstlane(Wl);
+      const uint64_t i0 = rl64(job.in_base, 0), o0 = rl64(job.out_base, 0);
+      const uint64_t si = rl64(job.in_base, 1) - i0, so = rl64(job.out_base, 1) - o0;
+      const uint64_t span = (W0 + 15u) & ~15u;
+      const bool shape = pkt0 + 64u <= prm.n && (kSeal || W0 >= WG_DATA_OVERHEAD_SZ) &&
+                         si >= span && so >= span &&
+                         63u * (si > so ? si : so) + W0 + 256u < (uint64_t)kNoAccessOffset;
+      const bool mine = job.status == WG_STATUS_OK && Wl == W0 &&
+                        job.in_base == i0 + (uint64_t)lane * si && job.out_base == o0 + (uint64_t)lane * so;
+      const uint32_t vote = shape && __ballot(!mine) == 0ull ? W0 : 0u;
+      __syncthreads();  // the previous group is done with the LDS (the slots overlap a tag park)
+      if (lane == 0u) wg_rounds[wave] = vote;
+      __syncthreads();
+      bool uni = wg_rounds[0] != 0u;
+      for (uint32_t w = 1; w < alive; ++w) uni = uni && wg_rounds[w] == wg_rounds[0];
+      __syncthreads();  // read before a uniform stage or the next vote overwrites them
+      if (uni) {
+        const uint32_t nr = (W0 + kRun - 1u) / kRun;
+        const uint32_t full_in = (i0 % 128u == 0u && si % 128u == 0u) ? 1u : 0u;
+        UniformGeom ug{i0, o0, si, so, 0ull, W0, nr, 0u, full_in};
+        // (equal on every lane: constants / SGPRs, so the uniform form's branches stay scalar)
+        job.len = __builtin_amdgcn_readfirstlane(job.len);
+        job.status = WG_STATUS_OK;
+        if constexpr (kOneKey)
+          run_wave<kSeal, true, true, false, false, true>(*stage_u(wave), ug, lane, job, prm.keys,
+                                                          prm.key_index, st, &sk);
+        else
+          run_wave<kSeal, true, true, false, true, true>(*stage_u(wave), ug, lane, job, prm.keys,
+                                                         prm.key_index, st);
+        continue;
+      }
+    }
+    DescGeom g{*stage_d(wave), reinterpret_cast<uint64_t>(prm.src) - 16u,
+               reinterpret_cast<uint64_t>(prm.dst) - 16u, wg_rounds, wave, alive};
+    if constexpr (kOneKey) {
+      run_wave<kSeal, false, true, true>(*stage_d(wave), g, lane, job, prm.keys, prm.key_index, st, &sk);
+      continue;
+    }
 #if WG_DESC_UNIFORM_KEY
     // a wave whose live packets all use one key slot (single-session batches:
     // config 3, a Tunn's batches) takes the SGPR-key form; the two forms run
@@ -1598,13 +1690,37 @@ __global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_s
 #pragma unroll
         for (int j = 0; j < 8; ++j) sk.k[j] = __builtin_amdgcn_readfirstlane(w[j]);
         sk.sidx = __builtin_amdgcn_readfirstlane(prm.key_index[us]);
-        run_wave<kSeal, false, true, true>(stage[wave], g, lane, job, prm.keys, prm.key_index, st, &sk);
+        run_wave<kSeal, false, true, true>(*stage_d(wave), g, lane, job, prm.keys, prm.key_index, st, &sk);
         continue;
       }
     }
 #endif
-    run_wave<kSeal, false, true>(stage[wave], g, lane, job, prm.keys, prm.key_index, st);
+    run_wave<kSeal, false, true>(*stage_d(wave), g, lane, job, prm.keys, prm.key_index, st);
   }
+}
+
+template <bool kSeal>
+__global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_sync_kernel(
+    DescParams prm) {
+  desc_sync_body<kSeal, false, false>(prm);
+}
+
+template <bool kSeal>
+__global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_affine_kernel(
+    DescParams prm) {
+  desc_sync_body<kSeal, true, false>(prm);
+}
+
+template <bool kSeal>
+__global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_sync_key1_kernel(
+    DescParams prm) {
+  desc_sync_body<kSeal, false, true>(prm);
+}
+
+template <bool kSeal>
+__global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_affine_key1_kernel(
+    DescParams prm) {
+  desc_sync_body<kSeal, true, true>(prm);
 }
 
 template __global__ void aead_strided_kernel<true, false>(StridedParams);
@@ -1615,6 +1731,12 @@ template __global__ void aead_desc_kernel<true>(DescParams);
 template __global__ void aead_desc_kernel<false>(DescParams);
 template __global__ void aead_desc_sync_kernel<true>(DescParams);
 template __global__ void aead_desc_sync_kernel<false>(DescParams);
+template __global__ void aead_desc_affine_kernel<true>(DescParams);
+template __global__ void aead_desc_affine_kernel<false>(DescParams);
+template __global__ void aead_desc_sync_key1_kernel<true>(DescParams);
+template __global__ void aead_desc_sync_key1_kernel<false>(DescParams);
+template __global__ void aead_desc_affine_key1_kernel<true>(DescParams);
+template __global__ void aead_desc_affine_key1_kernel<false>(DescParams);
 
 }  // namespace wg
 

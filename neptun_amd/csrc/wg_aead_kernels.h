@@ -60,6 +60,19 @@ template <bool kSeal, bool kTail> __global__ void aead_strided_kernel(StridedPar
 __global__ void aead_strided_open_text_kernel(StridedParams prm);
 template <bool kSeal> __global__ void aead_desc_kernel(DescParams prm);
 template <bool kSeal> __global__ void aead_desc_sync_kernel(DescParams prm);
+// Descriptor batches launched without a plan go to aead_desc_affine_kernel, whose
+// workgroups with affine packets (one length, constant slot strides) run the
+// uniform geometry with per-packet keys (0: aead_desc_sync_kernel for every launch).
+#ifndef WG_DESC_AFFINE
+#define WG_DESC_AFFINE 1
+#endif
+// ... and contexts with a single key slot to the *_key1 forms (SGPR key)
+template <bool kSeal> __global__ void aead_desc_sync_key1_kernel(DescParams prm);
+template <bool kSeal> __global__ void aead_desc_affine_key1_kernel(DescParams prm);
+#ifndef WG_DESC_KEY1
+#define WG_DESC_KEY1 1
+#endif
+template <bool kSeal> __global__ void aead_desc_affine_kernel(DescParams prm);
 
 // wg_plan.hip: counting sort of a descriptor batch by rounds (longest first)
 constexpr uint32_t kPlanBins = 256;   // rounds 0..254, 255+ share the top bin

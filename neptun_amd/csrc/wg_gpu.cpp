@@ -34,6 +34,12 @@ struct wg_gpu_ctx {
   std::mutex mu;                   // serialises key-table and route-table updates
 };
 
+// open into line-aligned plaintext slots on the text grid (1) or on the wire grid
+// with its output runs straddling the destination's lines (0: A/B only)
+#ifndef WG_TEXT_GRID
+#define WG_TEXT_GRID 1
+#endif
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -181,10 +187,19 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
     // per-packet tables hold buffer-relative offsets, hence non-null bases
     const uint32_t groups = (n + wg::kStridedThreads - 1) / wg::kStridedThreads;
     const dim3 grid(std::min(groups, ctx->cus * wg::kStridedBlocksPerCU));
-    if (seal)
-      hipLaunchKernelGGL(wg::aead_desc_sync_kernel<true>, grid, dim3(wg::kStridedThreads), 0, s, prm);
-    else
-      hipLaunchKernelGGL(wg::aead_desc_sync_kernel<false>, grid, dim3(wg::kStridedThreads), 0, s, prm);
+    // unordered launches may hold affine workgroups (fixed slots, one length);
+    // a plan's permutation gathers packets from all over the batch
+    const bool affine = WG_DESC_AFFINE && order == nullptr;
+    // a single-slot context: every packet that passes the slot check uses key 0
+    const bool key1 = WG_DESC_KEY1 && ctx->key_slots == 1;
+    using K = void (*)(wg::DescParams);
+    static const K kernels[2][2][2] = {  // [seal][affine][key1]
+        {{wg::aead_desc_sync_kernel<false>, wg::aead_desc_sync_key1_kernel<false>},
+         {wg::aead_desc_affine_kernel<false>, wg::aead_desc_affine_key1_kernel<false>}},
+        {{wg::aead_desc_sync_kernel<true>, wg::aead_desc_sync_key1_kernel<true>},
+         {wg::aead_desc_affine_kernel<true>, wg::aead_desc_affine_key1_kernel<true>}}};
+    hipLaunchKernelGGL(kernels[seal ? 1 : 0][affine ? 1 : 0][key1 ? 1 : 0], grid,
+                       dim3(wg::kStridedThreads), 0, s, prm);
   } else if (seal) {
     hipLaunchKernelGGL(wg::aead_desc_kernel<true>, dim3(grid_for(n)), dim3(wg::kBlockThreads), 0,
                        s, prm);
@@ -261,7 +276,7 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
                         dst_stride, counter_base, n, len, key_slot, 0u, 0u};
   // open into plaintext slots that start on 128-byte boundaries: the text
   // run grid keeps every output line whole (wg_aead.hip Ranges)
-  const bool text_grid = !seal && ((uintptr_t)dst % 128u) == 0 && dst_stride % 128u == 0;
+  const bool text_grid = WG_TEXT_GRID && !seal && ((uintptr_t)dst % 128u) == 0 && dst_stride % 128u == 0;
   if (ctx->pad_slots) {
     // zero-fill to the line end only where the output runs sit on whole lines
     // and that line end stays inside the slot (the uniform kernels' grid origin:

@@ -25,8 +25,10 @@ def test_model_is_a_floor_of_the_measured_instructions_config2(kernel):
     assert model <= measured <= 1.03 * model, (model, measured)
 
 
-@pytest.mark.parametrize("kernel", ["aead_desc_sync_kernel<true>", "aead_desc_sync_kernel<false>"])
-def test_model_is_a_floor_config4_per_lane_keys(kernel):
+@pytest.mark.parametrize("seal", [True, False])
+def test_model_is_a_floor_config4_per_lane_keys(seal):
+    d = json.load(open(os.path.join(ROOT, "profiles", "pmc_valu_config4.json")))["kernels"]
+    kernel = [k for k in d if k.endswith("<true>" if seal else "<false>")][0]
     model = cr.launch_floor((1350, 1 << 24), per_lane_keys=True)["model_valu_instr_per_64_packets"]
     assert model <= pmc_per_64(4, kernel, 1 << 24)
 

@@ -969,3 +969,164 @@ def test_descriptor_wave_shapes_match_oracle(torch_cuda, gpu):
             assert not back[a:a + P].any()
         else:
             assert np.array_equal(back[a:a + P], want2[a:a + P]) and np.array_equal(back[a:a + P], src[a:a + P])
+
+
+@pytest.mark.parametrize("P,ss,sd,n,base,breaks", [
+    (1350, 1408, 1408, 512 * 3 + 64 * 3 + 17, (0, 0), ()),   # config 4's slots; partial last group
+    (64, 96, 96, 1024, (48, 16), ()),                          # tight strides, lines not 128-aligned
+    (0, 32, 32, 512, (0, 0), ()),                              # empty payloads
+    (1000, 1152, 1040, 1536, (16, 0), (600,)),                 # unequal strides; group 1 not affine
+    (8900, 8960, 8960, 576, (0, 128), ()),                     # jumbo
+])
+def test_affine_descriptor_groups_match_oracle(torch_cuda, gpu, P, ss, sd, n, base, breaks):
+    """Descriptor batches whose workgroups hold one length at constant slot strides
+    run the uniform geometry with per-packet keys (WG_DESC_AFFINE): sealed and opened
+    bit-exact against the oracle over the whole destination (no byte outside a packet
+    written), beside groups that do not qualify (a partial last group, a group with
+    one packet out of place) and with open's failures inside affine groups (tampered
+    ciphertext zeroed, wrong receiver index, wrong message type)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(P + n)
+    n_keys = 64
+    keys = rng.integers(0, 256, (n_keys, 32), dtype=np.uint8)
+    kidx = rng.integers(0, 2**32, n_keys, dtype=np.uint64).astype(np.uint32)
+    gpu.set_keys(0, keys, kidx)
+    sizes = np.full(n, P, np.int64)
+    payloads = synth.host_payloads(sizes, seed=P + 7)
+    soffs = base[0] + ss * np.arange(n, dtype=np.int64)
+    doffs = base[1] + sd * np.arange(n, dtype=np.int64)
+    for b in breaks:  # swap two packets' wire slots: that workgroup is not affine
+        doffs[b], doffs[b + 1] = doffs[b + 1], doffs[b]
+    src = np.zeros(int(soffs[-1]) + ss + 64, np.uint8)
+    for i in range(n):
+        src[soffs[i]:soffs[i] + P] = np.frombuffer(payloads[i], np.uint8)
+    dst_size = int(doffs.max()) + sd + 64
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = soffs
+    descs["dst_off"] = doffs
+    descs["counter"] = rng.integers(0, 2**63, n, dtype=np.uint64)
+    descs["counter"][:3] = [2**32 - 1, 2**32, 2**64 - 1]
+    descs["len"] = sizes
+    descs["key_slot"] = rng.integers(0, n_keys, n).astype(np.uint32)
+    out, st = run_desc(torch, gpu, True, descs, src, dst_size)
+    want = np.zeros(dst_size, np.uint8)
+    wst = o.seal_batch(descs, keys, kidx, src, want)
+    assert (wst == 0).all() and (st == 0).all(), np.unique(st)
+    assert np.array_equal(out, want), "sealed bytes differ from the oracle"
+    # open them back, with failures inside the (affine) first group
+    d2 = np.zeros(n, DESC)
+    d2["src_off"] = doffs
+    d2["dst_off"] = soffs
+    d2["len"] = sizes + 32
+    d2["key_slot"] = descs["key_slot"]
+    wire = out.copy()
+    tampered, wrong_idx, wrong_type = [3, 200], [77], [130]
+    for t in tampered:
+        wire[int(doffs[t]) + 16 + int(rng.integers(0, P + 16))] ^= 0x10
+    for t in wrong_idx:
+        wire[int(doffs[t]) + 4] ^= 0x01
+    for t in wrong_type:
+        wire[int(doffs[t])] = 1
+    back, st2 = run_desc(torch, gpu, False, d2, wire, len(src))
+    want2 = np.zeros(len(src), np.uint8)
+    wst2 = o.open_batch(d2, keys, kidx, wire, want2)
+    assert (st2 == wst2).all(), [(i, st2[i], wst2[i]) for i in np.nonzero(st2 != wst2)[0][:8]]
+    assert (st2[tampered] == 10).all() and (st2[wrong_idx] != 0).all() and (st2[wrong_type] != 0).all()
+    assert np.array_equal(back, want2), "opened bytes differ from the oracle"
+    ok = np.ones(n, bool)
+    ok[tampered + wrong_idx + wrong_type] = False
+    for i in np.nonzero(ok)[0][:: max(1, n // 97)]:
+        assert np.array_equal(back[soffs[i]:soffs[i] + P], src[soffs[i]:soffs[i] + P])
+
+
+@pytest.fixture(scope="module")
+def gpu1(torch_cuda):
+    """A single-slot context: its descriptor launches take the SGPR-key forms."""
+    from neptun_amd import GpuContext
+    ctx = GpuContext(0, key_slots=1)
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("form", ["mixed", "ordered", "affine"])
+def test_single_slot_context_forms_match_oracle(torch_cuda, gpu1, form):
+    """Descriptor batches on a one-slot context (aead_desc_*_key1_kernel: the key
+    loaded once per kernel): unordered mixed lengths, the plan's ordered launch,
+    and affine groups -- sealed and opened bit-exact against the oracle, with
+    packets naming other slots failing with BAD_KEY_SLOT (open: the invalid and
+    no-session markers keep their statuses), tampered datagrams rejected and
+    zeroed, and a wrong receiver index refused."""
+    torch = torch_cuda
+    rng = np.random.default_rng({"mixed": 5, "ordered": 6, "affine": 7}[form])
+    keys = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+    kidx = np.array([0x5EED1234], np.uint32)
+    gpu1.set_keys(0, keys, kidx)
+    n = 512 * 4 + 200
+    if form == "affine":
+        P, S = 1350, 1408
+        sizes = np.full(n, P, np.int64)
+        soffs = S * np.arange(n, dtype=np.int64)
+        doffs = soffs.copy()
+        src = np.zeros(S * n + 64, np.uint8)
+        for i, p in enumerate(synth.host_payloads(sizes, seed=8)):
+            src[soffs[i]:soffs[i] + P] = np.frombuffer(p, np.uint8)
+        dst_size = S * n + 64
+    else:
+        sizes = rng.choice([0, 1, 64, 255, 1350, 4000, 8900], n)
+        src, soffs = pack(synth.host_payloads(sizes, seed=9))
+        soffs = np.array(soffs, np.int64)
+        doffs, pos = np.zeros(n, np.int64), 0
+        for i in rng.permutation(n):
+            doffs[i] = pos
+            pos = synth.round_up(pos + int(sizes[i]) + 32, 16)
+        dst_size = pos + 64
+    descs = np.zeros(n, DESC)
+    descs["src_off"], descs["dst_off"], descs["len"] = soffs, doffs, sizes
+    descs["counter"] = rng.integers(0, 2**63, n, dtype=np.uint64)
+    bad = [] if form == "affine" else [7, 600, 1500]
+    if bad:
+        descs["key_slot"][bad] = [1, 5, 2**31]
+    valid = np.ones(n, bool)
+    valid[bad] = False
+
+    def launch(seal, d, src_b, size):
+        d_descs = to_dev(torch, d.view(np.uint8))
+        d_src = to_dev(torch, src_b)
+        d_dst = torch.zeros(max(size, 16), dtype=torch.uint8, device="cuda")
+        d_st = torch.full((len(d),), -1, dtype=torch.int32, device="cuda")
+        if form == "ordered":
+            order = torch.zeros(len(d), dtype=torch.int32, device="cuda")
+            scratch = torch.zeros(262144 // 4, dtype=torch.int32, device="cuda")
+            gpu1.plan_batch(seal, d_descs, len(d), order, scratch)
+            (gpu1.seal_batch_ordered if seal else gpu1.open_batch_ordered)(
+                d_descs, order, len(d), d_src, d_dst, d_st)
+        else:
+            (gpu1.seal_batch if seal else gpu1.open_batch)(d_descs, len(d), d_src, d_dst, d_st)
+        torch.cuda.synchronize()
+        return d_dst.cpu().numpy(), d_st.cpu().numpy()
+
+    out, st = launch(True, descs, src, dst_size)
+    assert (st[bad] == 101).all() and (st[valid] == 0).all(), np.unique(st)
+    want = np.zeros(dst_size, np.uint8)
+    assert (o.seal_batch(descs[valid], keys, kidx, src, want) == 0).all()
+    assert np.array_equal(out, want), "sealed bytes differ from the oracle"
+    d2 = np.zeros(n, DESC)
+    d2["src_off"], d2["dst_off"], d2["len"] = doffs, soffs, sizes + 32
+    d2["key_slot"] = descs["key_slot"]
+    markers = [] if form == "affine" else [8, 9]
+    d2["key_slot"][markers] = [0xFFFFFFFE, 0xFFFFFFFF][: len(markers)]  # invalid / no-session
+    ok2 = valid.copy()
+    ok2[markers] = False
+    wire = out.copy()
+    tampered, wrong_idx = [11, 1300], [40]
+    for t in tampered:
+        wire[int(doffs[t]) + 16 + int(rng.integers(0, int(sizes[t]) + 16))] ^= 0x02
+    for t in wrong_idx:
+        wire[int(doffs[t]) + 5] ^= 0x80
+    back, st2 = launch(False, d2, wire, len(src))
+    assert (st2[bad] == 101).all() and (st2[markers] == [13, 14][: len(markers)]).all()
+    want2 = np.zeros(len(src), np.uint8)
+    wst2 = o.open_batch(d2[ok2], keys, kidx, wire, want2)  # (the oracle takes valid slots only)
+    assert (st2[ok2] == wst2).all(), [(i, st2[ok2][i], wst2[i]) for i in np.nonzero(st2[ok2] != wst2)[0][:8]]
+    assert (st2[tampered] == 10).all() and (st2[wrong_idx] != 0).all()
+    assert np.array_equal(back, want2), "opened bytes differ from the oracle"

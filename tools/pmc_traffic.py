@@ -47,6 +47,9 @@ def short(name):
     for tag in ("aead_strided_kernel<true, false>", "aead_strided_kernel<false, false>",
                 "aead_strided_open_text_kernel",
                 "aead_desc_sync_kernel<true>", "aead_desc_sync_kernel<false>",
+                "aead_desc_affine_kernel<true>", "aead_desc_affine_kernel<false>",
+                "aead_desc_sync_key1_kernel<true>", "aead_desc_sync_key1_kernel<false>",
+                "aead_desc_affine_key1_kernel<true>", "aead_desc_affine_key1_kernel<false>",
                 "aead_desc_kernel<true>", "aead_desc_kernel<false>"):
         if tag in name:
             return tag
