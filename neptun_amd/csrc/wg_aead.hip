@@ -153,6 +153,26 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #ifndef WG_TEXT_LOAD_CPOL
 #define WG_TEXT_LOAD_CPOL 0
 #endif
+// the text grid's two kinds of load piece, each its own instruction (exec-masked):
+// a run's chunk 7 is the HEAD of the next datagram line (its first access, read
+// again by the next round) and chunks 0-6 the BODY of this line (its last access)
+#ifndef WG_TEXT_SPLIT
+#define WG_TEXT_SPLIT 0
+#endif
+#ifndef WG_TEXT_HEAD_CPOL
+#define WG_TEXT_HEAD_CPOL 0
+#endif
+#ifndef WG_TEXT_BODY_CPOL
+#define WG_TEXT_BODY_CPOL 2
+#endif
+// (equal policies: the compiler merges the two arms into one load per piece, and
+// open's header wait, which counts 16 load instructions per round, runs early)
+#if WG_TEXT_SPLIT && WG_TEXT_HEAD_CPOL == WG_TEXT_BODY_CPOL
+#error "WG_TEXT_SPLIT needs two different cache policies"
+#endif
+// Measured (profiles/r03l_ab_text_split.txt): body nt / head default cut the open's
+// HBM reads 2.76 -> 2.36 GB per launch (the head lines stay in L2 more often) but
+// not its time (0.775 vs 0.773 ms): off.
 // the owner-lane stores of a packet's partial last chunk (dword / short / byte,
 // no slot padding) keep the default policy: as nt stores their partial writes
 // made an unpadded round trip 18 % slower
@@ -618,6 +638,18 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &
     const uint32_t v0 = y * stride + 16u * k0, v1 = y * stride + 16u * k1;
 #if WG_STAGE_CHAIN
     StageChain c(run, stride, r);
+    if constexpr (kText && WG_TEXT_SPLIT) {
+#pragma unroll
+      for (uint32_t j = 0; j < kChunks; ++j) {
+        if (((j & 1u) ? k1 : k0) != 7u)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, c.lds(j), 16, (j & 1u) ? v1 : v0, c.soff(j), 0,
+                                                   WG_TEXT_BODY_CPOL);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, c.lds(j), 16, (j & 1u) ? v1 : v0, c.soff(j), 0,
+                                                   WG_TEXT_HEAD_CPOL);
+      }
+      return;
+    }
 #pragma unroll
     for (uint32_t j = 0; j < kChunks; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, c.lds(j), 16, (j & 1u) ? v1 : v0, c.soff(j), 0,
@@ -1246,8 +1278,12 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
           dma_global<WG_HDR_NT != 0>(lds_offset(&S.tagp[0]), reinterpret_cast<const uint8_t *>(job.in_base - (16u - kG)));
         stage_in<kSeal>(run, g, lane, 0);  // exactly 8 pieces (round 0 is straight-line)
         u32x4 h;
-        asm volatile("s_waitcnt vmcnt(8)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(h) : "v"(lds_offset(&S.tagp[lane])) : "memory");
+        if constexpr (kText && WG_TEXT_SPLIT)  // (16 load instructions per round)
+          asm volatile("s_waitcnt vmcnt(16)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                       : "=v"(h) : "v"(lds_offset(&S.tagp[lane])) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(8)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                       : "=v"(h) : "v"(lds_offset(&S.tagp[lane])) : "memory");
         hdr = make_uint4(h.x, h.y, h.z, h.w);
       } else {
         // (a global-address-space load: a flat one may alias LDS and makes the
