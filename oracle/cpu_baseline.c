@@ -36,7 +36,8 @@ typedef struct {
   uint8_t key[32];
   uint8_t *pt, *wire, *out;
   size_t n;
-  int bad;
+  int bad, cpu, reps;
+  uint64_t seed;
   pthread_barrier_t *bar;
   double t_seal, t_open;
 } job_t;
@@ -54,10 +55,33 @@ static uint64_t splitmix64(uint64_t *s) {
   return z ^ (z >> 31);
 }
 
-static void *worker(void *arg) {
-  job_t *j = (job_t *)arg;
+/* The worker's own packets, allocated and written by the worker itself (after it
+ * pinned itself), so its buffers are local to its core's memory node. */
+static void job_init(job_t *j) {
   const size_t P = g_pkt, W = P + 32;
-  pthread_barrier_wait(j->bar);
+  uint64_t kseed = 0x4E455054554Full; /* "NEPTUN" + 1 */
+  for (int k = 0; k < 32; k += 8) { uint64_t v = splitmix64(&kseed); memcpy(j->key + k, &v, 8); }
+  j->pt = malloc(j->n * P);
+  j->wire = malloc(j->n * W);
+  j->out = malloc(j->n * (P + 16));
+  uint64_t seed = j->seed;
+  for (size_t i = 0; i < j->n * P; i += 8) {
+    uint64_t v = splitmix64(&seed);
+    memcpy(j->pt + i, &v, (j->n * P - i) < 8 ? (j->n * P - i) : 8);
+  }
+  memset(j->wire, 0, j->n * W);
+  memset(j->out, 0, j->n * (P + 16));
+  /* valid IPv4 header (ver 4, IHL 5, total_length = P, proto 17) so that
+   * validate_decapsulated_packet keeps all P bytes (noise/mod.rs:613-634) */
+  for (size_t i = 0; i < j->n && P >= 20; ++i) {
+    uint8_t *h = j->pt + i * P;
+    h[0] = 0x45; h[1] = 0; h[2] = (uint8_t)(P >> 8); h[3] = (uint8_t)P; h[9] = 17;
+    h[12] = 10; h[13] = 0; h[14] = 0; h[15] = 1; h[16] = 10; h[17] = 0; h[18] = 0; h[19] = 2;
+  }
+}
+
+static void run_once(job_t *j) {
+  const size_t P = g_pkt, W = P + 32;
   double t0 = now();
   for (size_t i = 0; i < j->n; ++i) {
     if (g_use_openssl)
@@ -81,9 +105,49 @@ static void *worker(void *arg) {
     if (rc) j->bad++;
   }
   double t2 = now();
-  j->t_seal = t1 - t0;
-  j->t_open = t2 - t1;
+  if (t1 - t0 < j->t_seal) j->t_seal = t1 - t0;
+  if (t2 - t1 < j->t_open) j->t_open = t2 - t1;
+}
+
+/* One thread per worker for all reps: pin (optional), build its packets, then per
+ * rep wait for the start barrier, run, and meet the main thread at the end barrier. */
+static void *worker(void *arg) {
+  job_t *j = (job_t *)arg;
+  if (j->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(j->cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  }
+  job_init(j);
+  j->t_seal = j->t_open = 1e30;
+  for (int r = 0; r < j->reps; ++r) {
+    pthread_barrier_wait(j->bar);
+    run_once(j);
+    pthread_barrier_wait(j->bar);
+  }
   return NULL;
+}
+
+/* --pin: one CPU per physical core, in the order of the process's affinity mask
+ * (the first SMT sibling of each core the mask allows). */
+static int physical_cpus(int *out, int max) {
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set)) return 0;
+  int k = 0;
+  for (int c = 0; c < CPU_SETSIZE && k < max; ++c) {
+    if (!CPU_ISSET(c, &set)) continue;
+    char path[128];
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c);
+    FILE *f = fopen(path, "r");
+    int first = c;
+    if (f) {
+      if (fscanf(f, "%d", &first) != 1) first = c;
+      fclose(f);
+    }
+    if (first == c) out[k++] = c;
+  }
+  return k;
 }
 
 static int cmpd(const void *a, const void *b) {
@@ -92,66 +156,66 @@ static int cmpd(const void *a, const void *b) {
 }
 
 int main(int argc, char **argv) {
-  size_t n = 65536;
-  int threads = 1, reps = 5;
+  size_t n = 65536, per_thread = 0;
+  int threads = 1, reps = 5, pin = 0;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--packets") && i + 1 < argc) n = strtoull(argv[++i], 0, 10);
+    else if (!strcmp(argv[i], "--packets-per-thread") && i + 1 < argc) per_thread = strtoull(argv[++i], 0, 10);
     else if (!strcmp(argv[i], "--threads") && i + 1 < argc) threads = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--reps") && i + 1 < argc) reps = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--size") && i + 1 < argc) g_pkt = strtoull(argv[++i], 0, 10);
     else if (!strcmp(argv[i], "--impl") && i + 1 < argc) g_use_openssl = !strcmp(argv[++i], "openssl");
-    else { fprintf(stderr, "usage: %s [--packets N] [--threads T] [--reps R] [--size P] [--impl openssl|oracle]\n", argv[0]); return 2; }
+    else if (!strcmp(argv[i], "--pin")) pin = 1;
+    else { fprintf(stderr, "usage: %s [--packets N | --packets-per-thread N] [--threads T] [--reps R] [--size P] [--impl openssl|oracle] [--pin]\n", argv[0]); return 2; }
   }
-  const size_t P = g_pkt, W = P + 32;
+  if (threads < 1 || reps < 1) return 2;
+  if (per_thread) n = per_thread * (size_t)threads;
+  const size_t P = g_pkt;
+  int *cpus = calloc(threads, sizeof(int));
+  int ncpu = pin ? physical_cpus(cpus, threads) : 0;
+  if (pin && ncpu < threads) {
+    fprintf(stderr, "--pin: only %d physical cores in the affinity mask for %d threads\n", ncpu, threads);
+    return 2;
+  }
   job_t *jobs = calloc(threads, sizeof(job_t));
   pthread_t *th = calloc(threads, sizeof(pthread_t));
   pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, threads + 1);
   uint64_t seed = 0x4E455054554Eull; /* "NEPTUN" */
-  uint64_t kseed = seed + 1;
   size_t per = n / threads;
   for (int t = 0; t < threads; ++t) {
     job_t *j = &jobs[t];
-    for (int k = 0; k < 32; k += 8) { uint64_t v = splitmix64(&kseed); memcpy(j->key + k, &v, 8); }
     j->n = per + (t < (int)(n % threads) ? 1 : 0);
-    j->pt = malloc(j->n * P);
-    j->wire = malloc(j->n * W);
-    j->out = malloc(j->n * (P + 16));
-    for (size_t i = 0; i < j->n * P; i += 8) {
-      uint64_t v = splitmix64(&seed);
-      memcpy(j->pt + i, &v, (j->n * P - i) < 8 ? (j->n * P - i) : 8);
-    }
-    /* valid IPv4 header (ver 4, IHL 5, total_length = P, proto 17) so that
-     * validate_decapsulated_packet keeps all P bytes (noise/mod.rs:613-634) */
-    for (size_t i = 0; i < j->n && P >= 20; ++i) {
-      uint8_t *h = j->pt + i * P;
-      h[0] = 0x45; h[1] = 0; h[2] = (uint8_t)(P >> 8); h[3] = (uint8_t)P; h[9] = 17;
-      h[12] = 10; h[13] = 0; h[14] = 0; h[15] = 1; h[16] = 10; h[17] = 0; h[18] = 0; h[19] = 2;
-    }
+    j->cpu = pin ? cpus[t] : -1;
+    j->reps = reps;
+    j->seed = seed + 0x1000003ull * (uint64_t)t;
+    j->bar = &bar;
+    pthread_create(&th[t], NULL, worker, j);
   }
   double *walls = calloc(reps, sizeof(double));
-  double best_seal = 1e30, best_open = 1e30;
-  int bad = 0;
   for (int r = 0; r < reps; ++r) {
-    pthread_barrier_init(&bar, NULL, threads + 1);
-    for (int t = 0; t < threads; ++t) { jobs[t].bar = &bar; jobs[t].bad = 0; pthread_create(&th[t], NULL, worker, &jobs[t]); }
-    pthread_barrier_wait(&bar);
+    pthread_barrier_wait(&bar); /* every worker built its packets / finished the last rep */
     double t0 = now();
-    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    pthread_barrier_wait(&bar);
     walls[r] = now() - t0;
     if (getenv("CPU_BASELINE_DEBUG")) fprintf(stderr, "rep %d wall %.4f\n", r, walls[r]);
-    double ms = 0, mo = 0;
-    for (int t = 0; t < threads; ++t) { bad += jobs[t].bad; if (jobs[t].t_seal > ms) ms = jobs[t].t_seal; if (jobs[t].t_open > mo) mo = jobs[t].t_open; }
-    if (ms < best_seal) best_seal = ms;
-    if (mo < best_open) best_open = mo;
-    pthread_barrier_destroy(&bar);
   }
+  int bad = 0;
+  double ms = 0, mo = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    bad += jobs[t].bad;
+    if (jobs[t].t_seal > ms) ms = jobs[t].t_seal;
+    if (jobs[t].t_open > mo) mo = jobs[t].t_open;
+  }
+  pthread_barrier_destroy(&bar);
   qsort(walls, reps, sizeof(double), cmpd);
   double med = walls[reps / 2];
   double gbps = (double)n * P * 8 / med / 1e9;
-  printf("{\"impl\": \"%s\", \"threads\": %d, \"packets\": %zu, \"size\": %zu, \"reps\": %d, "
+  printf("{\"impl\": \"%s\", \"threads\": %d, \"pinned\": %s, \"packets\": %zu, \"size\": %zu, \"reps\": %d, "
          "\"median_s\": %.6f, \"gbps\": %.4f, \"pkts_per_s\": %.1f, \"seal_gbps_best\": %.4f, "
          "\"open_gbps_best\": %.4f, \"tag_failures\": %d}\n",
-         g_use_openssl ? "openssl" : "oracle", threads, n, P, reps, med, gbps, n / med,
-         (double)n * P * 8 / best_seal / 1e9, (double)n * P * 8 / best_open / 1e9, bad);
+         g_use_openssl ? "openssl" : "oracle", threads, pin ? "true" : "false", n, P, reps, med, gbps,
+         n / med, (double)n * P * 8 / ms / 1e9, (double)n * P * 8 / mo / 1e9, bad);
   return bad ? 1 : 0;
 }
