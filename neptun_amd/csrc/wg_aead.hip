@@ -212,11 +212,16 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #if WG_STAMP
 constexpr int kStampBlocks = 4096, kStampRounds = 16, kStampPhases = 6;
 __device__ uint64_t g_stamps[2][kStampBlocks][kStampRounds][kStampPhases];
+// s_memrealtime (100 MHz) beside each round's start stamp: the in-kernel shader
+// clock is d(s_memtime) / d(s_memrealtime) x 100 MHz (tools/clock_trace.py)
+__device__ uint64_t g_realtime[2][kStampBlocks][kStampRounds];
 #define WG_STAMP_AT(seal, r, ph)                                                              \
   do {                                                                                      \
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0 && lane == 0 &&                \
-        blockIdx.x < kStampBlocks && (r) < kStampRounds)                                    \
+        blockIdx.x < kStampBlocks && (r) < kStampRounds) {                                  \
       g_stamps[seal][blockIdx.x][r][ph] = __builtin_amdgcn_s_memtime();                     \
+      if ((ph) == 0) g_realtime[seal][blockIdx.x][r] = __builtin_amdgcn_s_memrealtime();   \
+    }                                                                                       \
   } while (0)
 #else
 #define WG_STAMP_AT(seal, r, ph) do {} while (0)
@@ -1779,5 +1784,18 @@ template __global__ void aead_desc_affine_key1_kernel<false>(DescParams);
 #if WG_STAMP
 extern "C" int wg_gpu_debug_stamps(void *out, size_t bytes) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(wg::g_stamps), bytes) == hipSuccess ? 0 : -1;
+}
+extern "C" int wg_gpu_debug_realtime(void *out, size_t bytes) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(wg::g_realtime), bytes) == hipSuccess ? 0 : -1;
+}
+// device-side snapshot of both stamp arrays into `dst` (device memory, stamps then
+// realtime), queued on `stream` behind the launch it records: no host sync per step
+extern "C" int wg_gpu_debug_snapshot(void *dst, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const size_t a = sizeof(wg::g_stamps), b = sizeof(wg::g_realtime);
+  if (hipMemcpyFromSymbolAsync(dst, HIP_SYMBOL(wg::g_stamps), a, 0, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return -1;
+  return hipMemcpyFromSymbolAsync((char *)dst + a, HIP_SYMBOL(wg::g_realtime), b, 0,
+                                  hipMemcpyDeviceToDevice, st) == hipSuccess ? 0 : -1;
 }
 #endif
