@@ -1130,3 +1130,116 @@ def test_single_slot_context_forms_match_oracle(torch_cuda, gpu1, form):
     assert (st2[ok2] == wst2).all(), [(i, st2[ok2][i], wst2[i]) for i in np.nonzero(st2[ok2] != wst2)[0][:8]]
     assert (st2[tampered] == 10).all() and (st2[wrong_idx] != 0).all()
     assert np.array_equal(back, want2), "opened bytes differ from the oracle"
+
+
+def test_randomized_launch_shapes_match_oracle(torch_cuda, gpu, gpu1):
+    """Randomized sweep over the launch shapes the host picks kernels from, each
+    against the oracle bit for bit: strided batches (random n incl. partial waves,
+    P 0..2600, strides and output offsets on and off 128-byte lines -- the wire grid,
+    the text grid and the one-wave tail launch -- counters across 2^32), and descriptor
+    batches on a 4096-slot and a one-slot context (per-lane, SGPR-key, affine and
+    plan-ordered forms) with tampered and wrong-index datagrams.  Bytes outside every
+    packet's output must keep their canary value."""
+    torch = torch_cuda
+    rng = np.random.default_rng(20261017)
+    keys = rng.integers(0, 256, (4096, 32), dtype=np.uint8)
+    kidx = rng.integers(0, 2**32, 4096, dtype=np.uint64).astype(np.uint32)
+    gpu.set_keys(0, keys, kidx)
+    gpu1.set_keys(0, keys[:1], kidx[:1])
+    for it in range(32):  # strided
+        n = int(rng.choice([1, 63, 64, 65, 511, 512, 1000, 2049]))
+        P = int(rng.choice([0, 1, 15, 16, 17, 127, 128, 129, 1350, 1366, int(rng.integers(0, 2600))]))
+        Ss = synth.round_up(P + int(rng.choice([0, 16, 48, 160])), 16) or 16
+        Sw = synth.round_up(P + 32 + int(rng.choice([0, 16, 96, 250])), 16)
+        Sp = synth.round_up(P + int(rng.choice([0, 16, 112, 200])), 16) or 16
+        po = int(rng.choice([0, 16, 32, 128]))   # open's plaintext offset into its buffer
+        wo = int(rng.choice([0, 16, 128]))      # seal's datagram offset
+        base = int(rng.choice([0, 2**32 - 40, int(rng.integers(0, 2**62))]))
+        slot = int(rng.integers(0, 4096))
+        src = rng.integers(0, 256, n * Ss + 16, dtype=np.uint8)
+        d_src = to_dev(torch, src)
+        wire = torch.full((n * Sw + wo + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        gpu.seal_strided(n, P, slot, base, d_src, Ss, wire.data_ptr() + wo, Sw, st)
+        torch.cuda.synchronize()
+        assert (st == 0).all(), (it, n, P)
+        descs = np.zeros(n, DESC)
+        descs["src_off"] = np.arange(n, dtype=np.int64) * Ss
+        descs["dst_off"] = wo + np.arange(n, dtype=np.int64) * Sw
+        descs["counter"] = (np.uint64(base) + np.arange(n, dtype=np.uint64))
+        descs["len"] = P
+        descs["key_slot"] = slot
+        want = np.full(n * Sw + wo + 64, 0xA5, np.uint8)
+        assert (o.seal_batch(descs, keys, kidx, src, want) == 0).all()
+        assert np.array_equal(wire.cpu().numpy(), want), f"strided seal {it}: n={n} P={P} Sw={Sw} wo={wo}"
+        back = torch.full((n * Sp + po + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+        st.fill_(-1)
+        gpu.open_strided(n, P + 32, slot, wire.data_ptr() + wo, Sw, back.data_ptr() + po, Sp, st)
+        torch.cuda.synchronize()
+        assert (st == 0).all(), (it, n, P)
+        exp = np.full(n * Sp + po + 64, 0x5A, np.uint8)
+        for i in range(n):
+            exp[po + i * Sp:po + i * Sp + P] = src[i * Ss:i * Ss + P]
+        assert np.array_equal(back.cpu().numpy(), exp), f"strided open {it}: n={n} P={P} Sp={Sp} po={po}"
+    for it in range(24):  # descriptor batches
+        ctx = gpu1 if it % 3 == 0 else gpu
+        nk = 1 if ctx is gpu1 else 4096
+        n = int(rng.integers(1, 3000))
+        affine = it % 2 == 1
+        if affine:
+            P = int(rng.choice([0, 64, 1350, 1400]))
+            sizes = np.full(n, P, np.int64)
+            S = synth.round_up(P + 32 + int(rng.choice([0, 16, 80])), 16)
+            soffs = 16 * int(rng.integers(0, 8)) + S * np.arange(n, dtype=np.int64)
+            doffs = 16 * int(rng.integers(0, 8)) + S * np.arange(n, dtype=np.int64)
+            src = np.zeros(int(soffs[-1]) + S + 64, np.uint8)
+            for i, p in enumerate(synth.host_payloads(sizes, seed=it)):
+                src[soffs[i]:soffs[i] + P] = np.frombuffer(p, np.uint8)
+            dst_size = int(doffs[-1]) + S + 64
+        else:
+            sizes = rng.choice([0, 1, 16, 64, 200, 576, 1350, 1500, 4000, 8900], n)
+            src, soffs = pack(synth.host_payloads(sizes, seed=100 + it))
+            soffs = np.array(soffs, np.int64)
+            doffs, pos = np.zeros(n, np.int64), 0
+            for i in rng.permutation(n):
+                doffs[i] = pos
+                pos = synth.round_up(pos + int(sizes[i]) + 32 + 16 * int(rng.integers(0, 3)), 16)
+            dst_size = pos + 64
+        descs = np.zeros(n, DESC)
+        descs["src_off"], descs["dst_off"], descs["len"] = soffs, doffs, sizes
+        descs["counter"] = rng.integers(0, 2**63, n, dtype=np.uint64)
+        descs["key_slot"] = rng.integers(0, nk, n).astype(np.uint32)
+        ordered = not affine and it % 4 == 0
+
+        def launch(seal, d, src_b, size, fill):
+            d_descs = to_dev(torch, d.view(np.uint8))
+            d_src = to_dev(torch, src_b)
+            d_dst = torch.full((max(size, 16),), fill, dtype=torch.uint8, device="cuda")
+            d_st = torch.full((len(d),), -1, dtype=torch.int32, device="cuda")
+            if ordered:
+                order = torch.zeros(len(d), dtype=torch.int32, device="cuda")
+                scratch = torch.zeros(262144 // 4, dtype=torch.int32, device="cuda")
+                ctx.plan_batch(seal, d_descs, len(d), order, scratch)
+                (ctx.seal_batch_ordered if seal else ctx.open_batch_ordered)(
+                    d_descs, order, len(d), d_src, d_dst, d_st)
+            else:
+                (ctx.seal_batch if seal else ctx.open_batch)(d_descs, len(d), d_src, d_dst, d_st)
+            torch.cuda.synchronize()
+            return d_dst.cpu().numpy(), d_st.cpu().numpy()
+
+        out, st = launch(True, descs, src, dst_size, 0xC3)
+        want = np.full(max(dst_size, 16), 0xC3, np.uint8)
+        assert (o.seal_batch(descs, keys[:nk], kidx[:nk], src, want) == 0).all()
+        assert (st == 0).all() and np.array_equal(out, want), f"desc seal {it}: n={n} affine={affine} nk={nk}"
+        d2 = np.zeros(n, DESC)
+        d2["src_off"], d2["dst_off"], d2["len"], d2["key_slot"] = doffs, soffs, sizes + 32, descs["key_slot"]
+        wire = out.copy()
+        bad = rng.choice(n, size=min(n, 3), replace=False)
+        wire[int(doffs[bad[0]]) + 16 + int(rng.integers(0, int(sizes[bad[0]]) + 16))] ^= 0x08
+        if len(bad) > 1:
+            wire[int(doffs[bad[1]]) + 4] ^= 0x80   # receiver index
+        back, st2 = launch(False, d2, wire, len(src), 0x3C)
+        want2 = np.full(max(len(src), 16), 0x3C, np.uint8)
+        wst2 = o.open_batch(d2, keys[:nk], kidx[:nk], wire, want2)
+        assert (st2 == wst2).all() and (wst2[bad[0]] == 10), f"desc open status {it}"
+        assert np.array_equal(back, want2), f"desc open {it}: n={n} affine={affine} nk={nk} ordered={ordered}"
