@@ -23,7 +23,10 @@ constexpr uint32_t kNoAccessOffset = 0x7ffffff0u;  // 4 waves per workgroup (des
 #define WG_STRIDED_THREADS (WG_SYNC ? 512 : 256)
 #endif
 constexpr uint32_t kStridedThreads = WG_STRIDED_THREADS;
-constexpr uint32_t kStridedMinWaves = 4;  // __launch_bounds__ waves per SIMD: 128-VGPR cap
+#ifndef WG_STRIDED_MIN_WAVES
+#define WG_STRIDED_MIN_WAVES 4
+#endif
+constexpr uint32_t kStridedMinWaves = WG_STRIDED_MIN_WAVES;  // __launch_bounds__ waves per SIMD: 128-VGPR cap
 #ifndef WG_STRIDED_BLOCKS_PER_CU
 #define WG_STRIDED_BLOCKS_PER_CU (4u * kStridedMinWaves * 64u / kStridedThreads)
 #endif
