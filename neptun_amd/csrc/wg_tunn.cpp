@@ -138,7 +138,15 @@ size_t chunk_bytes() {  // staging bytes per pipeline chunk (WG_TUNN_CHUNK_KB ov
   const char *e = std::getenv("WG_TUNN_CHUNK_KB");
   return e ? std::max<size_t>(64, (size_t)std::atol(e)) << 10 : size_t(16) << 20;
 }
-constexpr uint32_t kSets = 2;                     // double buffering
+constexpr uint32_t kSets = 4;                     // staging sets per engine (at most)
+// staging sets a pipeline uses (WG_TUNN_SETS overrides, 2..kSets): with n sets the
+// host unpacks chunk c - (n - 1) right after submitting chunk c, so n - 1 chunks
+// are queued on the GPU's streams while the host copies
+uint32_t pipeline_sets() {  // (read per call, like chunk_bytes())
+  const char *e = std::getenv("WG_TUNN_SETS");
+  const int x = e ? std::atoi(e) : 2;
+  return (uint32_t)std::min<int>(kSets, std::max(2, x));
+}
 
 // ---------------------------------------------------------------------------
 // NUMA placement of an engine's host side (each GPU gets its own
@@ -608,8 +616,9 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
   const size_t nc = E.chunks.size();
   const bool tr = trace_on();
   const double t0 = tr ? now_us() : 0.0;
+  const size_t sets = pipeline_sets();
   auto wait_unpack = [&](size_t c) -> int {
-    Staging &S = E.st[c % kSets];
+    Staging &S = E.st[c % sets];
     const double a = tr ? now_us() : 0.0;
     TUNN_HIP(hipEventSynchronize(S.done), "tunn: chunk wait");
     const double b = tr ? now_us() : 0.0;
@@ -621,9 +630,9 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
     return WG_RC_OK;
   };
   for (size_t c = 0; c < nc; ++c) {
-    Staging &S = E.st[c % kSets];
-    if (S.busy) {  // chunk c - kSets still owns this set
-      const int rc = wait_unpack(c - kSets);
+    Staging &S = E.st[c % sets];
+    if (S.busy) {  // chunk c - sets still owns this set
+      const int rc = wait_unpack(c - sets);
       if (rc) return rc;
     }
     const Chunk &ch = E.chunks[c];
@@ -661,13 +670,14 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
     TUNN_HIP(hipEventRecord(S.done, S.stream), "tunn: event");
     S.busy = true;
     if (const int rc = injected_failure(c)) return rc;
-    if (c >= 1 && E.st[(c - 1) % kSets].busy) {  // overlap: unpack c-1 while c runs
-      const int rc2 = wait_unpack(c - 1);
+    // overlap: unpack c - (sets - 1) while the chunks after it run
+    if (c + 1 >= sets && E.st[(c + 1 - sets) % sets].busy) {
+      const int rc2 = wait_unpack(c + 1 - sets);
       if (rc2) return rc2;
     }
   }
-  for (size_t c = nc >= kSets ? nc - kSets : 0; c < nc; ++c)
-    if (E.st[c % kSets].busy) {
+  for (size_t c = nc >= sets ? nc - sets : 0; c < nc; ++c)
+    if (E.st[c % sets].busy) {
       const int rc = wait_unpack(c);
       if (rc) return rc;
     }
