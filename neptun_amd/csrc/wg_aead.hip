@@ -118,6 +118,12 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #define WG_DESC_FULL_ROUNDS 0
 #endif
 
+// uniform kernels' persistent walk: each XCD's workgroups on one contiguous eighth of
+// the batch (A/B knob, off: profiles/r03v_ab_xcd_walk.txt)
+#ifndef WG_XCD_CONTIG
+#define WG_XCD_CONTIG 0
+#endif
+
 #ifndef WG_HDR_NT
 #define WG_HDR_NT 0  // open's early header fetch with the streaming (nt) policy
 #endif
@@ -1461,6 +1467,27 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   if (status_out) *status_out = job.status;
 }
 
+// The persistent kernels' walk over workgroup-sized packet groups: workgroup b
+// takes groups b, b + grid, ... (round-robin), or, with xcd (WG_XCD_CONTIG),
+// the workgroups of each XCD -- dispatched round-robin over the 8 XCDs, so b runs
+// on XCD b % 8 -- walk one contiguous eighth of the batch.  Either way the last
+// group is the last iteration of the workgroup that takes it.
+struct GroupWalk {
+  uint32_t first, end, step;
+  __device__ GroupWalk(uint32_t groups, bool xcd) {
+    if (xcd && gridDim.x % 8u == 0u) {
+      const uint32_t x = blockIdx.x % 8u, span = (groups + 7u) / 8u;
+      first = x * span + blockIdx.x / 8u;
+      end = min(groups, x * span + span);
+      step = gridDim.x / 8u;
+    } else {
+      first = blockIdx.x;
+      end = groups;
+      step = gridDim.x;
+    }
+  }
+};
+
 // ---------------------------------------------------------------------------
 // kernels: 4 independent waves per workgroup, each with its own LDS stage
 // ---------------------------------------------------------------------------
@@ -1539,7 +1566,12 @@ __device__ __forceinline__ void strided_body(const StridedParams &prm) {
       for (int j = 0; j < 8; ++j) sk.k[j] = __builtin_amdgcn_readfirstlane(w[j]);
       sk.sidx = __builtin_amdgcn_readfirstlane(prm.key_index[prm.key_slot]);
     }
+#if WG_XCD_CONTIG
+    const GroupWalk walk(groups, true);
+    for (uint32_t grp = walk.first; grp < walk.end; grp += walk.step) {
+#else
     for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+#endif
       const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
       // only the last group can be partial, and it is this workgroup's last
       // iteration: a wave without packets ends (ended waves leave the barrier)
@@ -1639,7 +1671,14 @@ __device__ __forceinline__ void desc_sync_body(const DescParams &prm) {
     for (int j = 0; j < 8; ++j) sk.k[j] = __builtin_amdgcn_readfirstlane(w[j]);
     sk.sidx = __builtin_amdgcn_readfirstlane(prm.key_index[0]);
   }
+  // (a plan's order is length-sorted: contiguous ranges would hand whole XCDs the
+  // long packets, so only unordered launches may take the XCD walk)
+#if WG_XCD_CONTIG
+  const GroupWalk walk(groups, kAffine);
+  for (uint32_t grp = walk.first; grp < walk.end; grp += walk.step) {
+#else
   for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+#endif
     const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
     // only the last group can lack waves; it is this workgroup's last iteration
     if (pkt0 >= prm.n) return;
