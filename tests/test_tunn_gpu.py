@@ -471,3 +471,63 @@ def test_multi_engine_split_matches_sequential_tunn(torch_cuda, monkeypatch, chu
     tg.close()
     for c in ctxs:
         c.close()
+
+
+def large_ipv4_udp_packet():
+    """create_large_ipv4_udp_packet (noise/mod.rs:846-853): etherparse IPv4 (192.168.1.2 ->
+    192.168.1.3, TTL 5) + UDP (5678 -> 23) around 1400 zero bytes = 1428 bytes."""
+    total = 20 + 8 + 1400
+    ip = bytearray(20)
+    ip[0], ip[2:4], ip[8], ip[9] = 0x45, struct.pack(">H", total), 5, 17
+    ip[12:16], ip[16:20] = bytes([192, 168, 1, 2]), bytes([192, 168, 1, 3])
+    s = sum(struct.unpack(">10H", bytes(ip)))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    ip[10:12] = struct.pack(">H", ~s & 0xFFFF)
+    udp = struct.pack(">HHHH", 5678, 23, 8 + 1400, 0)
+    return bytes(ip) + udp + bytes(1400)
+
+
+def test_long_running_streams_byte_accounting(gpu):
+    """test_long_running_streams (noise/mod.rs:1116-1140): 4,000,000 encapsulate ->
+    decapsulate round trips of one 1428-byte IPv4/UDP packet between two Tunns, after
+    which the reference asserts rx >= 1424 * 4M and tx >= 1424 * 4M (the u64 byte
+    counters).  Here as 16 batches of 250,000 through the batch ABI: every result Ok
+    and every plaintext back, tx == rx == 4M * (1428 + 32) exactly (message_data_len,
+    session.rs:357), and the sender's counter at 4M."""
+    import numpy as np
+    from neptun_amd.tunn import Tunn
+    pkt = large_ipv4_udp_packet()
+    P, W = len(pkt), len(pkt) + 32
+    a, b = Tunn(gpu, FIRST_SLOT), Tunn(gpu, FIRST_SLOT - 16)
+    k1, k2 = bytes(range(32)), bytes(range(32, 64))
+    a.install_session(21, 34, k2, k1, True)
+    b.install_session(34, 21, k1, k2, True)
+    n, batches = 250_000, 16
+    S = (W + 15) // 16 * 16
+    src = np.frombuffer(pkt, np.uint8).copy()           # one buffer, like the reference
+    wire = np.zeros(n * S, np.uint8)
+    out = np.zeros(n * S, np.uint8)
+    slots = np.arange(n, dtype=np.uint64) * S
+    src_ptrs = np.full(n, src.ctypes.data, np.uint64)
+    src_lens = np.full(n, P, np.uint32)
+    wire_ptrs = wire.ctypes.data + slots
+    caps = np.full(n, S, np.uint32)
+    wire_lens = np.full(n, W, np.uint32)
+    out_ptrs = out.ctypes.data + slots
+    want = np.frombuffer(pkt, np.uint8)
+    for _ in range(batches):
+        res = a.encapsulate_ptrs(src_ptrs, src_lens, wire_ptrs, caps)
+        assert all(r[0] == M.WRITE_TO_NETWORK and r[2] == W for r in res)
+        res = b.decapsulate_ptrs(wire_ptrs, wire_lens, out_ptrs, caps)
+        assert all(r[0] == M.WRITE_TO_TUNNEL and r[2] == P for r in res)
+        assert (out.reshape(n, S)[:, :P] == want).all()
+    total = n * batches
+    tx, _ = a.stats()
+    _, rx = b.stats()
+    assert rx >= 1424 * total and tx >= 1424 * total  # the reference's assertion
+    assert tx == rx == total * W
+    ctr, _ = a.session_counters(21 % 8)  # a's session: local index 21
+    assert ctr == total
+    a.close()
+    b.close()
