@@ -614,6 +614,10 @@ def run(args, factory=None, device_fn=None, device_count=None):
                              "verification; not the headline value"}
         if sampler:
             sustained["power"] = sampler.stop()
+            pw_e = sustained["power"].get("socket_power_from_energy_W")
+            if pw_e:  # package energy per packet round trip (seal + open), at the sustained rate
+                sustained["power"]["energy_uJ_per_packet_roundtrip"] = round(
+                    pw_e * (ms / k2) * 1e-3 / wl.packets * 1e6, 4)
     avg = {"seal": mean(seal_ms), "open": mean(open_ms)}
     mine = {"rank": rank, "local_rank": local, "elapsed_s": round(my_elapsed, 6),
             "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
