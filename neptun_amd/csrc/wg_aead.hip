@@ -127,6 +127,14 @@ constexpr uint32_t kWaves = kBlockThreads / 64;  // generic kernels
 #ifndef WG_HDR_NT
 #define WG_HDR_NT 0  // open's early header fetch with the streaming (nt) policy
 #endif
+// uniform open: each group's headers prefetched into the tag park during the
+// previous group (its round 1), when the tag lies wholly in the last round and a
+// stage chunk past the datagram is free there (the tag is then checked inside the
+// last round, and the park is free from round 1 on): the group start no longer
+// waits for a header fetch before its one-time key
+#ifndef WG_OPEN_HDR_PREFETCH
+#define WG_OPEN_HDR_PREFETCH 0
+#endif
 #ifndef WG_HDR_DMA
 #define WG_HDR_DMA 1  // uniform open: headers by LDS-DMA ahead of round 0, counted vmcnt(8) wait
 #endif
@@ -1043,9 +1051,10 @@ struct PacketJob {
 // kInDesc: uniform geometry inside a descriptor kernel (the affine groups).
 template <bool kSeal, bool kUniform, bool kSync, bool kUKey = false, bool kLaneKeys = false,
           bool kInDesc = false, class Stage, class Geom>
-__device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
+__device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
-                                         int32_t *status_out, const SessionKey *pre = nullptr) {
+                                         int32_t *status_out, const SessionKey *pre = nullptr,
+                                         uint64_t next_hdr = 0, bool hdr_ready = false) {
   // run grid (Ranges): kG = grid coordinate of text byte 0
   constexpr bool kText = Geom::kTextGrid;
   constexpr uint32_t kG = kText ? 0u : 16u;
@@ -1108,6 +1117,18 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   const uint32_t wt = kG + (P & ~15u);           // grid offset of the tail chunk
   uint32_t tailB[4] = {0, 0, 0, 0};              // seal: chunk after the tail chunk (tag rest)
   uint32_t tg[4] = {0, 0, 0, 0};                 // open: the received tag, bytes [W - 16, W)
+  // header prefetch (WG_OPEN_HDR_PREFETCH; wave- and workgroup-uniform: P and the
+  // round count are launch constants): the tag's chunks in the last round, and
+  // that round's chunk 7 past the datagram's grid end (the tag is parked there)
+  constexpr bool kPfBuild = !kSeal && kUniform && kSync && WG_HDR_DMA && WG_OPEN_HDR_PREFETCH &&
+                            Stage::kTagPark && !kInDesc && !kLaneKeys && !WG_ABLATE_NO_MEM;
+  bool pf = false;
+  uint32_t tag_bad = 0u;  // pf: the tag check's result, from the last round
+  if constexpr (kPfBuild) {
+    const uint32_t last = rounds - 1u, gend = W - (16u - kG);
+    pf = rounds >= 2u && (wt >> 7) == last && (q == 0u || ((wt + 16u) >> 7) == last) &&
+         gend <= kRun * last + 112u;
+  }
 
   auto one_time_key = [&]() {
     uint32_t ks[16];
@@ -1188,7 +1209,9 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       for (int j = 0; j < 4; ++j) t[j] |= bytes_at(w, (int)q + 4 * j);
     }
     if constexpr (Stage::kTagPark) {
-      if (ra == r) {
+      if (kPfBuild && pf) {  // (ra == rb == the last round: the whole tag at once)
+        if (ra == r) run[row + (7u ^ sw)] = make_uint4(t[0], t[1], t[2], t[3]);
+      } else if (ra == r) {
         S.tagp[lane] = make_uint4(t[0], t[1], t[2], t[3]);
       } else if (q && rb == r) {
         const uint4 o = S.tagp[lane];
@@ -1285,11 +1308,14 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // the compiler placed the header's use, and its wait, between the
         // pieces, issuing most of round 0's DMA a memory latency late.)  The
         // tag park is free until round 0's tag bytes land (open_keep_tail).
-        if (my_runs)
+        if (my_runs && !(kPfBuild && hdr_ready))
           dma_global<WG_HDR_NT != 0>(lds_offset(&S.tagp[0]), reinterpret_cast<const uint8_t *>(job.in_base - (16u - kG)));
         stage_in<kSeal>(run, g, lane, 0);  // exactly 8 pieces (round 0 is straight-line)
         u32x4 h;
-        if constexpr (kText && WG_TEXT_SPLIT)  // (16 load instructions per round)
+        if (kPfBuild && hdr_ready)  // (landed during the previous group: its rounds waited vmcnt(0))
+          asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                       : "=v"(h) : "v"(lds_offset(&S.tagp[lane])) : "memory");
+        else if constexpr (kText && WG_TEXT_SPLIT)  // (16 load instructions per round)
           asm volatile("s_waitcnt vmcnt(16)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
                        : "=v"(h) : "v"(lds_offset(&S.tagp[lane])) : "memory");
         else
@@ -1344,6 +1370,10 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 #if !WG_ABLATE_NO_MEM
       if (r > 0) stage_in<kSeal>(run, g, ln, r);
 #endif
+      if constexpr (kPfBuild) {  // the next group's headers into the (free) tag park
+        if (pf && r == 1u && next_hdr)
+          dma_global<WG_HDR_NT != 0>(lds_offset(&S.tagp[0]), reinterpret_cast<const uint8_t *>(next_hdr));
+      }
       WG_STAMP_AT(kSeal, r, 1);
       // descriptor batches: a round every live packet fills with ciphertext
       // (wave-uniform) runs without per-chunk length tests, tail masks or tag work
@@ -1384,6 +1414,18 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         if (my_runs && !WG_ABLATE_NO_CRYPT) {
           apply_chunk0<kSeal, kText>(run, ln, r, Pr, poly, ks_save);
           if (kSeal) seal_tail(run, r);
+        }
+      }
+      if constexpr (kPfBuild) {  // the tag check, from the parked chunk 7 (before zero_outside)
+        if (pf && r == rounds - 1u && my_runs) {
+          const uint32_t tl = tail_lane();
+          const uint4 tv = run[8u * tl + (7u ^ swz(tl))];
+          poly_block(poly, 0u, 0u, P, 0u);
+          uint32_t tag[4];
+          const uint4 sp = S.park[tl];
+          const uint32_t sk4[4] = {sp.x, sp.y, sp.z, sp.w};
+          poly_finish(poly, sk4, tag);
+          tag_bad = (tv.x ^ tag[0]) | (tv.y ^ tag[1]) | (tv.z ^ tag[2]) | (tv.w ^ tag[3]);
         }
       }
       if constexpr (kUniform) {
@@ -1434,18 +1476,22 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   }
 
   if (!kSeal && job.status == WG_STATUS_OK) {
-    poly_block(poly, 0u, 0u, P, 0u);
-    uint32_t tag[4];
-    const uint4 sp = S.park[lane];
-    const uint32_t s[4] = {sp.x, sp.y, sp.z, sp.w};
-    poly_finish(poly, s, tag);
     uint32_t diff = 0;
-    if constexpr (Stage::kTagPark) {
-      const uint4 o = S.tagp[lane];
-      tg[0] = o.x; tg[1] = o.y; tg[2] = o.z; tg[3] = o.w;
-    }
+    if (kPfBuild && pf) {
+      diff = tag_bad;  // (checked in the last round)
+    } else {
+      poly_block(poly, 0u, 0u, P, 0u);
+      uint32_t tag[4];
+      const uint4 sp = S.park[lane];
+      const uint32_t s[4] = {sp.x, sp.y, sp.z, sp.w};
+      poly_finish(poly, s, tag);
+      if constexpr (Stage::kTagPark) {
+        const uint4 o = S.tagp[lane];
+        tg[0] = o.x; tg[1] = o.y; tg[2] = o.z; tg[3] = o.w;
+      }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) diff |= tg[j] ^ tag[j];
+      for (int j = 0; j < 4; ++j) diff |= tg[j] ^ tag[j];
+    }
     if (diff) {
       // tag mismatch: never expose unauthenticated plaintext (ring open_within
       // zeroes it); the streamed stores of this wave land first (same wave, in order)
@@ -1465,6 +1511,7 @@ __device__ __forceinline__ void run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     }
   }
   if (status_out) *status_out = job.status;
+  return kPfBuild && pf && next_hdr != 0u;  // the next group's headers are in the tag park
 }
 
 // The persistent kernels' walk over workgroup-sized packet groups: workgroup b
@@ -1496,9 +1543,10 @@ struct GroupWalk {
 // left over (generic geometry), so the hot kernel carries no generic path.
 // one wave's 64 packets [pkt0, pkt0 + 64) of a strided batch
 template <bool kSeal, bool kTail, bool kText, class Stage>
-__device__ __forceinline__ void strided_group(Stage &stage, const StridedParams &prm,
+__device__ __forceinline__ bool strided_group(Stage &stage, const StridedParams &prm,
                                               uint32_t pkt0, uint32_t lane,
-                                              const SessionKey *sk = nullptr) {
+                                              const SessionKey *sk = nullptr,
+                                              uint64_t next_hdr = 0, bool hdr_ready = false) {
   const uint32_t i = pkt0 + lane;
   PacketJob job;
   job.slot = prm.key_slot;
@@ -1531,15 +1579,17 @@ __device__ __forceinline__ void strided_group(Stage &stage, const StridedParams 
         lds_wait_dma();
         stage_out<kSeal>(run, g, lane, r);
       }
-      return;
+      return false;
     }
 #endif
     // (the text grid exists only in the phase-locked form)
-    run_wave<kSeal, true, WG_SYNC != 0 || kText>(stage, g, lane, job, prm.keys, prm.key_index, st, sk);
+    return run_wave<kSeal, true, WG_SYNC != 0 || kText>(stage, g, lane, job, prm.keys, prm.key_index, st,
+                                                        sk, next_hdr, hdr_ready);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
     LdsGeom g{stage};
     run_wave<kSeal, false, false>(stage, g, lane, job, prm.keys, prm.key_index, st);
+    return false;
   }
 }
 
@@ -1566,18 +1616,38 @@ __device__ __forceinline__ void strided_body(const StridedParams &prm) {
       for (int j = 0; j < 8; ++j) sk.k[j] = __builtin_amdgcn_readfirstlane(w[j]);
       sk.sidx = __builtin_amdgcn_readfirstlane(prm.key_index[prm.key_slot]);
     }
+    bool hdr_ready = false;  // (WG_OPEN_HDR_PREFETCH) this group's headers already in the tag park
+    (void)hdr_ready;
 #if WG_XCD_CONTIG
     const GroupWalk walk(groups, true);
+#define WALK_STEP walk.step
+#define WALK_END walk.end
     for (uint32_t grp = walk.first; grp < walk.end; grp += walk.step) {
 #else
+#define WALK_STEP gridDim.x
+#define WALK_END groups
     for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
 #endif
       const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
       // only the last group can be partial, and it is this workgroup's last
       // iteration: a wave without packets ends (ended waves leave the barrier)
       if (pkt0 + 64u > prm.n) return;
+#if WG_OPEN_HDR_PREFETCH
+      // open: this lane's datagram in the wave's next group (0: none), whose header
+      // run_wave may prefetch into the tag park
+      uint64_t next_hdr = 0;
+      if constexpr (!kSeal) {
+        const uint32_t npkt0 = ((grp + WALK_STEP) * kWaves + wave) * 64u;
+        if (grp + WALK_STEP < WALK_END && npkt0 + 64u <= prm.n)
+          next_hdr = reinterpret_cast<uint64_t>(prm.src) + (uint64_t)(npkt0 + lane) * prm.src_stride;
+      }
+      hdr_ready = strided_group<kSeal, false, kText>(stage[wave], prm, pkt0, lane, &sk, next_hdr, hdr_ready);
+#else
       strided_group<kSeal, false, kText>(stage[wave], prm, pkt0, lane, &sk);
+#endif
     }
+#undef WALK_STEP
+#undef WALK_END
   }
 }
 

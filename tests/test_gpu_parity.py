@@ -1243,3 +1243,62 @@ def test_randomized_launch_shapes_match_oracle(torch_cuda, gpu, gpu1):
         wst2 = o.open_batch(d2, keys[:nk], kidx[:nk], wire, want2)
         assert (st2 == wst2).all() and (wst2[bad[0]] == 10), f"desc open status {it}"
         assert np.array_equal(back, want2), f"desc open {it}: n={n} affine={affine} nk={nk} ordered={ordered}"
+
+
+@pytest.mark.parametrize("grid", ["wire_padded", "text"])
+def test_full_size_open_failures_in_every_group(torch_cuda, gpu, grid):
+    """1M x 1350 B opened with failures spread over the whole batch -- so every
+    persistent workgroup meets them in its later groups too (each walks 4 groups at
+    this size): flipped ciphertext and tag bytes (InvalidAeadTag, plaintext zeroed),
+    wrong receiver index and wrong message type (the packet left untouched).  Wire grid
+    with slot padding (the bench's open) and NepTUN's offset-0 open (text grid); every
+    other packet back bit for bit, statuses equal to the oracle's on sampled packets."""
+    torch = torch_cuda
+    n, P, S = 1 << 20, 1350, 1408
+    keys = synth.keys(1, seed=31)
+    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    rng = np.random.default_rng(31)
+    pt = synth.device_payloads(n, P, S, "cuda", offset=16)
+    wire = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    gpu.seal_strided(n, P, 0, 5, pt.data_ptr() + 16, S, wire, S, st)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    picks = rng.choice(n, size=4000, replace=False)
+    ct_bad, tag_bad, idx_bad, type_bad = np.array_split(picks, 4)
+    w = wire.view(n, S)
+    for rows, off in ((ct_bad, rng.integers(16, 16 + P, len(ct_bad))),
+                      (tag_bad, rng.integers(16 + P, 32 + P, len(tag_bad)))):
+        r_t, c_t = torch.from_numpy(rows).cuda(), torch.from_numpy(off).cuda()
+        w[r_t, c_t] ^= 0x20
+    w[torch.from_numpy(idx_bad).cuda(), 4] ^= 0x01
+    w[torch.from_numpy(type_bad).cuda(), 0] = 2
+    back = torch.full((n * S,), 0xCD, dtype=torch.uint8, device="cuda")
+    st.fill_(-1)
+    o_off = 16 if grid == "wire_padded" else 0
+    gpu.set_slot_padding(grid == "wire_padded")
+    try:
+        gpu.open_strided(n, P + 32, 0, wire, S, back.data_ptr() + o_off, S, st)
+        torch.cuda.synchronize()
+    finally:
+        gpu.set_slot_padding(False)
+    s_h = st.cpu().numpy()
+    aead = np.concatenate([ct_bad, tag_bad])
+    assert (s_h[aead] == 10).all(), np.unique(s_h[aead])          # InvalidAeadTag + 1
+    assert (s_h[idx_bad] == 5).all() and (s_h[type_bad] != 0).all()  # WrongIndex + 1
+    good = np.ones(n, bool)
+    good[picks] = False
+    assert (s_h[good] == 0).all()
+    b2 = back.view(n, S)
+    g_t = torch.from_numpy(np.nonzero(good)[0]).cuda()
+    assert torch.equal(b2[g_t, o_off:o_off + P], pt.view(n, S)[g_t, 16:16 + P])
+    assert not bool(b2[torch.from_numpy(aead).cuda(), o_off:o_off + P].any()), "failed tags not zeroed"
+    nogo = torch.from_numpy(np.concatenate([idx_bad, type_bad])).cuda()
+    assert bool((b2[nogo, o_off:o_off + P] == 0xCD).all()), "refused packets written"
+    # the oracle agrees on a sample of each kind
+    wh = wire.view(n, S)
+    for rows in (ct_bad[:8], tag_bad[:8], idx_bad[:8], good.nonzero()[0][:: n // 16]):
+        for r in rows:
+            code, _ = o.receive_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX,
+                                            wh[int(r), :P + 32].cpu().numpy().tobytes())
+            assert code == int(s_h[r]), (int(r), code, int(s_h[r]))
