@@ -38,6 +38,7 @@ def main():
     ctx.set_keys(0, synth.keys(1, seed=seed), np.array([synth.RECEIVER_IDX], np.uint32))
     stats = {"seed": seed, "iterations": 0, "packets": 0, "bytes": 0, "mismatches": [], "forms": {}}
     t_end = time.time() + seconds
+    last_print = time.time()
     it = 0
     while time.time() < t_end:
         it += 1
@@ -105,6 +106,11 @@ def main():
             bad.append({"what": "open bytes"})
         stats["iterations"] += 1
         stats["packets"] += 2 * n
+        if time.time() - last_print > 30:  # progress (a long soak must not look hung)
+            last_print = time.time()
+            print(json.dumps({"progress_s": round(seconds - (t_end - last_print), 1),
+                              "iterations": stats["iterations"], "packets": stats["packets"],
+                              "mismatches": len(stats["mismatches"])}), flush=True)
         stats["bytes"] += 2 * int(sizes.sum())
         if bad:
             stats["mismatches"].append({"iteration": it, "n": n, "mixed": mixed, "stride": S, "problems": bad})
