@@ -7,7 +7,8 @@ forms the host picks for that launch) -- and require the two destination
 buffers, canaries included, to be byte-identical; open both back and require
 the plaintext, statuses and untouched canaries; every few iterations also a
 mixed-length descriptor batch through the plan (ordered launch) against its
-unordered twin.  A one-in-a-million corruption in any form shows up as a
+unordered twin, and every third a batch with a random key slot per packet (a
+4096-slot table: the affine descriptor kernel against the plan-ordered one).  A one-in-a-million corruption in any form shows up as a
 mismatch between forms that share no kernel.  Prints one JSON summary line.
 
     python tools/stress.py [SECONDS] [OUT.json]
@@ -34,8 +35,12 @@ def main():
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(int(time.time()) & 0xFFFF)
     seed = int(rng.integers(1 << 30))
-    ctx = neptun_amd.GpuContext(0, key_slots=1)
-    ctx.set_keys(0, synth.keys(1, seed=seed), np.array([synth.RECEIVER_IDX], np.uint32))
+    ctx1 = neptun_amd.GpuContext(0, key_slots=1)
+    ctx1.set_keys(0, synth.keys(1, seed=seed), np.array([synth.RECEIVER_IDX], np.uint32))
+    # per-packet keys (config 4's shape): a 4096-slot table, random slot per packet
+    ctxk = neptun_amd.GpuContext(0, key_slots=4096)
+    ctxk.set_keys(0, synth.keys(4096, seed=seed + 1),
+                  np.full(4096, synth.RECEIVER_IDX, np.uint32) + np.arange(4096, dtype=np.uint32))
     stats = {"seed": seed, "iterations": 0, "packets": 0, "bytes": 0, "mismatches": [], "forms": {}}
     t_end = time.time() + seconds
     last_print = time.time()
@@ -43,6 +48,8 @@ def main():
     while time.time() < t_end:
         it += 1
         mixed = it % 5 == 0
+        keyed = it % 3 == 0 and not mixed  # per-packet keys: two descriptor forms, no strided one
+        ctx = ctxk if keyed else ctx1
         n = int(rng.choice([64, 4096, 65536, 262144, 1 << 20])) + int(rng.integers(0, 64))
         if mixed:
             n = min(n, 200000)
@@ -60,9 +67,11 @@ def main():
         descs["dst_off"] = np.arange(n, dtype=np.int64) * S
         descs["counter"] = ctr0 + np.arange(n, dtype=np.uint64)
         descs["len"] = sizes
+        if keyed:
+            descs["key_slot"] = rng.integers(0, 4096, n).astype(np.uint32)
         d_descs = torch.from_numpy(descs.view(np.uint8)).to(dev)
         outs, sts = [], []
-        forms = ["desc-ordered", "desc"] if mixed else ["strided", "desc"]
+        forms = ["desc-ordered", "desc"] if (mixed or keyed) else ["strided", "desc"]
         for form in forms:
             w = torch.full((n * S + 64,), 0xA5, dtype=torch.uint8, device=dev)
             st = torch.full((n,), -1, dtype=torch.int32, device=dev)
@@ -77,7 +86,8 @@ def main():
                 ctx.seal_batch(d_descs, n, pt, w, st)
             outs.append(w)
             sts.append(st)
-            stats["forms"][form] = stats["forms"].get(form, 0) + 1
+            tag = form + ("-keyed" if keyed else "")
+            stats["forms"][tag] = stats["forms"].get(tag, 0) + 1
         torch.cuda.synchronize()
         bad = []
         if not torch.equal(outs[0], outs[1]):
@@ -90,7 +100,7 @@ def main():
         d2["len"] = sizes + 32
         back = torch.full((n * S + 64,), 0x5A, dtype=torch.uint8, device=dev)
         st2 = torch.full((n,), -1, dtype=torch.int32, device=dev)
-        if mixed:
+        if mixed or keyed:
             ctx.open_batch(torch.from_numpy(d2.view(np.uint8)).to(dev), n, outs[0], back, st2)
         else:
             ctx.open_strided(n, int(sizes[0]) + 32, 0, outs[0], S, back, S, st2)
@@ -113,7 +123,8 @@ def main():
                               "mismatches": len(stats["mismatches"])}), flush=True)
         stats["bytes"] += 2 * int(sizes.sum())
         if bad:
-            stats["mismatches"].append({"iteration": it, "n": n, "mixed": mixed, "stride": S, "problems": bad})
+            stats["mismatches"].append({"iteration": it, "n": n, "mixed": mixed, "keyed": keyed, "stride": S,
+                                        "problems": bad})
             if len(stats["mismatches"]) > 5:
                 break
         del pt, outs, back
