@@ -7,8 +7,8 @@ resulting 1M datagrams (receive_packet_data, session.rs:265-302), all in HBM
 (BASELINE config 2 per GPU; with --gpus 8 it is config 5: 8M packets, 1M per
 GPU, contiguous shards, no collective on the data path -> "scaling": "weak").
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+    python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: starts N ranks itself)
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU; N must match)
     python bench.py --config 3|4   (supplementary lines for DESIGN.md)
 
 Rank 0 prints one JSON line.  value = Gbit/s of plaintext round-trip goodput
@@ -521,6 +521,13 @@ def run(args, factory=None, device_fn=None, device_count=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        # a launcher's world and the flag disagree: publishing either count would lie
+        if rank == 0:
+            print(json.dumps({"error": f"--gpus {args.gpus} but WORLD_SIZE={world}: the rank count "
+                                       "must equal --gpus", "n_gpus": world, "gpus_flag": args.gpus}),
+                  flush=True)
+        return 2
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     visible = torch.cuda.device_count() if device_count is None else device_count
@@ -713,8 +720,57 @@ def run(args, factory=None, device_fn=None, device_count=None):
     return 0 if ok else 1
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_local(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this same
+    script, one per GPU (the reference's one worker per core, packet_workers.rs:113-131,
+    becomes one rank per GPU), with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set the
+    way torchrun sets them.  Nothing here touches the GPU (children are started, never
+    exec'd into); rank 0 prints the line.  If a rank dies, the others are stopped
+    instead of waiting at a barrier.  Returns the worst exit code."""
+    env0 = dict(os.environ, WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(_free_port()), LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
+    rcs: dict[int, int] = {}
+    failed_at = None
+    while len(rcs) < n:
+        for r, p in enumerate(procs):
+            if r not in rcs and p.poll() is not None:
+                rcs[r] = p.returncode
+                if p.returncode != 0 and failed_at is None:
+                    failed_at = time.time()
+        if failed_at is not None and time.time() - failed_at > 30:
+            for r, p in enumerate(procs):  # the exact children started above
+                if r not in rcs:
+                    p.kill()
+        time.sleep(0.05)
+    bad = [rc for rc in rcs.values() if rc != 0]
+    return max(bad, key=abs) if bad else 0
+
+
 def main():
-    sys.exit(run(parse()))
+    args = parse()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus > 1:
+        sys.exit(launch_local(args.gpus, sys.argv[1:]))
+    hook = os.environ.get("BENCH_FAKE_DEVICE")
+    if hook:  # test-only: the CPU stand-in of tests/bench_fake.py (never on a GPU run)
+        import importlib
+        m = importlib.import_module(hook)
+        sys.exit(run(args, factory=m.FakeWorkload, device_fn=m.cpu_device,
+                     device_count=int(os.environ.get("BENCH_FAKE_GPUS", args.gpus))))
+    sys.exit(run(args))
 
 
 if __name__ == "__main__":

@@ -402,8 +402,11 @@ struct DescGeom {
       const uint64_t ia = anchor(in_base, l0), oa = anchor(out_base, l0);
       const uint64_t io = in_base - ia, oo = out_base - oa;
       // every byte a staged packet moves (its extent + a 16-byte tail chunk)
-      // stays below kNoAccess, and kNoAccess + 128 r never wraps
-      const bool far = ok && (io + ihi + 16u >= kNoAccessOffset - 1024u ||
+      // stays below kNoAccess, and kNoAccess + 128 r never wraps; a packet
+      // more than 1 GiB below the anchor would wrap io / oo:
+      // such a wave takes the generic path
+      const bool far = ok && (in_base < ia || out_base < oa ||
+                              io + ihi + 16u >= kNoAccessOffset - 1024u ||
                               oo + ohi + 16u >= kNoAccessOffset - 1024u);
       fast = __ballot(far) == 0ull;
       if (fast) {

@@ -13,52 +13,7 @@ import time
 
 import pytest
 import torch.multiprocessing as mp
-
-
-class CpuEvent:
-    def __init__(self):
-        self.t = None
-
-    def record(self, stream=None):
-        self.t = time.perf_counter()
-
-    def elapsed_time(self, other):
-        return (other.t - self.t) * 1e3
-
-
-def cpu_device(local):
-    return "cpu", None, (lambda: None), CpuEvent
-
-
-class FakeWorkload:
-    """Same interface as bench.StridedWorkload; rank r sleeps (r+1) ms per step."""
-
-    def __init__(self, args, dev, rank, world):
-        self.rank = rank
-        self.packets = 1000 * (rank + 1)
-        self.payload_bytes = 1350 * self.packets
-        self.launch_bytes = {"seal": 2732 * self.packets, "open": 2732 * self.packets}
-        self.kernels = {"seal": "fake_seal", "open": "fake_open"}
-        self.fail = os.environ.get("FAKE_FAIL_RANK") == str(rank)
-
-    def step(self, stream, evs=None):
-        if evs:
-            evs[0].record()
-        time.sleep(0.001 * (self.rank + 1))
-        if evs:
-            evs[1].record()
-        time.sleep(0.0005)
-        if evs:
-            evs[2].record()
-
-    def verify(self):
-        return not self.fail
-
-    def describe(self, world):
-        return {"workload": "fake", "parallelism": f"{world} shard(s), no collective"}
-
-    def close(self):
-        pass
+from bench_fake import FakeWorkload, cpu_device
 
 
 def _worker(rank, world, port, outdir, fail_rank, device_count=None):
@@ -69,7 +24,7 @@ def _worker(rank, world, port, outdir, fail_rank, device_count=None):
     if fail_rank is not None:
         os.environ["FAKE_FAIL_RANK"] = str(fail_rank)
     import bench
-    args = bench.parse(["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--sustain-seconds", "0.05"])
+    args = bench.parse(["--gpus", str(world), "--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--sustain-seconds", "0.05"])
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
         rc = bench.run(args, factory=FakeWorkload, device_fn=cpu_device,
@@ -172,3 +127,64 @@ def test_limiter_label_needs_the_power_limit():
     assert bench.power_limiter(dict(pw, socket_power_W=1323.0)) is None
     assert bench.power_limiter(dict(pw, ppt_violation=["NOT ACTIVE"])) is None
     assert bench.power_limiter({}) is None
+
+
+def _bench_cli(args, extra_env=None, timeout=120):
+    """Run `python bench.py ...` as a real command (the driver's form) with the CPU
+    stand-in injected through BENCH_FAKE_DEVICE; returns (rc, stdout lines)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(BENCH_FAKE_DEVICE="tests.bench_fake", **(extra_env or {}))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], cwd=root, env=env,
+                         capture_output=True, text=True, timeout=timeout)
+    return out.returncode, [x for x in out.stdout.splitlines() if x.startswith("{")]
+
+
+COMMON = ["--steps", "5", "--warmup", "1", "--no-cpu-baseline", "--sustain-seconds", "0.05"]
+
+
+def test_gpus_flag_starts_that_many_ranks():
+    """`bench.py --gpus 2` with no launcher starts two rank processes
+    itself and prints ONE line for both: n_gpus 2, two per_rank entries, the slower
+    rank's time, the two shards' payload summed."""
+    rc, lines = _bench_cli(["--gpus", "2", *COMMON])
+    assert rc == 0 and len(lines) == 1, lines
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and len(line["per_rank"]) == 2
+    assert [r["rank"] for r in line["per_rank"]] == [0, 1]
+    assert line["packets_per_step"] == 3000 and line["ms_per_step"] >= 2.5
+
+
+def test_gpus_flag_one_is_a_single_rank():
+    rc, lines = _bench_cli(["--gpus", "1", *COMMON])
+    assert rc == 0 and len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and "per_rank" not in line
+
+
+def test_gpus_flag_and_launcher_world_must_agree():
+    """A launcher's WORLD_SIZE that differs from --gpus is refused with an error line."""
+    rc, lines = _bench_cli(["--gpus", "8", *COMMON],
+                           extra_env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2
+    line = json.loads(lines[0])
+    assert "error" in line and line["n_gpus"] == 1 and line["gpus_flag"] == 8
+
+
+def test_gpus_flag_refuses_more_ranks_than_gpus():
+    """--gpus 2 on a node with one visible GPU: the ranks refuse (rc 2, one error line)."""
+    rc, lines = _bench_cli(["--gpus", "2", *COMMON], extra_env={"BENCH_FAKE_GPUS": "1"})
+    assert rc == 2 and len(lines) == 1
+    assert json.loads(lines[0])["visible_gpus"] == 1
+
+
+def test_gpus_flag_a_dead_rank_ends_the_run():
+    """A rank that dies before the start barrier does not leave the others waiting:
+    the launcher stops them and exits non-zero."""
+    t0 = time.time()
+    rc, lines = _bench_cli(["--gpus", "2", *COMMON], extra_env={"FAKE_CRASH_RANK": "1"})
+    assert rc != 0
+    assert time.time() - t0 < 100

@@ -1302,3 +1302,71 @@ def test_full_size_open_failures_in_every_group(torch_cuda, gpu, grid):
             code, _ = o.receive_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX,
                                             wh[int(r), :P + 32].cpu().numpy().tobytes())
             assert code == int(s_h[r]), (int(r), code, int(s_h[r]))
+
+
+@pytest.mark.parametrize("form", ["per_lane", "key1", "ordered"])
+def test_descriptor_packets_below_the_fast_anchor(torch_cuda, gpu, gpu1, form):
+    """the descriptor kernels' fast addressing anchors each wave at
+    its first staged packet - 1 GiB.  A packet of the same wave that starts just below
+    that anchor and ends past it (lanes 1 of these waves, 16 .. 1344 bytes below it on
+    both the input and the output side) must not take the 32-bit fast path (its offset
+    would wrap) -- sealed and opened bit-exact against the oracle, with every byte
+    outside the packets left at its canary value, in the per-lane, one-slot (SGPR
+    key) and plan-ordered kernel forms."""
+    torch = torch_cuda
+    ctx = gpu1 if form == "key1" else gpu
+    rng = np.random.default_rng(404)
+    nk = 1 if ctx is gpu1 else 64
+    keys = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+    kidx = rng.integers(0, 2**32, nk, dtype=np.uint64).astype(np.uint32)
+    ctx.set_keys(0, keys, kidx)
+    P, S, GiB = 1350, 1408, 1 << 30
+    H = GiB + (1 << 20)            # lane 0 of every wave lives above 1 GiB
+    deltas = [-16, -48, -512, -1344]
+    n = 64 * len(deltas)
+    offs = np.zeros(n, np.int64)
+    for w, dl in enumerate(deltas):
+        for lane in range(64):
+            offs[64 * w + lane] = H + (64 * w + lane) * S
+        offs[64 * w + 1] = offs[64 * w] - GiB + dl   # straddles the wave's anchor
+    size = int(offs.max()) + S + 4096
+    payloads = synth.host_payloads(np.full(n, P), seed=405)
+    src = np.full(size, 0x11, np.uint8)
+    for i in range(n):
+        src[offs[i]:offs[i] + P] = np.frombuffer(payloads[i], np.uint8)
+    descs = np.zeros(n, DESC)
+    descs["src_off"], descs["dst_off"], descs["len"] = offs, offs, P
+    descs["counter"] = rng.integers(0, 2**63, n, dtype=np.uint64)
+    descs["key_slot"] = rng.integers(0, nk, n).astype(np.uint32)
+
+    def launch(seal, d, src_b, fill):
+        d_descs = to_dev(torch, d.view(np.uint8))
+        d_src = to_dev(torch, src_b)
+        d_dst = torch.full((size,), fill, dtype=torch.uint8, device="cuda")
+        d_st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        if form == "ordered":
+            order = torch.zeros(n, dtype=torch.int32, device="cuda")
+            scratch = torch.zeros(262144 // 4, dtype=torch.int32, device="cuda")
+            ctx.plan_batch(seal, d_descs, n, order, scratch)
+            (ctx.seal_batch_ordered if seal else ctx.open_batch_ordered)(
+                d_descs, order, n, d_src, d_dst, d_st)
+        else:
+            (ctx.seal_batch if seal else ctx.open_batch)(d_descs, n, d_src, d_dst, d_st)
+        torch.cuda.synchronize()
+        del d_src
+        return d_dst, d_st.cpu().numpy()
+
+    wire_d, st = launch(True, descs, src, 0xC3)
+    want = np.full(size, 0xC3, np.uint8)
+    assert (o.seal_batch(descs, keys, kidx, src, want) == 0).all()
+    assert (st == 0).all(), np.unique(st)
+    assert torch.equal(wire_d, to_dev(torch, want)), "sealed bytes (or canaries) differ from the oracle"
+    d2 = descs.copy()
+    d2["len"] = P + 32
+    wire = wire_d.cpu().numpy()
+    del wire_d
+    back_d, st2 = launch(False, d2, wire, 0x3C)
+    want2 = np.full(size, 0x3C, np.uint8)
+    assert (o.open_batch(d2, keys, kidx, wire, want2) == 0).all()
+    assert (st2 == 0).all(), np.unique(st2)
+    assert torch.equal(back_d, to_dev(torch, want2)), "opened bytes (or canaries) differ from the oracle"
