@@ -37,8 +37,14 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
-    ap.add_argument("--packets", type=int, default=1 << 20, help="config 2: packets per GPU")
+    ap.add_argument("--packets", type=int, default=0,
+                    help="config 2: packets per GPU (0 = 1M at 1350 B; other --size values keep the "
+                         "same payload bytes per step, 1M x 1350 B, rounded to whole 512-packet groups)")
     ap.add_argument("--size", type=int, default=1350)
+    ap.add_argument("--op", default="roundtrip", choices=("roundtrip", "seal", "open"),
+                    help="config 2: what one step runs -- seal then open (BASELINE's headline), or only "
+                         "the seal (the reference's own AEAD bench, chacha20poly1305_benching.rs:37-55) "
+                         "or only the open of a batch sealed before timing")
     ap.add_argument("--stride", type=int, default=0, help="config 2 slot stride (0 = round up to 128)")
     ap.add_argument("--layout", default="slots", choices=("slots", "neptun"),
                     help="config 2 buffers: 'slots' = datagram at slot+0 / plaintext at slot+16 on both "
@@ -89,7 +95,8 @@ class StridedWorkload:
 
         import neptun_amd
         from tools import synth
-        self.n, self.P = n, P = args.packets, args.size
+        self.n, self.P = n, P = packets_for(args), args.size
+        self.op = getattr(args, "op", "roundtrip")
         S = args.stride or synth.round_up(P + 32, 128)
         if S % 16 or S < P + 32:
             raise SystemExit("--stride must be a multiple of 16 and hold P + 32 bytes")
@@ -124,25 +131,33 @@ class StridedWorkload:
         self.kernels = {"seal": "aead_strided_kernel<true, false>",
                         "open": "aead_strided_open_text_kernel" if self.layout == "neptun"
                         else "aead_strided_kernel<false, false>"}
-        # the committed PMC summaries were profiled on the default shape only
-        default_shape = n == 1 << 20 and P == 1350 and S == synth.round_up(P + 32, 128) and (
+        # the committed PMC summaries were profiled per size on the default slot shape
+        default_shape = n == packets_for(args) and S == synth.round_up(P + 32, 128) and (
             self.layout == "neptun" or self.pad)
-        self.profile_tag = (("config2_neptun" if self.layout == "neptun" else "config2")
-                            if default_shape else None)
+        base = "config2_neptun" if self.layout == "neptun" else "config2"
+        self.profile_tag = (base if P == 1350 else f"{base}_p{P}") if default_shape else None
 
     def _seal_src(self):
         return (self.wire if self.layout == "neptun" else self.pt).data_ptr() + 16
+
+    def prepare(self, stream):
+        """--op open: seal the batch once, untimed, so every timed step opens it."""
+        if self.op == "open":
+            self.ctx.seal_strided(self.n, self.P, 0, self.counter_base, self._seal_src(), self.S,
+                                  self.wire, self.S, self.st_seal, stream)
 
     def step(self, stream, evs=None):
         S, P, n = self.S, self.P, self.n
         if evs:
             evs[0].record(stream)
-        self.ctx.seal_strided(n, P, 0, self.counter_base, self._seal_src(), S, self.wire, S,
-                              self.st_seal, stream)
+        if self.op != "open":
+            self.ctx.seal_strided(n, P, 0, self.counter_base, self._seal_src(), S, self.wire, S,
+                                  self.st_seal, stream)
         if evs:
             evs[1].record(stream)
-        self.ctx.open_strided(n, P + 32, 0, self.wire, S, self.back.data_ptr() + self.open_off, S,
-                              self.st_open, stream)
+        if self.op != "seal":
+            self.ctx.open_strided(n, P + 32, 0, self.wire, S, self.back.data_ptr() + self.open_off, S,
+                                  self.st_open, stream)
         if evs:
             evs[2].record(stream)
 
@@ -154,7 +169,12 @@ class StridedWorkload:
             # the original plaintext, then check that one
             self.wire.copy_(self.pt)
             self.back.zero_()
-            self.step(None)
+            self.ctx.seal_strided(n, P, 0, self.counter_base, self._seal_src(), S, self.wire, S,
+                                  self.st_seal)
+            self.ctx.open_strided(n, P + 32, 0, self.wire, S, self.back.data_ptr() + o, S, self.st_open)
+            torch.cuda.synchronize()
+        elif self.op == "seal":  # (the seal-only steps: open once, untimed, to check them)
+            self.ctx.open_strided(n, P + 32, 0, self.wire, S, self.back.data_ptr() + o, S, self.st_open)
             torch.cuda.synchronize()
         ok = int((self.st_seal != 0).sum()) == 0 and int((self.st_open != 0).sum()) == 0
         return ok and torch.equal(self.back.view(n, S)[:, o:o + P], self.pt.view(n, S)[:, 16:16 + P])
@@ -175,8 +195,13 @@ class StridedWorkload:
                  wire[j, :self.P + 32].tobytes()) for j, i in enumerate(idx)]
 
     def describe(self, world):
-        d = {"workload": f"BASELINE config {'2' if world == 1 else '5'}: {self.n} x {self.P} B "
-                         "packets per GPU, single session, seal then open, device-resident",
+        what = {"roundtrip": "seal then open", "seal": "seal only (the reference's AEAD bench shape)",
+                "open": "open only (of a batch sealed before timing)"}[self.op]
+        cfg = ('2' if world == 1 else '5') if self.P == 1350 and self.op == "roundtrip" else \
+            f"{'2' if world == 1 else '5'} shape at {self.P} B"
+        d = {"workload": f"BASELINE config {cfg}: {self.n} x {self.P} B "
+                         f"packets per GPU, single session, {what}, device-resident",
+             "op": self.op,
              "packets_per_gpu": self.n, "packet_bytes": self.P, "slot_stride": self.S,
              "global_packets": world * self.n, "parallelism": f"{world} shard(s), no collective",
              "layout": self.layout,
@@ -279,6 +304,15 @@ class DescWorkload:
         self.ctx.close()
 
 
+def packets_for(args) -> int:
+    """config 2 packets per GPU: --packets, else 1M x 1350 B worth of payload at --size."""
+    if args.packets:
+        return args.packets
+    if args.size == 1350:
+        return 1 << 20
+    return max(512, (((1 << 20) * 1350 // max(args.size, 1)) // 512) * 512)
+
+
 def make_workload(args, dev, rank, world):
     return StridedWorkload(args, dev, rank, world) if args.config == 2 else DescWorkload(
         args, dev, rank, world)
@@ -375,7 +409,7 @@ def power_limiter(pw: dict) -> str | None:
     return None
 
 
-def cpu_baseline(threads: int, cpus: dict, curve=()) -> dict:
+def cpu_baseline(threads: int, cpus: dict, curve=(), size: int = 1350, op: str = "roundtrip") -> dict:
     """Config 1 on the host cores: oracle/build/cpu_baseline (NepTUN framing over
     OpenSSL EVP, the stand-in for ring's asm; see oracle/cpu_baseline.c), one
     session and 64 Ki x 1350 B packets per worker thread like packet_workers.rs:113-131
@@ -387,41 +421,53 @@ def cpu_baseline(threads: int, cpus: dict, curve=()) -> dict:
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
 
+    # config 1: 64 Ki x 1350 B per worker; at other sizes the same payload bytes per worker
+    per_thread = 65536 if size == 1350 else max(1024, 65536 * 1350 // max(size, 1))
+    # which figure is the baseline: the round trip (median wall), or the op run alone
+    key = {"roundtrip": "gbps", "seal": "seal_gbps_best", "open": "open_gbps_best"}[op]
+
     def run(t, reps):
-        out = subprocess.run([exe, "--impl", "openssl", "--threads", str(t), "--packets-per-thread", "65536",
-                              "--reps", str(reps), "--pin"], capture_output=True, text=True, timeout=300)
+        out = subprocess.run([exe, "--impl", "openssl", "--threads", str(t), "--packets-per-thread",
+                              str(per_thread), "--size", str(size), "--reps", str(reps), "--pin"],
+                             capture_output=True, text=True, timeout=300)
         if out.returncode:
             raise RuntimeError(out.stderr)
-        return json.loads(out.stdout)
+        r = json.loads(out.stdout)
+        r["gbps_op"] = r[key]
+        return r
 
     one = run(1, 11)
-    pts = {1: one["gbps"]}
+    pts = {1: one["gbps_op"]}
     for t in sorted({int(c) for c in curve if 1 < int(c) < threads}):
-        pts[t] = run(t, 9)["gbps"]
+        pts[t] = run(t, 9)["gbps_op"]
     many = run(threads, 9)
-    pts[threads] = many["gbps"]
-    eff = {t: g / t / one["gbps"] for t, g in pts.items()}
+    pts[threads] = many["gbps_op"]
+    eff = {t: g / t / one["gbps_op"] for t, g in pts.items()}
     # the all-core figure scales the per-core rate of the largest measured count
     # that still scaled (>= 0.8 of one core's rate per core): past it the job's
     # share of a machine other jobs also load is what gets measured
     t_ok = max(t for t, e in eff.items() if e >= 0.8)
     all_cores = threads >= cpus["physical_cores"]  # (a share that covers every core: measured)
     out = {
-        "value": round(many["gbps"], 3),
+        "value": round(many["gbps_op"], 3),
         "unit": "Gbit/s",
         "cores": threads,
         "kind": "port",
         "cpu_model": cpus["model"],
         "physical_cores": cpus["physical_cores"],
         "allowed_cpus": cpus["allowed_cpus"],
-        "sample": (f"config 1 per worker: 65536 x 1350 B encap+decap round trip per thread, one session "
+        "sample": (f"config 1 per worker: {per_thread} x {size} B encap+decap per thread ("
+                   f"{ {'roundtrip': 'round-trip wall time', 'seal': 'best seal time', 'open': 'best open time'}[op] }"
+                   f" is the figure), one session "
                    f"per thread, NepTUN framing (session.rs:205-302) over OpenSSL 3 EVP_chacha20_poly1305 "
                    f"(stand-in for ring 0.17 asm; the Rust reference cannot be built here), each thread "
                    f"pinned to its own physical core, median of 9 reps on {threads} threads = this job's "
                    f"CPU share ({cpus['allowed_cpus']} CPUs in the affinity mask, {cpus['logical_cpus']} "
                    f"logical / {cpus['physical_cores']} physical cores on the machine, {cpus['model']}); "
-                   f"1 thread: {one['gbps']:.3f} Gbit/s"),
-        "one_core_gbps": round(one["gbps"], 3),
+                   f"1 thread: {one['gbps_op']:.3f} Gbit/s"),
+        "one_core_gbps": round(one["gbps_op"], 3),
+        "size": size, "op": op,
+        "seal_gbps": round(many["seal_gbps_best"], 3), "open_gbps": round(many["open_gbps_best"], 3),
         "threads_gbps": {str(k): round(v, 3) for k, v in sorted(pts.items())},
         "scaling_efficiency": {str(k): round(v, 3) for k, v in sorted(eff.items())},
         "scaling_efficiency_at_share": round(eff[threads], 3),
@@ -429,7 +475,7 @@ def cpu_baseline(threads: int, cpus: dict, curve=()) -> dict:
         # machine whose other cores run other jobs, so the all-core figure is an
         # extrapolation from measured per-core rates -- labelled, not measured
         "all_physical_cores_extrapolated_gbps": round(pts[t_ok] / t_ok * cpus["physical_cores"], 1),
-        "all_physical_cores_upper_bound_gbps": round(one["gbps"] * cpus["physical_cores"], 1),
+        "all_physical_cores_upper_bound_gbps": round(one["gbps_op"] * cpus["physical_cores"], 1),
         "all_physical_cores_note": (f"per-core rate at {t_ok} pinned threads (the largest measured count "
                                     f"at >= 0.8 of one core's per-core rate) x physical cores; upper bound "
                                     f"= one core x physical cores.  Not run on all cores: the GPU box grants "
@@ -551,6 +597,8 @@ def run(args, factory=None, device_fn=None, device_count=None):
         dev, stream, sync, new_event = device_fn(local)
 
     wl = (factory or make_workload)(args, dev, rank, world)
+    if hasattr(wl, "prepare"):
+        wl.prepare(stream)
     for _ in range(args.warmup):
         wl.step(stream)
     sync()
@@ -645,15 +693,34 @@ def run(args, factory=None, device_fn=None, device_count=None):
     elif rank == 0:
         total_payload, total_pkts = float(totals[0]), float(totals[1])
         gbps = total_payload * 8 * args.steps / elapsed / 1e9
-        dom = "seal" if avg["seal"] >= avg["open"] else "open"
+        op = getattr(wl, "op", "roundtrip")
+        ran = ["seal", "open"] if op == "roundtrip" else [op]
+        dom = max(ran, key=lambda k: avg[k])
         achieved = wl.launch_bytes[dom] / (avg[dom] * 1e-3) / 1e9
         tag = getattr(wl, "profile_tag", f"config{args.config}")  # (None: non-default shape)
         tr = load_pmc("traffic", wl.kernels[dom], tag)
         pw = (sustained or {}).get("power") or {}
         live_clock = pw["gfx_clock_MHz"] / 1e3 if pw.get("gfx_clock_MHz") else None
+        if args.config != 2:
+            metric = f"Gbit/s device-resident ChaCha20-Poly1305 seal+open, BASELINE config {args.config}"
+        elif op == "roundtrip" and args.size == 1350:
+            metric = METRIC
+        else:
+            metric = (f"Gbit/s device-resident ChaCha20-Poly1305 "
+                      f"{ {'roundtrip': 'seal+open', 'seal': 'seal', 'open': 'open'}[op] }, {args.size}B pkts")
+        live_clk = live_clock
+        per_kernel = {}
+        for k in ran:  # each launch against both rooflines
+            kb = wl.launch_bytes[k] / (avg[k] * 1e-3) / 1e9
+            cr_k = compute_roofline(wl, wl.kernels[k], avg[k], live_clk,
+                                    ((sustained or {}).get("kernel_ms") or {}).get(k))
+            per_kernel[k] = {"kernel": wl.kernels[k], "ms": round(avg[k], 4),
+                             "gbps_payload": round(wl.payload_bytes * 8 / (avg[k] * 1e-3) / 1e9, 1),
+                             "hbm_frac": round(kb / HBM_PEAK_GBS, 4),
+                             "compute_frac": (cr_k or {}).get("frac"),
+                             "floor_ms_at_live_clock": (cr_k or {}).get("floor_ms_at_clock")}
         line = {
-            "metric": METRIC if args.config == 2 else
-            f"Gbit/s device-resident ChaCha20-Poly1305 seal+open, BASELINE config {args.config}",
+            "metric": metric,
             "value": round(gbps, 2),
             "unit": "Gbit/s",
             "n_gpus": world,
@@ -683,11 +750,11 @@ def run(args, factory=None, device_fn=None, device_count=None):
                 "compute": compute_roofline(wl, wl.kernels[dom], avg[dom], live_clock,
                                             ((sustained or {}).get("kernel_ms") or {}).get(dom)),
             },
-            "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
-            "seal_gbps": round(wl.payload_bytes * 8 / (avg["seal"] * 1e-3) / 1e9, 1),
-            "open_gbps": round(wl.payload_bytes * 8 / (avg["open"] * 1e-3) / 1e9, 1),
-            "roundtrip_hbm_frac": round((wl.launch_bytes["seal"] + wl.launch_bytes["open"]) /
-                                        ((avg["seal"] + avg["open"]) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel_ms": {k: round(avg[k], 4) for k in ran},
+            **{f"{k}_gbps": per_kernel[k]["gbps_payload"] for k in ran},
+            "per_kernel": per_kernel,
+            "roundtrip_hbm_frac": round(sum(wl.launch_bytes[k] for k in ran) /
+                                        (sum(avg[k] for k in ran) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "packets_per_step": int(total_pkts),
             "verified": "all statuses Ok, open(seal(x)) == x over the whole batch, and "
                         f"{evp.get('checked', 0)} sealed datagrams spread over the batch equal "
@@ -701,6 +768,7 @@ def run(args, factory=None, device_fn=None, device_count=None):
         if lim:
             line["roofline"]["limiter"] = lim
         if world == 1 and not args.no_cpu_baseline and args.config == 2:
+            # (at --size P and --op: the CPU path at the same size, the same operation)
             cpus = host_cpus()
             # one thread per physical core this job may use: the GPU box grants a
             # job a CPU share (OMP_NUM_THREADS there) of a larger machine
@@ -708,7 +776,7 @@ def run(args, factory=None, device_fn=None, device_count=None):
             threads = args.cpu_threads or max(1, min(cpus["allowed_cpus"], cpus["physical_cores"], share))
             curve = [int(x) for x in args.cpu_curve.split(",") if x.strip()] if args.cpu_curve else []
             try:
-                line["cpu_baseline"] = cpu_baseline(threads, cpus, curve)
+                line["cpu_baseline"] = cpu_baseline(threads, cpus, curve, size=args.size, op=op)
             except Exception as e:  # reported, never fatal to the GPU number
                 line["cpu_baseline"] = {"error": str(e)[:200]}
     if line is not None:

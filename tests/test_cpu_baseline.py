@@ -46,3 +46,13 @@ def test_cpu_baseline_fields():
     else:
         assert d["all_physical_cores_extrapolated_gbps"] > 0
         assert d["all_physical_cores_upper_bound_gbps"] >= d["all_physical_cores_extrapolated_gbps"] * 0.999
+
+
+def test_cpu_baseline_at_the_reference_bench_sizes():
+    """--size P --op seal: the CPU baseline runs P-byte packets and reports the seal rate
+    (the reference's chacha20poly1305_benching.rs shape), with the same payload bytes per
+    worker as config 1."""
+    cpus = bench.host_cpus()
+    d = bench.cpu_baseline(1, cpus, [], size=8192, op="seal")
+    assert d["size"] == 8192 and d["op"] == "seal" and d["value"] == d["seal_gbps"] > 0
+    assert "8192 B" in d["sample"] and "best seal time" in d["sample"]

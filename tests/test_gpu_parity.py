@@ -294,11 +294,17 @@ def test_in_place_seal_and_open(torch_cuda, gpu):
 
 
 def test_config2_full_size_round_trip(torch_cuda, gpu):
-    """1M x 1350 B (BASELINE config 2): seal->open identity, status, sampled oracle parity."""
+    """1M x 1350 B (BASELINE config 2): seal->open identity, status, and EVERY sealed
+    datagram equal to the oracle's (chunked host comparison, tests/oracle_chunks.py);
+    then one 64 Ki-packet chunk of oracle-sealed datagrams (other payloads, other
+    counters) spliced into the batch is opened by the GPU back to the oracle's
+    plaintext -- the open kernel checked on bytes it did not produce itself."""
     torch = torch_cuda
+    from oracle_chunks import seal_matches_oracle
     n, P, S = 1 << 20, 1350, 1408
     keys = synth.keys(1)
-    gpu.set_keys(0, keys, np.array([synth.RECEIVER_IDX], np.uint32))
+    kidx = np.array([synth.RECEIVER_IDX], np.uint32)
+    gpu.set_keys(0, keys, kidx)
     pt = synth.device_payloads(n, P, S, "cuda")
     wire = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
     back = torch.zeros(n * S, dtype=torch.uint8, device="cuda")
@@ -308,13 +314,31 @@ def test_config2_full_size_round_trip(torch_cuda, gpu):
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0
     assert torch.equal(back.view(n, S)[:, :P], pt.view(n, S)[:, :P])
-    # sampled bit-exactness against the oracle (every 1021st packet)
-    rows = np.arange(0, n, 1021)
-    wire_rows = wire.view(n, S)[torch.from_numpy(rows).cuda()].cpu().numpy()
-    pt_rows = pt.view(n, S)[torch.from_numpy(rows).cuda()].cpu().numpy()
-    for r, w, p in zip(rows, wire_rows, pt_rows):
-        want = o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, int(r), p[:P].tobytes())
-        assert w[:P + 32].tobytes() == want
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = descs["dst_off"] = np.arange(n, dtype=np.int64) * S
+    descs["counter"] = np.arange(n, dtype=np.uint64)
+    descs["len"] = P
+    r = seal_matches_oracle(pt, wire, descs, np.arange(n, dtype=np.int64) * S, n * S, keys, kidx)
+    assert r["checked"] == n and r["mismatches"] == 0, r
+    # oracle-produced datagrams opened on the GPU
+    lo, k = n // 2 + 7, 1 << 16
+    rng = np.random.default_rng(2)
+    host_pt = rng.integers(0, 256, k * S, dtype=np.uint8)
+    od = np.zeros(k, DESC)
+    od["src_off"] = od["dst_off"] = np.arange(k, dtype=np.int64) * S
+    od["counter"] = rng.integers(0, 2**63, k, dtype=np.uint64)
+    od["len"] = P
+    host_wire = np.zeros(k * S, np.uint8)
+    assert (o.seal_batch(od, keys, kidx, host_pt, host_wire) == 0).all()
+    wire[lo * S:(lo + k) * S] = to_dev(torch, host_wire)
+    back.zero_()
+    st.fill_(-1)
+    gpu.open_strided(n, P + 32, 0, wire, S, back, S, st)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    got = back[lo * S:(lo + k) * S].cpu().numpy().reshape(k, S)
+    assert np.array_equal(got[:, :P], host_pt.reshape(k, S)[:, :P])
+    assert torch.equal(back.view(n, S)[:lo, :P], pt.view(n, S)[:lo, :P])
 
 
 @pytest.mark.parametrize("layout", ["slots_padded", "neptun"])
@@ -327,8 +351,8 @@ def test_config2_full_size_bench_layouts(torch_cuda, gpu, layout):
     neptun -- seal in place (device/mod.rs:1297-1337), open into fresh slots at
       offset 0 (device/mod.rs:1140-1148, the text grid), no padding: the bytes of
       the open slots past the plaintext untouched.
-    Both: all statuses Ok, open(seal(x)) == x, every 1021st datagram equal to the
-    oracle's format_packet_data."""
+    Both: all statuses Ok, open(seal(x)) == x, every datagram equal to the oracle's
+    (chunked host comparison)."""
     torch = torch_cuda
     n, P, S = 1 << 20, 1350, 1408
     keys = synth.keys(1)
@@ -362,13 +386,15 @@ def test_config2_full_size_bench_layouts(torch_cuda, gpu, layout):
             "in-place seal: bytes past the datagram written"
     assert int((st_s != 0).sum()) == 0 and int((st_o != 0).sum()) == 0
     assert torch.equal(back.view(n, S)[:, o_off:o_off + P], pt.view(n, S)[:, 16:16 + P])
-    rows = np.arange(0, n, 1021)
-    idx = torch.from_numpy(rows).cuda()
-    wire_rows = wire.view(n, S)[idx].cpu().numpy()
-    pt_rows = pt.view(n, S)[idx].cpu().numpy()
-    for r, w, p in zip(rows, wire_rows, pt_rows):
-        want = o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, int(r), p[16:16 + P].tobytes())
-        assert w[:P + 32].tobytes() == want
+    from oracle_chunks import seal_matches_oracle
+    descs = np.zeros(n, DESC)
+    descs["src_off"] = np.arange(n, dtype=np.int64) * S + 16
+    descs["dst_off"] = np.arange(n, dtype=np.int64) * S
+    descs["counter"] = np.arange(n, dtype=np.uint64)
+    descs["len"] = P
+    r = seal_matches_oracle(pt, wire, descs, np.arange(n, dtype=np.int64) * S, n * S, keys,
+                            np.array([synth.RECEIVER_IDX], np.uint32))
+    assert r["checked"] == n and r["mismatches"] == 0, r
 
 
 # ---------------------------------------------------------------------------
@@ -474,8 +500,8 @@ def test_per_peer_keys_match_oracle(torch_cuda, gpu):
 def test_config4_full_size_per_peer(torch_cuda, gpu):
     """BASELINE config 4 at full size: 4096 peers x 4096 packets (16.8M x 1350 B, keys
     per lane from the 4096-slot table): statuses, round trip, every peer's counters
-    exactly 0..4095 in its headers, sampled oracle parity -- all checks on the device
-    except the samples (the buffers are 22.6 GB each)."""
+    exactly 0..4095 and its receiver index in its headers, and every datagram equal to
+    the oracle's (chunked host comparison over the 22.6 GB batch)."""
     torch = torch_cuda
     from tools import workloads
     peers = per = 4096
@@ -496,18 +522,22 @@ def test_config4_full_size_per_peer(torch_cuda, gpu):
     peer = torch.from_numpy(b.seal_host["key_slot"].astype(np.int64)).cuda()
     key = torch.sort(peer * per + ctr).values
     assert torch.equal(key, torch.arange(b.n, dtype=torch.int64, device="cuda"))
-    del key, ctr, offs, peer
-    for i in range(0, b.n, 65521):
-        off, p = int(b.offs[i]), 1350
-        d = b.seal_host[i]
-        sl = int(d["key_slot"])
-        pt = b.pt[off + 16:off + 16 + p].cpu().numpy().tobytes()
-        got = b.wire[off:off + p + 32].cpu().numpy().tobytes()
-        assert got == o.format_packet_data(keys[sl].tobytes(), int(kidx[sl]), int(d["counter"]), pt)
+    # every header's receiver index is its peer's key_index (no slot mix-up)
+    ridx = torch.zeros(b.n, dtype=torch.int64, device="cuda")
+    for j in range(4):
+        ridx |= b.wire[offs + 4 + j].to(torch.int64) << (8 * j)
+    want_ridx = torch.from_numpy(kidx.astype(np.int64)).cuda()[peer]
+    assert torch.equal(ridx, want_ridx)
+    del key, ctr, offs, peer, ridx, want_ridx
+    # every datagram against the oracle (chunked host comparison)
+    from oracle_chunks import seal_matches_oracle
+    r = seal_matches_oracle(b.pt, b.wire, b.seal_host, b.offs, b.total, keys, kidx)
+    assert r["checked"] == b.n and r["mismatches"] == 0, r
 
 
 def test_config3_full_size_round_trip(torch_cuda, gpu):
-    """BASELINE config 3 at full size (1.31M packets): statuses, round trip, sampled oracle."""
+    """BASELINE config 3 at full size (1.31M packets): statuses, round trip, every datagram
+    equal to the oracle's (chunked host comparison)."""
     torch = torch_cuda
     from tools import workloads
     b = workloads.config3(1 << 18, "cuda")
@@ -520,11 +550,9 @@ def test_config3_full_size_round_trip(torch_cuda, gpu):
     torch.cuda.synchronize()
     assert int((b.st_seal != 0).sum()) == 0 and int((b.st_open != 0).sum()) == 0
     assert b.round_trip_equal()
-    for i in range(0, b.n, 4099):
-        off, p = int(b.offs[i]), int(b.sizes[i])
-        pt = b.pt[off + 16:off + 16 + p].cpu().numpy().tobytes()
-        got = b.wire[off:off + p + 32].cpu().numpy().tobytes()
-        assert got == o.format_packet_data(keys[0].tobytes(), synth.RECEIVER_IDX, i, pt)
+    from oracle_chunks import seal_matches_oracle
+    r = seal_matches_oracle(b.pt, b.wire, b.seal_host, b.offs, b.total, keys, kidx)
+    assert r["checked"] == b.n and r["mismatches"] == 0, r
 
 
 # ---------------------------------------------------------------------------

@@ -107,3 +107,38 @@ def test_batch_forms_match_single():
         want = o.format_packet_data(keys[d["key_slot"]].tobytes(), int(kidx[d["key_slot"]]),
                                     int(d["counter"]), src[d["src_off"]:d["src_off"] + d["len"]].tobytes())
         assert dst[d["dst_off"]:d["dst_off"] + d["len"] + 32].tobytes() == want
+
+
+def test_chunked_whole_batch_check_finds_every_corruption():
+    """tests/oracle_chunks.py (the GPU suite's whole-batch oracle comparison) run on
+    host tensors: a correct batch passes in full, and a flipped byte in any packet --
+    including one in a chunk's last packet -- is reported by index."""
+    import torch
+    from oracle_chunks import chunk_bounds, seal_matches_oracle
+    from tools import synth
+    rng = np.random.default_rng(8)
+    sizes = rng.choice([0, 1, 64, 1350, 8900], 3000).astype(np.int64)
+    slot = (sizes + 32 + 127) // 128 * 128
+    starts = np.zeros(len(sizes), np.int64)
+    starts[1:] = np.cumsum(slot)[:-1]
+    end = int(slot.sum())
+    src = rng.integers(0, 256, end, dtype=np.uint8)
+    d = np.zeros(len(sizes), o.DESC_DTYPE)
+    d["src_off"], d["dst_off"], d["len"] = starts + 16, starts, sizes
+    d["counter"] = rng.integers(0, 2**63, len(sizes), dtype=np.uint64)
+    d["key_slot"] = rng.integers(0, 4, len(sizes))
+    keys = synth.keys(4, seed=3)
+    kidx = np.arange(4, dtype=np.uint32) + 9
+    wire = np.zeros(end, np.uint8)
+    assert (o.seal_batch(d, keys, kidx, src, wire) == 0).all()
+    bounds = chunk_bounds(starts, end, 1 << 16)
+    assert bounds[0][0] == 0 and bounds[-1][1] == len(sizes)
+    assert all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
+    t_src, t_wire = torch.from_numpy(src), torch.from_numpy(wire.copy())
+    r = seal_matches_oracle(t_src, t_wire, d, starts, end, keys, kidx, chunk_bytes=1 << 16)
+    assert r == {"checked": 3000, "payload_bytes": int(sizes.sum()), "mismatches": 0, "bad": []}
+    last = bounds[1][1] - 1
+    for i in (5, last):
+        t_wire[int(starts[i]) + 4] ^= 1   # the receiver index
+    r = seal_matches_oracle(t_src, t_wire, d, starts, end, keys, kidx, chunk_bytes=1 << 16)
+    assert r["mismatches"] == 2 and r["bad"] == [5, last]
