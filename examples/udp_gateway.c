@@ -69,6 +69,7 @@ typedef struct {
   _Atomic int rx_done;
   _Atomic int send_done;       /* the sender has sent (or given up on) all its datagrams */
   _Atomic uint32_t n_written_off; /* datagrams the sender's flow control counts as lost */
+  _Atomic int rx_idle;         /* the reader's last recvmmsg timed out with nothing */
   /* decrypt worker output */
   uint8_t **dst;
   uint32_t *dst_cap;
@@ -150,13 +151,18 @@ static void *sender(void *arg) {
     while (done < k) {
       if (atomic_load(&g->rx_done) || atomic_load(&g->failed)) break;
       const uint32_t rx = atomic_load(&g->n_rx);
-      const uint32_t inflight = atomic_load(&g->n_sent) - rx - atomic_load(&g->n_written_off);
+      /* signed: datagrams written off as lost that arrive late after all would
+         otherwise underflow the in-flight count */
+      const int64_t inflight64 = (int64_t)atomic_load(&g->n_sent) - rx - atomic_load(&g->n_written_off);
+      const uint32_t inflight = inflight64 > 0 ? (uint32_t)inflight64 : 0u;
       if (inflight >= g->window) {
         t = now();
         if (stall_since < 0 || rx != stall_rx) {
           stall_since = t;
           stall_rx = rx;
-        } else if (t - stall_since > 1.0) {
+        } else if (t - stall_since > 5.0 && atomic_load(&g->rx_idle)) {
+          /* only once the reader has sat idle in recvmmsg (not while it is busy
+             decrypting a slow batch) and the window has not moved for 5 s */
           atomic_fetch_add(&g->n_written_off, inflight);
           stall_since = -1.0;
         }
@@ -208,6 +214,7 @@ static void *reader(void *arg) {
     const double t = now();
     const int r = recvmmsg(g->sb, msgs, m, MSG_WAITFORONE, &to);
     g->t_recv += now() - t;
+    atomic_store(&g->rx_idle, r <= 0);
     if (r <= 0) {
       /* every datagram that was sent has arrived or is lost: stop after 2 s
          idle once the sender is done; nothing at all for 60 s ends it too */

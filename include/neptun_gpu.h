@@ -371,7 +371,11 @@ typedef struct wg_session_keys {
   uint32_t peer_index;             /* the response's sender index */
   uint8_t sending_key[32];         /* temp2 */
   uint8_t receiving_key[32];       /* temp3 */
-} wg_session_keys;                 /* 72 bytes */
+  uint32_t receiver_idx;           /* the response's receiver index (0 on WrongPacketType): jobs[i]
+                                      must be the InitSent state of that local index -- the caller
+                                      checks it (receive_handshake_response, handshake.rs:620-630) */
+  uint32_t pad;
+} wg_session_keys;                 /* 80 bytes */
 
 typedef struct wg_cookie_open_job {
   uint8_t message[64];             /* COOKIE_REPLY */

@@ -582,6 +582,8 @@ __global__ __launch_bounds__(256) void handshake_response_kernel(HandshakeRespon
   uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   o.status = status;
   o.peer_index = status == WG_STATUS_WRONG_PACKET_TYPE ? 0u : w[1];
+  o.receiver_idx = status == WG_STATUS_WRONG_PACKET_TYPE ? 0u : w[2];  // (state match)
+  o.pad = 0u;
   // Session::new(local_index, peer_index, temp3, temp2): sending = temp2, receiving = temp3
   st_words(o.sending_key, ok ? t2 : z, 8);
   st_words(o.receiving_key, ok ? t3 : z, 8);

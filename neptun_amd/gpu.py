@@ -54,12 +54,12 @@ INIT_SENT_DTYPE = np.dtype([("message", "u1", 148), ("local_index", "<u4"), ("ch
 RESPONSE_RECEIVED_JOB_DTYPE = np.dtype([("chaining_key", "u1", 32), ("hash", "u1", 32),
                                         ("ephemeral_private", "u1", 32), ("preshared_key", "u1", 32)])
 SESSION_KEYS_DTYPE = np.dtype([("status", "<i4"), ("peer_index", "<u4"), ("sending_key", "u1", 32),
-                               ("receiving_key", "u1", 32)])
+                               ("receiving_key", "u1", 32), ("receiver_idx", "<u4"), ("pad", "<u4")])
 COOKIE_OPEN_JOB_DTYPE = np.dtype([("message", "u1", 64), ("cookie_key", "u1", 32), ("mac1", "u1", 16)])
 COOKIE_OPEN_OUT_DTYPE = np.dtype([("status", "<i4"), ("receiver_idx", "<u4"), ("cookie", "u1", 16)])
 assert (INITIATION_JOB_DTYPE.itemsize, INIT_SENT_DTYPE.itemsize, RESPONSE_RECEIVED_JOB_DTYPE.itemsize,
         SESSION_KEYS_DTYPE.itemsize, COOKIE_OPEN_JOB_DTYPE.itemsize,
-        COOKIE_OPEN_OUT_DTYPE.itemsize) == (208, 232, 128, 72, 112, 24)
+        COOKIE_OPEN_OUT_DTYPE.itemsize) == (208, 232, 128, 80, 112, 24)
 
 STATUS = {
     0: "Ok", 1: "DestinationBufferTooSmall", 2: "IncorrectPacketLength", 3: "UnexpectedPacket",

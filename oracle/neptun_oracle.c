@@ -12,7 +12,7 @@
  *       AAD     empty                                              (:239)
  *       body    ChaCha20-Poly1305 ciphertext, no padding, 16 B tag (:229, :246)
  *   - Session::receive_packet_data    session.rs:265-302 (minus the replay
- *       window, which lives in oracle/replay.py): open_in_place, failure ->
+ *       window, which lives in oracle/tunn_model.py): open_in_place, failure ->
  *       InvalidAeadTag (:290-296)
  *   - Tunn::parse_incoming_packet     neptun/src/noise/mod.rs:139-199 (DATA arm)
  *   - the AEAD itself: ring 0.17.14 LessSafeKey with CHACHA20_POLY1305

@@ -400,6 +400,7 @@ def test_initiator_handshake_on_gpu_end_to_end(torch_cuda, gpu):
             exp = H.receive_response(ck, h, ei, si, rmsgs[i], psks[i])
             assert st == exp[0] == 0, (i, st)
             assert int(res[i]["peer_index"]) == 0x0A000000 + i
+            assert int(res[i]["receiver_idx"]) == idx  # the initiator's local index: picks the state
             assert res[i]["sending_key"].tobytes() == exp[1] == resp[i]["receiving_key"].tobytes()
             assert res[i]["receiving_key"].tobytes() == exp[2] == resp[i]["sending_key"].tobytes()
         # whole batch under initiator 0's key: only entry 0 (and any other entry of
@@ -409,6 +410,18 @@ def test_initiator_handshake_on_gpu_end_to_end(torch_cuda, gpu):
         allres = out.cpu().numpy().view(G.SESSION_KEYS_DTYPE)
         assert int(allres[0]["status"]) == 0
         assert all(int(allres[i]["status"]) in (H.INVALID_AEAD_TAG, H.WRONG_PACKET_TYPE) for i in range(1, n))
+        # a job that is not the InitSent state of the message's receiver index (states
+        # swapped): InvalidAeadTag, and receiver_idx names the state the caller should
+        # have picked
+        ok_i = [i for i in range(n) if kind[i] == "ok"][:2]
+        a, b = ok_i
+        o1 = torch.zeros(G.SESSION_KEYS_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        gpu.handshake_receive_response_batch(want[a][0], 1, d_m[stride * a:], stride,
+                                             d_ij[G.RESPONSE_RECEIVED_JOB_DTYPE.itemsize * b:], o1,
+                                             check_mac1=check_mac1)
+        torch.cuda.synchronize()
+        r1 = o1.cpu().numpy().view(G.SESSION_KEYS_DTYPE)[0]
+        assert int(r1["status"]) == H.INVALID_AEAD_TAG and int(r1["receiver_idx"]) == want[a][2]
 
 
 def test_cookie_reply_open_matches_oracle(torch_cuda, gpu):
