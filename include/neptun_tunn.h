@@ -115,7 +115,14 @@ int wg_tunn_set_time(wg_tunn *t, uint64_t now);
  * caller's buffers directly over PCIe (no staging copies); decapsulate /
  * decrypt batches read registered datagrams directly (their plaintext is still
  * staged: the replay decision that gates the write to dst comes after the
- * GPU).  Results are identical either way. */
+ * GPU).  Results are identical either way.
+ *
+ * Data movement (both modes, WG_TUNN_ZEROCOPY=1 selects kernels that read and
+ * write pinned host memory over PCIe instead): a batch flows in chunks through
+ * pinned staging; each chunk is copied to the device by the copy engines
+ * (registered datagrams in contiguous runs straight from the caller's memory),
+ * opened / sealed in HBM and copied back.  The host copies run on a pool of
+ * WG_TUNN_THREADS threads (default: the CPUs this process may use, at most 16). */
 /* sending counter of the current session / replay state of a ring slot (for tests) */
 int wg_tunn_session_counters(const wg_tunn *t, uint32_t ring_slot, uint64_t *sending_counter,
                              wg_replay *window);
@@ -138,6 +145,26 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
 int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
                           const uint32_t *len, uint8_t *const *dst, const uint32_t *dst_cap,
                           wg_tunn_result *res);
+
+/* Where a Tunn's batch time goes (diagnostics; cumulative since creation or the
+ * last reset, summed over engines).  Host phases are wall time on the thread
+ * that runs them; the pool phases count the wall time of the whole parallel
+ * step.  The device times come from timing events on the chunk streams and are
+ * only collected after wg_tunn_set_phase_timing(t, 1). */
+typedef struct wg_tunn_phases {
+  uint64_t calls, chunks, packets;
+  double total_us;        /* inside the batch calls */
+  double checks_us;       /* pass 1: parse / session / index checks (pool), counter reservation */
+  double pack_us;         /* packets into pinned staging + descriptors (pool) */
+  double submit_us;       /* enqueueing copies and kernels */
+  double wait_us;         /* the calling / driver thread blocked on a chunk's completion */
+  double decide_us;       /* in-order replay window pass (decapsulate; one thread) */
+  double copy_out_us;     /* validation + results out of staging into dst (pool) */
+  double dev_h2d_us, dev_kernel_us, dev_d2h_us;  /* device time per stage, summed over chunks */
+} wg_tunn_phases;
+int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out);
+int wg_tunn_reset_phases(wg_tunn *t);
+int wg_tunn_set_phase_timing(wg_tunn *t, int on);
 
 #ifdef __cplusplus
 }

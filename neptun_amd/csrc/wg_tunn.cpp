@@ -28,8 +28,10 @@
 #include <sched.h>
 #include <sys/syscall.h>
 #include <unistd.h>
+#include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <chrono>
 #include <condition_variable>
@@ -133,6 +135,42 @@ inline uint64_t ld64(const uint8_t *p) {
   return v;
 }
 inline uint64_t round128(uint64_t x) { return (x + 127) / 128 * 128; }
+
+// Packet copies into / out of pinned staging with streaming (non-temporal)
+// stores: the bytes are read next by the copy engines or the caller, not by this
+// core, and a streaming store skips the read-for-ownership of the destination
+// line (a third of a cached memcpy's DRAM traffic).  WG_TUNN_NT=0: memcpy.
+bool nt_copies() {
+  const char *e = std::getenv("WG_TUNN_NT");
+  return !e || std::atoi(e) != 0;
+}
+void copy_bytes(uint8_t *dst, const uint8_t *src, size_t n, bool nt) {
+  if (!nt || n < 256) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
+  std::memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 48), d);
+  }
+  for (; i + 16 <= n; i += 16)
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i),
+                     _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i)));
+  std::memcpy(dst + i, src + i, n - i);
+  _mm_sfence();  // streaming stores are weakly ordered: visible before the DMA / caller reads
+}
 
 size_t chunk_bytes() {  // staging bytes per pipeline chunk (WG_TUNN_CHUNK_KB overrides, per call)
   const char *e = std::getenv("WG_TUNN_CHUNK_KB");
@@ -333,15 +371,66 @@ class Driver {
   std::thread th_;  // last: started after the members it uses
 };
 
+// Output scatter (DMA mode): a kernel copies each packet's output bytes from the
+// device staging straight into the caller's registered buffer (zero-copy writes
+// over PCIe: 54 GB/s device-to-host on MI355X against 30-38 GB/s for the copy
+// engines, and it runs beside the copy engines' host-to-device input copies:
+// 86 GB/s both ways, tools/microbench_dma.cpp, profiles/r04h_dma.jsonl).  Job:
+// a_len bytes from a_base + a_off, then b_len bytes from b_base + b_off, to dst.
+struct Scatter {
+  uint64_t dst;    // device address of the caller's (registered) destination
+  uint32_t a_off, a_len, b_off, b_len;
+};
+
+__global__ __launch_bounds__(256) void scatter_kernel(const Scatter *__restrict__ jobs, uint32_t m,
+                                                      const uint8_t *__restrict__ a_base,
+                                                      const uint8_t *__restrict__ b_base) {
+  const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  if (j >= m) return;
+  const Scatter sc = jobs[j];
+  uint8_t *dst = reinterpret_cast<uint8_t *>(sc.dst);
+  const uint8_t *a = a_base + sc.a_off, *b = b_base + sc.b_off;
+  const uint32_t L = sc.a_len + sc.b_len;
+  const bool aligned = (sc.dst & 15u) == 0 && (reinterpret_cast<uintptr_t>(a) & 15u) == 0;
+  for (uint32_t o = 16u * lane; o < L; o += 1024u) {
+    if (aligned && o + 16u <= sc.a_len) {  // a whole piece of segment a
+      *reinterpret_cast<uint4 *>(dst + o) = *reinterpret_cast<const uint4 *>(a + o);
+      continue;
+    }
+    uint8_t v[16];
+#pragma unroll
+    for (uint32_t q = 0; q < 16u; ++q) {
+      const uint32_t x = o + q;
+      v[q] = x < sc.a_len ? a[x] : (x < L ? b[x - sc.a_len] : 0u);
+    }
+    if ((sc.dst & 15u) == 0 && o + 16u <= L) {
+      uint4 w;
+      __builtin_memcpy(&w, v, 16);
+      *reinterpret_cast<uint4 *>(dst + o) = w;
+    } else {
+      for (uint32_t q = 0; q < 16u && o + q < L; ++q) dst[o + q] = v[q];
+    }
+  }
+}
+
 // one pinned + device buffer set of the pipeline
 struct Staging {
   uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
   wg_packet_desc *h_desc = nullptr, *d_desc = nullptr;
+  struct Scatter *h_sc = nullptr;  // the output scatter's per-packet jobs (pinned, read by the kernel)
   int32_t *h_st = nullptr, *d_st = nullptr;
   size_t bytes = 0, descs = 0;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // phase timing: h2d / kernel / d2h edges
+  bool timed = false;     // the chunk in flight recorded ev[]
   bool busy = false;      // work enqueued and not yet waited for
+  // explicit-copy chunks: the pack hook copied the input itself (DMA runs out of
+  // registered caller memory), the output is DMA'd by a hook (runs into
+  // registered caller memory) or deferred until the in-order decisions (mid hook)
+  bool in_dma = false, out_dma = false, defer_out = false;
+  hipEvent_t done2 = nullptr;  // the deferred outputs (mid) have landed
+  uint8_t stage = 0;           // run_chunks: kIdle / kSubmitted / kOutputs / kReady
   unsigned host_flags = hipHostMallocDefault;  // + hipHostMallocNumaUser on NUMA-bound engines
 };
 
@@ -349,6 +438,7 @@ void free_buffers(Staging &s) {
   (void)hipHostFree(s.h_in);
   (void)hipHostFree(s.h_out);
   (void)hipHostFree(s.h_desc);
+  (void)hipHostFree(s.h_sc);
   (void)hipHostFree(s.h_st);
   (void)hipFree(s.d_in);
   (void)hipFree(s.d_out);
@@ -356,6 +446,7 @@ void free_buffers(Staging &s) {
   (void)hipFree(s.d_st);
   s.h_in = s.h_out = s.d_in = s.d_out = nullptr;
   s.h_desc = s.d_desc = nullptr;
+  s.h_sc = nullptr;
   s.h_st = s.d_st = nullptr;
   s.bytes = s.descs = 0;
 }
@@ -378,13 +469,16 @@ hipError_t reserve(Staging &s, size_t bytes, size_t descs) {
   }
   if (descs > s.descs) {
     (void)hipHostFree(s.h_desc);
+    (void)hipHostFree(s.h_sc);
     (void)hipHostFree(s.h_st);
     (void)hipFree(s.d_desc);
     (void)hipFree(s.d_st);
     s.h_desc = s.d_desc = nullptr;
+    s.h_sc = nullptr;
     s.h_st = s.d_st = nullptr;
     s.descs = 0;
     if ((e = hipHostMalloc(&s.h_desc, descs * sizeof(wg_packet_desc), fl)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&s.h_sc, descs * sizeof(Scatter), fl)) != hipSuccess) return e;
     if ((e = hipHostMalloc(&s.h_st, descs * 4, fl)) != hipSuccess) return e;
     if ((e = hipMalloc(&s.d_desc, descs * sizeof(wg_packet_desc))) != hipSuccess) return e;
     if ((e = hipMalloc(&s.d_st, descs * 4)) != hipSuccess) return e;
@@ -393,15 +487,26 @@ hipError_t reserve(Staging &s, size_t bytes, size_t descs) {
   return e;
 }
 
+struct Run {
+  const uint8_t *host;
+  uint64_t pitch, dev_off, dev_pitch;
+  uint32_t width, rows;
+};
+
 // a contiguous range [k0, k1) of the selected packets and its staging bytes
 struct Chunk {
   size_t k0, k1, bytes;
 };
 
+// copy threads per engine incl. its driver: WG_TUNN_THREADS, else the CPUs this
+// process may run on (its affinity mask, not the machine: a GPU box grants a job a
+// share of a larger host) split over the engines, at most 16
 unsigned pool_workers(unsigned engines) {
   if (const char *e = std::getenv("WG_TUNN_THREADS")) return (unsigned)std::max(1, std::atoi(e)) - 1;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  return std::max(1u, std::min(8u, hw / std::max(1u, engines))) - 1;  // copy threads incl. the driver
+  cpu_set_t set;
+  unsigned cpus = std::max(1u, std::thread::hardware_concurrency());
+  if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = std::max(1, CPU_COUNT(&set));
+  return std::max(1u, std::min(16u, cpus / std::max(1u, engines))) - 1;
 }
 
 // The device side of a Tunn: one GPU context with its staging sets, streams
@@ -420,6 +525,11 @@ struct Engine {
   std::vector<uint64_t> dsrc, ddst;  // per selected packet: device addresses (direct mode)
   std::vector<uint64_t> reg;         // registered ranges (host, bytes, dev), snapshot per batch
   uint64_t tx = 0;                   // per-call tx_bytes share (summed by the caller)
+  wg_tunn_phases ph{};               // this engine's share of the phase times
+  bool timing = false;               // record device timing events (wg_tunn_set_phase_timing)
+  bool zc = true;                    // this batch's chunks run zero-copy kernels (else explicit copies)
+  std::vector<uint8_t> reg_in, reg_out;  // per packet of the share: host buffer registered (DMA runs)
+  std::vector<Run> runs;             // scratch
 };
 
 }  // namespace
@@ -434,11 +544,21 @@ struct wg_tunn {
   uint64_t time_current = 0;
   uint64_t session_timers[WG_N_SESSIONS] = {};
   std::vector<Engine *> eng;
+  wg_tunn_phases ph{};      // caller-side phases (checks, decide, totals)
   // per-call scratch (kept to avoid reallocations)
   std::vector<uint32_t> sel, slot;
+  std::vector<int32_t> code;    // pass 1: per packet, key slot if selected, else -1
+  std::vector<uint64_t> ctr_all, ctr;  // datagram counters: per packet / per selected packet
+  std::vector<uint8_t> act;     // per selected packet: what lands in dst (open_selected)
+  std::vector<uint8_t> out_dma; // per selected packet: its dst bytes were DMA'd (no host copy)
 };
 
 namespace {
+
+inline double now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct DevGuard {
   int prev = -1;
@@ -456,6 +576,22 @@ struct DevGuard {
     hipError_t e_ = (call);                                               \
     if (e_ != hipSuccess) return wg_pipe_fail(WG_RC_HIP_ERROR, what, e_); \
   } while (0)
+
+// per batch call: counts the call and its wall time (wg_tunn_get_phases);
+// checks_done() ends the pass-1 phase
+struct PhaseCall {
+  wg_tunn *t;
+  double t0, tc = -1.0;
+  PhaseCall(wg_tunn *tt, uint32_t n) : t(tt), t0(now_us()) {
+    t->ph.calls += 1;
+    t->ph.packets += n;
+  }
+  void checks_done() {
+    tc = now_us();
+    t->ph.checks_us += tc - t0;
+  }
+  ~PhaseCall() { t->ph.total_us += now_us() - t0; }
+};
 
 // set_current_session (mod.rs:528-542): switch unless the current slot holds a
 // session established later than the new one (session_timers compare)
@@ -550,21 +686,14 @@ int for_engines(wg_tunn *t, const std::function<int(Engine &)> &job) {
   return rc;
 }
 
-inline double now_us() {
-  return std::chrono::duration<double, std::micro>(
-             std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 // Zero-copy (default; WG_TUNN_ZEROCOPY=0 switches to explicit copies): the AEAD
 // kernel reads the pinned input staging and writes the pinned output staging
 // directly over PCIe, so reads and writes of a chunk share the link in both
 // directions at once instead of running as H2D copy -> kernel -> D2H copy
 // (measured: 143 / 156 vs 124 / 112 Gbit/s encap / decap, profiles/r01_tunn_*).
-bool zero_copy() {
-  static const bool v = [] {
-    const char *e = std::getenv("WG_TUNN_ZEROCOPY");
-    return !e || std::atoi(e) != 0;
-  }();
-  return v;
+bool zero_copy() {  // (read per batch)
+  const char *e = std::getenv("WG_TUNN_ZEROCOPY");
+  return !e || std::atoi(e) != 0;
 }
 
 // direct mode is possible at all: zero-copy kernels and some registered memory
@@ -573,9 +702,73 @@ bool direct_possible(Engine &E) {
   wg_ctx_reg_snapshot(E.ctx, E.reg);
   return !E.reg.empty();
 }
-bool trace_on() {
-  static const bool v = std::getenv("WG_TUNN_TRACE") != nullptr;
-  return v;
+// this batch moves registered buffers by DMA runs (explicit copies; one engine)
+bool dma_possible(wg_tunn *t, Engine &E);
+// DMA runs (explicit-copy mode, registered caller memory): packets whose host
+// buffers sit at a constant pitch with one length, and whose staging slots do
+// too, move as ONE 2D copy (rows = packets) on the copy engines -- the way the
+// pinned pipe reaches the link rate (wg_pipe.cpp) -- instead of a host memcpy
+// into pinned staging.  WG_TUNN_DMA=0 turns it off.
+bool dma_runs() {  // (read per batch, like the other WG_TUNN_* knobs)
+  const char *e = std::getenv("WG_TUNN_DMA");
+  return !e || std::atoi(e) != 0;
+}
+
+// Cut packets [a, b) with use(k) into runs: host(k) pointer, width(k) bytes,
+// dev(k) staging offset.  Returns false (runs unusable: too many small copies)
+// when there are more than max_runs.
+template <class Use, class Host, class Width, class Dev>
+bool make_runs(size_t a, size_t b, Use use, Host host, Width width, Dev dev, size_t max_runs,
+               std::vector<Run> &out) {
+  out.clear();
+  for (size_t k = a; k < b; ++k) {
+    if (!use(k)) continue;
+    const uint8_t *h = host(k);
+    const uint32_t w = width(k);
+    const uint64_t d = dev(k);
+    if (!out.empty()) {
+      Run &r = out.back();
+      const uint8_t *last = r.host + r.pitch * (r.rows - 1);
+      const uint64_t last_dev = r.dev_off + r.dev_pitch * (r.rows - 1);
+      if (w == r.width && h > last && d > last_dev) {
+        const uint64_t hp = (uint64_t)(h - last), dp = d - last_dev;
+        if (r.rows == 1 && hp >= w && dp >= w) {
+          r.pitch = hp;
+          r.dev_pitch = dp;
+          r.rows = 2;
+          continue;
+        }
+        if (r.rows > 1 && hp == r.pitch && dp == r.dev_pitch) {
+          ++r.rows;
+          continue;
+        }
+      }
+    }
+    if (out.size() >= max_runs) return false;
+    out.push_back(Run{h, w, d, w, w, 1});
+  }
+  return true;
+}
+
+hipError_t copy_runs(const std::vector<Run> &runs, uint8_t *dev_base, bool h2d, hipStream_t s) {
+  for (const Run &r : runs) {
+    hipError_t e;
+    if (h2d)
+      e = hipMemcpy2DAsync(dev_base + r.dev_off, r.dev_pitch, r.host, r.pitch, r.width, r.rows,
+                           hipMemcpyHostToDevice, s);
+    else
+      e = hipMemcpy2DAsync(const_cast<uint8_t *>(r.host), r.pitch, dev_base + r.dev_off, r.dev_pitch,
+                           r.width, r.rows, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+size_t max_runs(size_t m) { return std::max<size_t>(4, m / 16); }
+
+bool dma_possible(wg_tunn *t, Engine &E) {
+  if (!dma_runs() || t->eng.size() != 1) return false;
+  wg_ctx_reg_snapshot(E.ctx, E.reg);
+  return !E.reg.empty();
 }
 
 // Test-only fault injection: WG_TUNN_FAIL_CHUNK=c makes the batch fail with a
@@ -600,88 +793,145 @@ struct PipelineDrain {
       if (S.busy) {
         (void)hipStreamSynchronize(S.stream);
         S.busy = false;
+        S.stage = 0;
       }
   }
 };
 
 // Pipeline driver over one engine: pack(c, S) fills set S for chunk c (descs +
 // bytes), the GPU runs chunk c on S's stream, unpack(c, S) consumes the
-// results.  Chunks are unpacked strictly in order.  abs_src / abs_dst:
-// descriptors carry absolute device addresses of registered caller memory on
-// that side (no staging bytes there).
-template <class Pack, class Unpack>
+// results.  abs_src / abs_dst: descriptors carry absolute device addresses of
+// registered caller memory on that side (no staging bytes there).
+struct NoHook {
+  int operator()(const Chunk &, Staging &) const { return 0; }
+};
+
+// post_kernel(ch, S): after the kernel is enqueued (explicit-copy mode), may
+// enqueue the output's DMA runs itself (S.out_dma).  mid(ch, S): once the chunk's
+// statuses are on the host, before unpack, strictly in chunk order (the in-order
+// decisions); returns 1 when it enqueued more device work (outputs that waited for
+// its decisions: S.done2 then marks them), 0 if not, < 0 on a HIP error.
+// Stages per chunk: submitted -> [status back] mid -> [outputs back] unpack.
+// After chunk c is submitted the driver runs mid for chunk c - 1 and unpacks the
+// chunks whose outputs are in flight one chunk longer (c - 2 when outputs waited
+// for mid, else c - 1), so a chunk's deferred output copies overlap the next
+// chunk's input copies and kernel instead of the host waiting for them.
+enum : uint8_t { kIdle = 0, kSubmitted = 1, kOutputs = 2, kReady = 3 };
+
+template <class Pack, class Unpack, class Post = NoHook, class Mid = NoHook>
 int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = false,
-               bool abs_dst = false) {
+               bool abs_dst = false, Post post_kernel = Post(), Mid mid = Mid()) {
   PipelineDrain drain_guard(E);
   const size_t nc = E.chunks.size();
-  const bool tr = trace_on();
-  const double t0 = tr ? now_us() : 0.0;
   const size_t sets = pipeline_sets();
-  auto wait_unpack = [&](size_t c) -> int {
+  const bool zc = E.zc;
+  E.ph.chunks += nc;
+  size_t next_mid = 0, next_unpack = 0;
+  auto stage_mid = [&](size_t c) -> int {
     Staging &S = E.st[c % sets];
-    const double a = tr ? now_us() : 0.0;
+    const double a = now_us();
     TUNN_HIP(hipEventSynchronize(S.done), "tunn: chunk wait");
-    const double b = tr ? now_us() : 0.0;
+    E.ph.wait_us += now_us() - a;
+    const int mr = (int)mid(E.chunks[c], S);
+    if (mr < 0) return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: output copies", hipGetLastError());
+    if (mr > 0) {  // outputs that waited for the in-order decisions
+      if (S.timed) TUNN_HIP(hipEventRecord(S.ev[3], S.stream), "tunn: event");  // (d2h incl. the decide gap)
+      TUNN_HIP(hipEventRecord(S.done2, S.stream), "tunn: event");
+      S.stage = kOutputs;
+    } else {
+      S.stage = kReady;
+    }
+    return WG_RC_OK;
+  };
+  auto stage_unpack = [&](size_t c) -> int {
+    Staging &S = E.st[c % sets];
+    if (S.stage == kOutputs) {
+      const double a = now_us();
+      TUNN_HIP(hipEventSynchronize(S.done2), "tunn: chunk output wait");
+      E.ph.wait_us += now_us() - a;
+    }
+    if (S.timed) {  // device time per stage (wg_tunn_set_phase_timing)
+      float ms = 0.f;
+      if (!zc && hipEventElapsedTime(&ms, S.ev[0], S.ev[1]) == hipSuccess) E.ph.dev_h2d_us += 1e3 * ms;
+      if (hipEventElapsedTime(&ms, S.ev[1], S.ev[2]) == hipSuccess) E.ph.dev_kernel_us += 1e3 * ms;
+      if (!zc && hipEventElapsedTime(&ms, S.ev[2], S.ev[3]) == hipSuccess) E.ph.dev_d2h_us += 1e3 * ms;
+      S.timed = false;
+    }
     S.busy = false;
+    S.stage = kIdle;
     unpack(E.chunks[c], S);
-    if (tr)
-      std::fprintf(stderr, "tunn dev %d %s chunk %zu: wait %.0f us, unpack %.0f us (t=%.0f)\n",
-                   E.device, seal ? "seal" : "open", c, b - a, now_us() - b, now_us() - t0);
+    return WG_RC_OK;
+  };
+  // run mid for every chunk < c_mid and unpack every chunk < c_unpack (in order),
+  // plus chunk c_unpack itself when its outputs did not wait for mid
+  auto advance = [&](size_t c_mid, size_t c_unpack, bool ready_too) -> int {
+    while (next_mid < c_mid)
+      if (const int rc = stage_mid(next_mid++)) return rc;
+    while (next_unpack < next_mid &&
+           (next_unpack < c_unpack ||
+            (ready_too && next_unpack == c_unpack && E.st[next_unpack % sets].stage == kReady)))
+      if (const int rc = stage_unpack(next_unpack++)) return rc;
     return WG_RC_OK;
   };
   for (size_t c = 0; c < nc; ++c) {
     Staging &S = E.st[c % sets];
-    if (S.busy) {  // chunk c - sets still owns this set
-      const int rc = wait_unpack(c - sets);
-      if (rc) return rc;
-    }
+    if (S.busy)  // chunk c - sets still owns this set
+      if (const int rc = advance(c - sets + 1, c - sets + 1, false)) return rc;
     const Chunk &ch = E.chunks[c];
     const size_t m = ch.k1 - ch.k0;
-    const double pa = tr ? now_us() : 0.0;
+    const double pa = now_us();
     TUNN_HIP(reserve(S, (abs_src && abs_dst) ? 128 : ch.bytes + 128, m), "tunn: staging");
-    const double pb = tr ? now_us() : 0.0;
-    pack(ch, S);
-    if (tr)
-      std::fprintf(stderr, "tunn dev %d %s chunk %zu: %zu B reserve %.0f us, pack %.0f us (t=%.0f)\n",
-                   E.device, seal ? "seal" : "open", c, ch.bytes, pb - pa, now_us() - pb, now_us() - t0);
-    if (zero_copy()) {
+    S.in_dma = S.out_dma = S.defer_out = false;
+    const bool timed = E.timing;
+    if (timed && !S.ev[0])
+      for (auto &e : S.ev) TUNN_HIP(hipEventCreate(&e), "tunn: timing event");
+    if (!zc && timed) TUNN_HIP(hipEventRecord(S.ev[0], S.stream), "tunn: event");
+    pack(ch, S);  // (may enqueue the chunk's input DMA runs: S.in_dma; ev[0] goes first)
+    const double pb = now_us();
+    E.ph.pack_us += pb - pa;
+    if (zc) {
       const uint8_t *in = abs_src ? nullptr : S.h_in;
       uint8_t *out = abs_dst ? nullptr : S.h_out;
+      if (timed) TUNN_HIP(hipEventRecord(S.ev[1], S.stream), "tunn: event");
       const int rc = seal ? wg_gpu_seal_batch(E.ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
                                               S.stream)
                           : wg_gpu_open_batch(E.ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
                                               S.stream);
       if (rc) return rc;
+      if (timed) TUNN_HIP(hipEventRecord(S.ev[2], S.stream), "tunn: event");
     } else {
-      TUNN_HIP(hipMemcpyAsync(S.d_in, S.h_in, ch.bytes, hipMemcpyHostToDevice, S.stream), "tunn: H2D");
+      if (!S.in_dma)
+        TUNN_HIP(hipMemcpyAsync(S.d_in, S.h_in, ch.bytes, hipMemcpyHostToDevice, S.stream), "tunn: H2D");
       TUNN_HIP(hipMemcpyAsync(S.d_desc, S.h_desc, m * sizeof(wg_packet_desc),
                               hipMemcpyHostToDevice, S.stream),
                "tunn: descs H2D");
+      if (timed) TUNN_HIP(hipEventRecord(S.ev[1], S.stream), "tunn: event");
       const int rc = seal ? wg_gpu_seal_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out,
                                               S.d_st, S.stream)
                           : wg_gpu_open_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out,
                                               S.d_st, S.stream);
       if (rc) return rc;
-      TUNN_HIP(hipMemcpyAsync(S.h_out, S.d_out, ch.bytes, hipMemcpyDeviceToHost, S.stream),
-               "tunn: D2H");
+      if (timed) TUNN_HIP(hipEventRecord(S.ev[2], S.stream), "tunn: event");
+      post_kernel(ch, S);  // (may DMA the outputs straight to registered dst: S.out_dma)
+      if (!S.out_dma && !S.defer_out)
+        TUNN_HIP(hipMemcpyAsync(S.h_out, S.d_out, ch.bytes, hipMemcpyDeviceToHost, S.stream),
+                 "tunn: D2H");
       TUNN_HIP(hipMemcpyAsync(S.h_st, S.d_st, m * 4, hipMemcpyDeviceToHost, S.stream),
                "tunn: status D2H");
+      if (timed) TUNN_HIP(hipEventRecord(S.ev[3], S.stream), "tunn: event");
     }
     TUNN_HIP(hipEventRecord(S.done, S.stream), "tunn: event");
     S.busy = true;
+    S.stage = kSubmitted;
+    S.timed = timed;
+    E.ph.submit_us += now_us() - pb;
     if (const int rc = injected_failure(c)) return rc;
-    // overlap: unpack c - (sets - 1) while the chunks after it run
-    if (c + 1 >= sets && E.st[(c + 1 - sets) % sets].busy) {
-      const int rc2 = wait_unpack(c + 1 - sets);
-      if (rc2) return rc2;
-    }
+    // overlap: with sets - 1 chunks still queued behind this one, decide the
+    // oldest and unpack what has landed (see above)
+    if (c + 2 >= sets)
+      if (const int rc = advance(c + 2 - sets, c + 2 - sets > 0 ? c + 1 - sets : 0, true)) return rc;
   }
-  for (size_t c = nc >= sets ? nc - sets : 0; c < nc; ++c)
-    if (E.st[c % sets].busy) {
-      const int rc = wait_unpack(c);
-      if (rc) return rc;
-    }
-  return WG_RC_OK;
+  return advance(nc, nc, true);
 }
 
 // parse_incoming_packet (mod.rs:139-199): 1 = data, 0 = handshake/cookie, <0 = -InvalidPacket
@@ -693,12 +943,12 @@ int parse_kind(const uint8_t *d, uint32_t L) {
   return 1;
 }
 
-// validate_decapsulated_packet (mod.rs:606-670) on the plaintext pt[..P]
-void validate(wg_tunn *t, const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
+// validate_decapsulated_packet (mod.rs:606-670) on the plaintext pt[..P]; returns
+// what it adds to rx_bytes (the pool threads sum it, the caller adds it to the Tunn)
+uint64_t validate(const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
   if (P == 0) {
-    t->rx_bytes += WG_DATA_OVERHEAD_SZ;  // keepalive
     r.kind = WG_TUNN_DONE;
-    return;
+    return WG_DATA_OVERHEAD_SZ;  // keepalive
   }
   uint32_t ip_len = 0;
   const uint8_t v = pt[0] >> 4;
@@ -712,22 +962,26 @@ void validate(wg_tunn *t, const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
     std::memcpy(r.src_ip, pt + 8, 16);
   } else {
     set_err(r, WG_STATUS_INVALID_PACKET);
-    return;
+    return 0;
   }
   if (ip_len > P) {
     set_err(r, WG_STATUS_INVALID_PACKET);
-    return;
+    return 0;
   }
-  t->rx_bytes += (uint64_t)ip_len + WG_DATA_OVERHEAD_SZ;  // message_data_len, session.rs:357
   r.kind = WG_TUNN_WRITE_TO_TUNNEL;
   r.len = ip_len;
+  return (uint64_t)ip_len + WG_DATA_OVERHEAD_SZ;  // message_data_len, session.rs:357
 }
 
 // Open the selected datagrams.  decide(k, S, kk) runs in packet order on one
 // thread (kk = index of packet k inside its chunk's staging S) and returns what
 // lands in dst: 0 nothing, 1 plaintext + tag bytes, 2 zeros + tag bytes
 // (session.rs:287-296: ct||tag copied into dst, opened in place, ring zeroes
-// the plaintext on a tag mismatch); the copies then run on the pools.
+// the plaintext on a tag mismatch), | kFinish when finish(k, plaintext, P) must
+// run.  decide only touches the per-packet arrays (counters, statuses), so the
+// in-order pass stays in cache; finish (validate_decapsulated_packet: reads the
+// plaintext's IP header, fills the result, returns its rx_bytes share) runs with
+// the byte copies on the pools.
 //  * one engine: a double-buffered chunk pipeline; each chunk is decided as it
 //    returns while the next runs on the GPU;
 //  * several engines: the selection is cut into rounds of about
@@ -736,40 +990,85 @@ void validate(wg_tunn *t, const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
 //    the caller decides the round's packets in order, then every engine copies
 //    its share out.  Pinned staging per engine stays one chunk whatever the
 //    batch size (a 16M-packet batch over 2 GPUs needs no more than 1 GPU does).
-template <class Decide>
+constexpr uint8_t kFinish = 0x80;
+
+template <class Decide, class Finish>
 int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *len,
-                  uint8_t *const *dst, Decide decide) {
+                  uint8_t *const *dst, Decide decide, Finish finish) {
   const bool multi = t->eng.size() > 1;
   auto size = [&](size_t k) { return round128(len[t->sel[k]]); };
   if (!multi) split(t, size);
-  auto copy_out = [&](Engine &E, const Chunk &ch, Staging &S, const std::vector<uint8_t> &action) {
+  t->act.assign(t->sel.size(), 0);
+  t->out_dma.assign(t->sel.size(), 0);
+  const bool nt = nt_copies();
+  std::atomic<uint64_t> rx{0};
+  auto copy_out = [&](Engine &E, const Chunk &ch, Staging &S) {
+    const double a = now_us();
     E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+      uint64_t my_rx = 0;
       for (size_t kk = lo; kk < hi; ++kk) {
-        const uint8_t a = action[ch.k0 + kk - (multi ? 0 : ch.k0)];
-        if (!a) continue;
         const size_t k = ch.k0 + kk;
+        const uint8_t a = t->act[k];
+        if (!a) continue;
         const uint32_t i = t->sel[k];
         const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
-        if (a == 1) std::memcpy(dst[i], S.h_out + S.h_desc[kk].dst_off, P);
-        else std::memset(dst[i], 0, P);
-        std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
+        // plaintext (or ring's zeros): DMA'd into dst already, else in the pinned staging
+        const bool in_dst = t->out_dma[k];
+        const uint8_t *pt = in_dst ? dst[i] : S.h_out + S.h_desc[kk].dst_off;
+        if (!in_dst) {  // (the scatter kernel wrote plaintext and tag bytes itself)
+          if ((a & 3) == 1) copy_bytes(dst[i], pt, P, nt);
+          else std::memset(dst[i], 0, P);
+          std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
+        }
+        if (a & kFinish) my_rx += finish(k, in_dst ? dst[i] : pt, P);
       }
+      rx.fetch_add(my_rx, std::memory_order_relaxed);
     });
+    E.ph.copy_out_us += now_us() - a;
   };
-  std::vector<uint8_t> action;
-  if (multi) action.assign(t->sel.size(), 0);
+  auto decide_range = [&](size_t k0, size_t k1, const Staging &S, size_t kk0) {
+    const double a = now_us();
+    for (size_t k = k0; k < k1; ++k) t->act[k] = decide(k, S, kk0 + (k - k0));
+    t->ph.decide_us += now_us() - a;
+  };
   auto engine_job = [&](Engine &E) -> int {
+    // DMA runs (one engine, registered buffers): datagrams in, plaintexts out by 2D copies
+    const bool dma = !multi && dma_possible(t, E);
+    E.zc = zero_copy() && !dma;
     make_chunks(E, size, multi ? ~size_t(0) : 0);
-    // direct input: every datagram 16-byte aligned inside memory registered on this engine
-    bool direct = direct_possible(E);
+    // direct input (zero-copy): every datagram 16-byte aligned inside registered memory
+    bool direct = !dma && direct_possible(E);
     E.dsrc.resize(E.k1 - E.k0);
     for (size_t k = E.k0; direct && k < E.k1; ++k) {
       const uint32_t i = t->sel[k];
       direct = (reinterpret_cast<uint64_t>(datagram[i]) & 15u) == 0 &&
                dev_addr(E, datagram[i], len[i], E.dsrc[k - E.k0]);
     }
+    if (dma) {
+      E.reg_in.assign(E.k1 - E.k0, 0);
+      E.reg_out.assign(E.k1 - E.k0, 0);
+      E.ddst.resize(E.k1 - E.k0);
+      uint64_t unused;
+      for (size_t k = E.k0; k < E.k1; ++k) {
+        const uint32_t i = t->sel[k];
+        E.reg_in[k - E.k0] = dev_addr(E, datagram[i], len[i], unused);
+        E.reg_out[k - E.k0] = dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0]);
+      }
+    }
     auto pack = [&](const Chunk &ch, Staging &S) {
-      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+      const size_t m = ch.k1 - ch.k0;
+      if (dma) {
+        S.defer_out = true;  // plaintexts move once the replay window has decided (mid)
+        const size_t j0 = ch.k0 - E.k0;
+        bool all = true;
+        for (size_t j = j0; j < j0 + m && all; ++j) all = E.reg_in[j];
+        S.in_dma = all && make_runs(
+            ch.k0, ch.k1, [](size_t) { return true; }, [&](size_t k) { return datagram[t->sel[k]]; },
+            [&](size_t k) { return len[t->sel[k]]; }, [&](size_t k) { return E.off[k - E.k0]; },
+            max_runs(m), E.runs);
+        if (S.in_dma && copy_runs(E.runs, S.d_in, true, S.stream) != hipSuccess) S.in_dma = false;
+      }
+      E.pool->run(m, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = k - E.k0;
           const uint32_t i = t->sel[k];
@@ -777,46 +1076,76 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
             // dst is staging: the replay decision comes after the GPU (session.rs:279-300)
             S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
           } else {
-            std::memcpy(S.h_in + E.off[j], datagram[i], len[i]);
+            if (!S.in_dma) copy_bytes(S.h_in + E.off[j], datagram[i], len[i], nt);
             S.h_desc[kk] = wg_packet_desc{E.off[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
           }
         }
       });
     };
-    std::vector<uint8_t> act;
-    auto unpack = [&](const Chunk &ch, Staging &S) {
-      if (multi) return;  // decided after every engine is back
-      act.assign(ch.k1 - ch.k0, 0);
-      for (size_t kk = 0; kk < act.size(); ++kk) act[kk] = decide(ch.k0 + kk, S, kk);
-      copy_out(E, ch, S, act);
+    // statuses are back: decide in packet order, then (DMA) move what lands in
+    // dst -- plaintext + tag bytes, or ring's zeros + tag on a tag failure -- with
+    // the scatter kernel straight into the registered dst buffers; packets whose
+    // dst is not registered take the chunk's staging copy instead
+    auto mid = [&](const Chunk &ch, Staging &S) -> int {
+      if (multi) return 0;  // decided after every engine is back
+      decide_range(ch.k0, ch.k1, S, 0);
+      if (!S.defer_out) return 0;
+      uint32_t nsc = 0;
+      bool rest = false;
+      for (size_t k = ch.k0; k < ch.k1; ++k) {
+        if (!(t->act[k] & 3)) continue;
+        const size_t j = k - E.k0;
+        if (!E.reg_out[j]) {
+          rest = true;
+          continue;
+        }
+        const uint32_t P = len[t->sel[k]] - WG_DATA_OVERHEAD_SZ;
+        const uint32_t o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
+        S.h_sc[nsc++] = Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE};
+        t->out_dma[k] = 1;
+      }
+      if (nsc) {
+        hipLaunchKernelGGL(scatter_kernel, dim3((nsc + 3u) / 4u), dim3(256), 0, S.stream, S.h_sc, nsc,
+                           (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
+        if (hipGetLastError() != hipSuccess) return -1;
+      }
+      if (rest && hipMemcpyAsync(S.h_out, S.d_out, ch.bytes, hipMemcpyDeviceToHost, S.stream) != hipSuccess)
+        return -1;
+      return 1;
     };
-    return run_chunks(E, false, pack, unpack, direct, false);
+    auto unpack = [&](const Chunk &ch, Staging &S) {
+      if (multi) return;
+      copy_out(E, ch, S);
+    };
+    return run_chunks(E, false, pack, unpack, direct, false, NoHook(), mid);
   };
-  if (!multi) return for_engines(t, engine_job);
-  // several engines: rounds of about engines x chunk_bytes() staging bytes
-  const size_t n = t->sel.size();
-  const uint64_t cap = (uint64_t)chunk_bytes() * t->eng.size();
-  for (size_t a = 0; a < n;) {
-    size_t b = a;
-    uint64_t acc = 0;
-    while (b < n && (b == a || acc + size(b) <= cap)) acc += size(b++);
-    split(t, size, a, b);
-    const int rc = for_engines(t, engine_job);
-    if (rc) return rc;
-    // one chunk per engine, its results still in staging set 0; decided in
-    // packet order (engine ranges are contiguous and ordered)
-    for (Engine *E : t->eng) {
-      if (E->chunks.empty()) continue;
-      for (size_t k = E->k0; k < E->k1; ++k) action[k] = decide(k, E->st[0], k - E->k0);
+  int rc = WG_RC_OK;
+  if (!multi) {
+    rc = for_engines(t, engine_job);
+  } else {
+    // several engines: rounds of about engines x chunk_bytes() staging bytes
+    const size_t n = t->sel.size();
+    const uint64_t cap = (uint64_t)chunk_bytes() * t->eng.size();
+    for (size_t a = 0; a < n && !rc;) {
+      size_t b = a;
+      uint64_t acc = 0;
+      while (b < n && (b == a || acc + size(b) <= cap)) acc += size(b++);
+      split(t, size, a, b);
+      rc = for_engines(t, engine_job);
+      if (rc) break;
+      // one chunk per engine, its results still in staging set 0; decided in
+      // packet order (engine ranges are contiguous and ordered)
+      for (Engine *E : t->eng)
+        if (!E->chunks.empty()) decide_range(E->k0, E->k1, E->st[0], 0);
+      rc = for_engines(t, [&](Engine &E) -> int {
+        if (!E.chunks.empty()) copy_out(E, E.chunks[0], E.st[0]);
+        return WG_RC_OK;
+      });
+      a = b;
     }
-    const int rc2 = for_engines(t, [&](Engine &E) -> int {
-      if (!E.chunks.empty()) copy_out(E, E.chunks[0], E.st[0], action);
-      return WG_RC_OK;
-    });
-    if (rc2) return rc2;
-    a = b;
   }
-  return WG_RC_OK;
+  t->rx_bytes += rx.load();
+  return rc;
 }
 
 void destroy_engine(Engine *E) {
@@ -828,6 +1157,9 @@ void destroy_engine(Engine *E) {
       if (S.stream) (void)hipStreamSynchronize(S.stream);
       free_buffers(S);
       if (S.done) (void)hipEventDestroy(S.done);
+      if (S.done2) (void)hipEventDestroy(S.done2);
+      for (auto &e : S.ev)
+        if (e) (void)hipEventDestroy(e);
       if (S.stream) (void)hipStreamDestroy(S.stream);
     }
   }
@@ -848,6 +1180,7 @@ int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out) {
   for (auto &S : E->st) {
     hipError_t e = hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&S.done2, hipEventDisableTiming);
     if (e != hipSuccess) {
       destroy_engine(E);
       return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", e);
@@ -968,6 +1301,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   if (!t || (n && (!src || !src_len || !dst || !dst_cap || !res)))
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "encapsulate_batch: null", hipSuccess);
   if (n == 0) return WG_RC_OK;
+  PhaseCall pc(t, n);
   Session &s = t->sessions[t->current % WG_N_SESSIONS];  // mod.rs:310
   const uint32_t slot = t->first_slot + 2 * (uint32_t)(t->current % WG_N_SESSIONS) + 1;
   // pass 1 (host, in order): checks and counter reservation
@@ -1002,13 +1336,18 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   // packets carry counters ctr0 + k, disjoint across GPUs
   const uint64_t ctr0 = s.sending_counter;
   s.sending_counter += t->sel.size();
+  pc.checks_done();
   auto size = [&](size_t k) { return round128((uint64_t)src_len[t->sel[k]] + WG_DATA_OVERHEAD_SZ); };
   split(t, size);
+  const bool nt = nt_copies();
   const int rc = for_engines(t, [&](Engine &E) -> int {
-    // direct mode: src and dst of every packet 16-byte aligned inside memory
-    // registered on this engine -> the kernel reads the caller's plaintext and
+    // DMA runs: registered src / dst moved by 2D copies (explicit-copy chunks)
+    const bool dma = dma_possible(t, E);
+    E.zc = zero_copy() && !dma;
+    // direct mode (zero-copy, WG_TUNN_DMA=0): src and dst of every packet 16-byte aligned
+    // inside memory registered on this engine -> the kernel reads the caller's plaintext and
     // writes the caller's datagram over PCIe, no host copies at all
-    bool direct = direct_possible(E);
+    bool direct = !dma && direct_possible(E);
     E.dsrc.resize(E.k1 - E.k0);
     E.ddst.resize(E.k1 - E.k0);
     for (size_t k = E.k0; direct && k < E.k1; ++k) {
@@ -1018,22 +1357,60 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
                dev_addr(E, src[i], src_len[i], E.dsrc[j]) &&
                dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[j]);
     }
+    if (dma) {
+      E.reg_in.assign(E.k1 - E.k0, 0);
+      E.reg_out.assign(E.k1 - E.k0, 0);
+      uint64_t unused;
+      for (size_t k = E.k0; k < E.k1; ++k) {
+        const uint32_t i = t->sel[k];
+        E.reg_in[k - E.k0] = dev_addr(E, src[i], src_len[i], unused);
+        E.reg_out[k - E.k0] = dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[k - E.k0]);
+      }
+    }
     make_chunks(E, size, direct ? ~size_t(0) : 0);
     auto pack = [&](const Chunk &ch, Staging &S) {
-      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+      const size_t m = ch.k1 - ch.k0;
+      if (dma) {  // the whole chunk's plaintexts as DMA runs when they form few of them
+        const size_t j0 = ch.k0 - E.k0;
+        bool all = true;
+        for (size_t j = j0; j < j0 + m && all; ++j) all = E.reg_in[j];
+        S.in_dma = all && make_runs(
+            ch.k0, ch.k1, [](size_t) { return true; },
+            [&](size_t k) { return src[t->sel[k]]; }, [&](size_t k) { return src_len[t->sel[k]]; },
+            [&](size_t k) { return E.off[k - E.k0] + WG_DATA_OFFSET; }, max_runs(m), E.runs);
+        if (S.in_dma && copy_runs(E.runs, S.d_in, true, S.stream) != hipSuccess) S.in_dma = false;
+      }
+      E.pool->run(m, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = k - E.k0;
           const uint32_t i = t->sel[k];
           if (direct) {
             S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.ddst[j], ctr0 + k, src_len[i], slot};
           } else {
-            std::memcpy(S.h_in + E.off[j] + WG_DATA_OFFSET, src[i], src_len[i]);  // NepTUN slot layout
+            if (!S.in_dma)
+              copy_bytes(S.h_in + E.off[j] + WG_DATA_OFFSET, src[i], src_len[i], nt);  // NepTUN slot layout
             S.h_desc[kk] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr0 + k, src_len[i], slot};
           }
         }
       });
     };
+    // the datagrams straight into registered dst (the seal has no in-order decision)
+    auto post = [&](const Chunk &ch, Staging &S) {
+      if (!dma) return 0;
+      const size_t m = ch.k1 - ch.k0, j0 = ch.k0 - E.k0;
+      bool all = true;
+      for (size_t j = j0; j < j0 + m && all; ++j) all = E.reg_out[j];
+      if (!all) return 0;  // (the chunk's datagrams go through pinned staging)
+      for (size_t kk = 0; kk < m; ++kk)
+        S.h_sc[kk] = Scatter{E.ddst[j0 + kk], (uint32_t)E.off[j0 + kk],
+                             src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ, 0, 0};
+      hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((m + 3) / 4)), dim3(256), 0, S.stream, S.h_sc,
+                         (uint32_t)m, (const uint8_t *)S.d_out, (const uint8_t *)S.d_out);
+      S.out_dma = hipGetLastError() == hipSuccess;
+      return 0;
+    };
     auto unpack = [&](const Chunk &ch, Staging &S) {
+      const double a = now_us();
       E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const uint32_t i = t->sel[ch.k0 + kk];
@@ -1043,7 +1420,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
             continue;
           }
           // the whole dst[..P+32]: header, ciphertext, tag (dst[16..] held src before)
-          if (!direct) std::memcpy(dst[i], S.h_out + S.h_desc[kk].dst_off, w);
+          if (!direct && !S.out_dma) copy_bytes(dst[i], S.h_out + S.h_desc[kk].dst_off, w, nt);
           std::memset(&res[i], 0, sizeof res[i]);
           res[i].kind = WG_TUNN_WRITE_TO_NETWORK;
           res[i].len = w;
@@ -1051,8 +1428,9 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
       });
       for (size_t kk = 0; kk < ch.k1 - ch.k0; ++kk)  // mod.rs:321
         if (S.h_st[kk] == WG_STATUS_OK) E.tx += src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
+      E.ph.copy_out_us += now_us() - a;
     };
-    return run_chunks(E, true, pack, unpack, direct, direct);
+    return run_chunks(E, true, pack, unpack, direct, direct, post);
   });
   for (Engine *E : t->eng) t->tx_bytes += E->tx;
   return rc;
@@ -1064,56 +1442,76 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
   if (!t || (n && (!datagram || !len || !dst || !dst_cap || !res)))
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decapsulate_batch: null", hipSuccess);
   if (n == 0) return WG_RC_OK;
-  // pass 1 (stateless checks, reference order): parse, session, dst size, index
+  PhaseCall pc(t, n);
+  // pass 1 (stateless checks, reference order; on the pool): parse, session, dst
+  // size, index -- and each datagram's counter, so the in-order pass never reads
+  // the datagrams again
+  t->code.resize(n);
+  t->ctr_all.resize(n);
+  t->eng[0]->pool->run(n, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const uint8_t *d = datagram[i];
+      const uint32_t L = len[i];
+      std::memset(&res[i], 0, sizeof res[i]);
+      t->code[i] = -1;
+      if (L == 0) {  // "repeated call": send_queued_packet is the CPU Tunn's business
+        res[i].kind = WG_TUNN_NOT_DATA;
+        continue;
+      }
+      const int pk = parse_kind(d, L);
+      if (pk < 0) { set_err(res[i], -pk); continue; }
+      if (pk == 0) {  // handshake init / response / cookie (mod.rs:150-181)
+        res[i].kind = WG_TUNN_NOT_DATA;
+        continue;
+      }
+      const uint32_t ridx = ld32(d + 4);
+      const Session &s = t->sessions[ridx % WG_N_SESSIONS];
+      int32_t e = WG_STATUS_OK;
+      if (!s.live) e = WG_STATUS_NO_CURRENT_SESSION;                                 // mod.rs:553-556
+      else if ((uint64_t)dst_cap[i] < L - WG_DATA_OFFSET) e = WG_STATUS_DESTINATION_BUFFER_TOO_SMALL;  // session.rs:271
+      else if (ridx != s.receiving_index) e = WG_STATUS_WRONG_INDEX;                // session.rs:275
+      if (e) { set_err(res[i], e); continue; }
+      // until its chunk returns a selected packet reads as failed
+      set_err(res[i], WG_STATUS_CRYPTO_FAILED);
+      t->code[i] = (int32_t)(t->first_slot + 2 * (ridx % WG_N_SESSIONS));
+      t->ctr_all[i] = ld64(d + 8);
+    }
+  });
   t->sel.clear();
   t->slot.clear();
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint8_t *d = datagram[i];
-    const uint32_t L = len[i];
-    std::memset(&res[i], 0, sizeof res[i]);
-    if (L == 0) {  // "repeated call": send_queued_packet is the CPU Tunn's business
-      res[i].kind = WG_TUNN_NOT_DATA;
-      continue;
+  t->ctr.clear();
+  for (uint32_t i = 0; i < n; ++i)
+    if (t->code[i] >= 0) {
+      t->sel.push_back(i);
+      t->slot.push_back((uint32_t)t->code[i]);
+      t->ctr.push_back(t->ctr_all[i]);
     }
-    const int pk = parse_kind(d, L);
-    if (pk < 0) { set_err(res[i], -pk); continue; }
-    if (pk == 0) {  // handshake init / response / cookie (mod.rs:150-181)
-      res[i].kind = WG_TUNN_NOT_DATA;
-      continue;
-    }
-    const uint32_t ridx = ld32(d + 4);
-    const Session &s = t->sessions[ridx % WG_N_SESSIONS];
-    int32_t e = WG_STATUS_OK;
-    if (!s.live) e = WG_STATUS_NO_CURRENT_SESSION;                                 // mod.rs:553-556
-    else if ((uint64_t)dst_cap[i] < L - WG_DATA_OFFSET) e = WG_STATUS_DESTINATION_BUFFER_TOO_SMALL;  // session.rs:271
-    else if (ridx != s.receiving_index) e = WG_STATUS_WRONG_INDEX;                // session.rs:275
-    if (e) { set_err(res[i], e); continue; }
-    t->sel.push_back(i);
-    t->slot.push_back(t->first_slot + 2 * (ridx % WG_N_SESSIONS));
-  }
+  pc.checks_done();
   if (t->sel.empty()) return WG_RC_OK;
-  for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);  // until its chunk returns
   // pass 2 (sequential, packet order, per chunk as it returns): replay window,
-  // validation, stats; the byte copies follow on the pools
-  return open_selected(t, datagram, len, dst, [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
-    const uint32_t i = t->sel[k];
-    std::memset(&res[i], 0, sizeof res[i]);
-    const uint8_t *d = datagram[i];
-    const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
-    const uint32_t ridx = ld32(d + 4);
-    const uint64_t ctr = ld64(d + 8);
-    Session &s = t->sessions[ridx % WG_N_SESSIONS];
-    int32_t e = wg_replay_will_accept(&s.window, ctr);  // session.rs:279
-    if (e) { set_err(res[i], e); return 0; }
-    const int32_t g_st = S.h_st[kk];
-    if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }
-    e = wg_replay_mark_did_receive(&s.window, ctr);  // session.rs:300, :192-199
-    if (e) { set_err(res[i], e); return 1; }
-    s.window.receive_cnt += 1;
-    set_current_session(t, ridx);  // mod.rs:562
-    validate(t, S.h_out + S.h_desc[kk].dst_off, P, res[i]);
-    return 1;
-  });
+  // stats; validation and the byte copies follow on the pools
+  return open_selected(
+      t, datagram, len, dst,
+      [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
+        const uint32_t i = t->sel[k];
+        const uint64_t ctr = t->ctr[k];
+        const uint32_t ring = (t->slot[k] - t->first_slot) / 2;
+        Session &s = t->sessions[ring];
+        int32_t e = wg_replay_will_accept(&s.window, ctr);  // session.rs:279
+        if (e) { set_err(res[i], e); return 0; }
+        const int32_t g_st = S.h_st[kk];
+        if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }
+        e = wg_replay_mark_did_receive(&s.window, ctr);  // session.rs:300, :192-199
+        if (e) { set_err(res[i], e); return 1; }
+        s.window.receive_cnt += 1;
+        set_current_session(t, s.receiving_index);  // mod.rs:562 (pass 1: ridx == receiving_index)
+        return 1 | kFinish;
+      },
+      [&](size_t k, const uint8_t *pt, uint32_t P) -> uint64_t {
+        wg_tunn_result &r = res[t->sel[k]];
+        std::memset(&r, 0, sizeof r);
+        return validate(pt, P, r);
+      });
 }
 
 int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
@@ -1122,6 +1520,7 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
   if (!t || (n && (!datagram || !len || !dst || !dst_cap || !res)))
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decrypt_batch: null", hipSuccess);
   if (n == 0) return WG_RC_OK;
+  PhaseCall pc(t, n);
   t->sel.clear();
   t->slot.clear();
   for (uint32_t i = 0; i < n; ++i) {
@@ -1150,16 +1549,52 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
   }
   if (t->sel.empty()) return WG_RC_OK;
   for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);  // until its chunk returns
-  return open_selected(t, datagram, len, dst, [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
-    const uint32_t i = t->sel[k];
-    std::memset(&res[i], 0, sizeof res[i]);
-    const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
-    const int32_t g_st = S.h_st[kk];
-    if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }
-    validate(t, S.h_out + S.h_desc[kk].dst_off, P, res[i]);
-    if (res[i].kind == WG_TUNN_DONE) set_err(res[i], WG_STATUS_UNEXPECTED_PACKET);  // mod.rs:412
-    return 1;
-  });
+  pc.checks_done();
+  return open_selected(
+      t, datagram, len, dst,
+      [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
+        const uint32_t i = t->sel[k];
+        const int32_t g_st = S.h_st[kk];
+        if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }
+        return 1 | kFinish;
+      },
+      [&](size_t k, const uint8_t *pt, uint32_t P) -> uint64_t {
+        wg_tunn_result &r = res[t->sel[k]];
+        std::memset(&r, 0, sizeof r);
+        const uint64_t rx = validate(pt, P, r);
+        if (r.kind == WG_TUNN_DONE) set_err(r, WG_STATUS_UNEXPECTED_PACKET);  // mod.rs:412
+        return rx;
+      });
+}
+
+int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out) {
+  if (!t || !out) return WG_RC_INVALID_ARGUMENT;
+  *out = t->ph;
+  for (const Engine *E : t->eng) {
+    const wg_tunn_phases &p = E->ph;
+    out->chunks += p.chunks;
+    out->pack_us += p.pack_us;
+    out->submit_us += p.submit_us;
+    out->wait_us += p.wait_us;
+    out->copy_out_us += p.copy_out_us;
+    out->dev_h2d_us += p.dev_h2d_us;
+    out->dev_kernel_us += p.dev_kernel_us;
+    out->dev_d2h_us += p.dev_d2h_us;
+  }
+  return WG_RC_OK;
+}
+
+int wg_tunn_reset_phases(wg_tunn *t) {
+  if (!t) return WG_RC_INVALID_ARGUMENT;
+  t->ph = wg_tunn_phases{};
+  for (Engine *E : t->eng) E->ph = wg_tunn_phases{};
+  return WG_RC_OK;
+}
+
+int wg_tunn_set_phase_timing(wg_tunn *t, int on) {
+  if (!t) return WG_RC_INVALID_ARGUMENT;
+  for (Engine *E : t->eng) E->timing = on != 0;
+  return WG_RC_OK;
 }
 
 }  // extern "C"

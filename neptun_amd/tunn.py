@@ -32,6 +32,18 @@ class TunnResult(ctypes.Structure):
                 ("pad", ctypes.c_uint8 * 3)]
 
 
+class Phases(ctypes.Structure):
+    """wg_tunn_phases: where a Tunn's batch time goes (cumulative, microseconds)."""
+    _fields_ = [("calls", ctypes.c_uint64), ("chunks", ctypes.c_uint64), ("packets", ctypes.c_uint64)] + [
+        (f, ctypes.c_double) for f in ("total_us", "checks_us", "pack_us", "submit_us", "wait_us",
+                                       "decide_us", "copy_out_us", "dev_h2d_us", "dev_kernel_us",
+                                       "dev_d2h_us")]
+
+    def as_dict(self):
+        return {f: (round(getattr(self, f), 1) if isinstance(getattr(self, f), float) else getattr(self, f))
+                for f, _ in self._fields_}
+
+
 def _bind(L):
     if getattr(L, "_tunn_bound", False):
         return L
@@ -51,6 +63,9 @@ def _bind(L):
     L.wg_tunn_engines.restype = u32
     L.wg_tunn_engine_info.argtypes = [vp, u32, c.POINTER(c.c_int), c.POINTER(c.c_int)]
     L.wg_tunn_session_counters.argtypes = [vp, u32, c.POINTER(u64), c.POINTER(Replay)]
+    L.wg_tunn_get_phases.argtypes = [vp, c.POINTER(Phases)]
+    L.wg_tunn_reset_phases.argtypes = [vp]
+    L.wg_tunn_set_phase_timing.argtypes = [vp, c.c_int]
     for fn in (L.wg_tunn_encapsulate_batch, L.wg_tunn_decapsulate_batch, L.wg_tunn_decrypt_batch):
         fn.argtypes = [vp, u32, vp, vp, vp, vp, c.POINTER(TunnResult)]
     L._tunn_bound = True
@@ -147,6 +162,17 @@ class Tunn:
         tx, rx = ctypes.c_uint64(), ctypes.c_uint64()
         check(self._lib.wg_tunn_stats(self._h, ctypes.byref(tx), ctypes.byref(rx)), "wg_tunn_stats")
         return tx.value, rx.value
+
+    def phases(self, reset: bool = False) -> dict:
+        """Cumulative phase times (wg_tunn_get_phases); reset=True zeroes them after."""
+        p = Phases()
+        check(self._lib.wg_tunn_get_phases(self._h, ctypes.byref(p)), "wg_tunn_get_phases")
+        if reset:
+            check(self._lib.wg_tunn_reset_phases(self._h), "wg_tunn_reset_phases")
+        return p.as_dict()
+
+    def set_phase_timing(self, on: bool):
+        check(self._lib.wg_tunn_set_phase_timing(self._h, int(bool(on))), "wg_tunn_set_phase_timing")
 
     def session_counters(self, ring_slot):
         c, w = ctypes.c_uint64(), Replay()

@@ -531,3 +531,99 @@ def test_long_running_streams_byte_accounting(gpu):
     assert ctr == total
     a.close()
     b.close()
+
+
+class SlotArena(Arena):
+    """Packets in fixed-size slots of one buffer (a gateway's packet pool): the
+    layout the Tunn moves as DMA runs (one 2D copy per run of equal-length packets)."""
+
+    def __init__(self, blobs, slot, n=None, fill=0xEE):
+        import numpy as np
+        n = len(blobs) if n is None else n
+        self.caps = [slot] * n
+        self.buf = np.full(n * slot + 8192, fill, np.uint8)
+        base = self.buf.ctypes.data
+        self.pad = (-base) % 4096
+        self.offs = (self.pad + slot * np.arange(n)).astype(np.uint64)
+        for o, b in zip(self.offs, blobs):
+            self.buf[int(o):int(o) + len(b)] = np.frombuffer(b, np.uint8)
+        self.ptrs = (base + self.offs).astype(np.uint64)
+        self.lens = np.array([len(b) for b in blobs] + [0] * (n - len(blobs)), np.uint32)
+
+
+@pytest.mark.parametrize("dma", ["1", "0"])
+def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
+    """Registered packet pools with fixed slots (WG_TUNN_DMA=1: 2D DMA runs in and out,
+    the plaintext copied to dst only after the in-order replay decisions; 0: the
+    zero-copy direct kernels), several chunks per batch: mostly 1350-byte packets in
+    order, with a sprinkle of other lengths (runs break), replays, too-old counters,
+    tampered tags (ring's zeros land in dst), wrong indices and keepalives; one batch
+    with a dst outside the registered pool (that chunk falls back to staging).
+    Results, dst bytes, windows and stats equal the sequential model's."""
+    import ctypes
+
+    import numpy as np
+    monkeypatch.setenv("WG_TUNN_DMA", dma)
+    monkeypatch.setenv("WG_TUNN_CHUNK_KB", "2048")
+    rng = random.Random(55)
+    tm, tg, sessions = make_pair(gpu, rng)
+    n, slot = 6000, 1536
+    srcs = [ipv4(rng, 1350 if rng.random() > 0.02 else rng.choice([64, 1349, 700])) for _ in range(n)]
+    a_src, a_dst = SlotArena(srcs, slot), SlotArena([], slot, n)
+    for a in (a_src, a_dst):
+        gpu.register_host(*a.window())
+    caps = np.full(n, slot, np.uint32)
+    dm = [bytearray(b"\xee" * slot) for _ in range(n)]
+    res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dm)]
+    tg.phases(reset=True)
+    res_g = tg.encapsulate_ptrs(a_src.ptrs, a_src.lens, a_dst.ptrs, caps)
+    check_same(res_g, res_m, [bytearray(a_dst.get(k, slot)) for k in range(n)], dm, "slot encap")
+    ph = tg.phases(reset=True)
+    assert ph["calls"] == 1 and ph["packets"] == n and ph["chunks"] >= (4 if dma == "1" else 1)
+    # inbound: the peer's traffic on session 0, in order with damage sprinkled in
+    local, peer, rk, sk = sessions[0]
+    state = {"c": 0}
+
+    def inbound():
+        dgs = []
+        for _ in range(n):
+            c = state["c"]
+            r = rng.random()
+            P = 1350 if rng.random() > 0.02 else rng.choice([0, 64, 1000])
+            pt = ipv4(rng, P) if P else b""
+            ctr = c if r > 0.03 else max(0, c - rng.randrange(1, 40)) if r > 0.015 else max(0, c - 3000)
+            state["c"] = max(c, ctr + 1)
+            d = bytearray(o.format_packet_data(rk, local, ctr, pt))
+            r = rng.random()
+            if r < 0.01:
+                d[rng.randrange(16, len(d))] ^= 0x04
+            elif r < 0.015:
+                d[4:8] = struct.pack("<I", local + 8)
+            dgs.append(bytes(d))
+        return dgs
+
+    for outside in (False, True):
+        dgs = inbound()
+        a_in, a_out = SlotArena(dgs, slot), SlotArena([], slot, n)
+        for a in (a_in, a_out):
+            gpu.register_host(*a.window())
+        out_ptrs = a_out.ptrs.copy()
+        stray = ctypes.create_string_buffer(b"\xee" * slot, slot)
+        if outside:  # one accepted packet's dst in ordinary (unregistered) memory
+            out_ptrs[4321] = ctypes.addressof(stray)
+        dm = [bytearray(b"\xee" * slot) for _ in range(n)]
+        res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+        res_g = tg.decapsulate_ptrs(a_in.ptrs, a_in.lens, out_ptrs, caps)
+        dg = [bytearray(a_out.get(k, slot)) for k in range(n)]
+        if outside:
+            assert res_m[4321][0] == M.WRITE_TO_TUNNEL or res_m[4321][0] == M.ERR
+            dg[4321] = bytearray(stray.raw)
+        check_same(res_g, res_m, dg, dm, f"slot decap (a dst outside the pool: {outside})")
+        kinds = [r[:2] for r in res_m]
+        assert (M.ERR, M.INVALID_AEAD_TAG) in kinds and (M.ERR, M.DUPLICATE_COUNTER) in kinds
+        for a in (a_in, a_out):
+            gpu.unregister_host(a.window()[0])
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    for a in (a_src, a_dst):
+        gpu.unregister_host(a.window()[0])
+    tg.close()

@@ -21,6 +21,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def per_call(ph: dict) -> dict:
+    """wg_tunn_get_phases averaged per batch call."""
+    c = max(1, ph["calls"])
+    out = {k: round(v / c, 1) for k, v in ph.items() if k.endswith("_us")}
+    out["chunks_per_call"] = round(ph["chunks"] / c, 2)
+    return out
+
+
 def main():
     import numpy as np
 
@@ -32,6 +40,8 @@ def main():
     ap.add_argument("--reps", type=int, default=9)
     ap.add_argument("--register", action="store_true",
                     help="register the packet buffers (direct, copy-free batches)")
+    ap.add_argument("--phase-timing", action="store_true",
+                    help="also time the device stages with events (wg_tunn_set_phase_timing)")
     a = ap.parse_args()
     P = a.P
     ctx = neptun_amd.GpuContext(0, key_slots=64)
@@ -63,6 +73,9 @@ def main():
         res = (TunnResult * n)()
         vp = ctypes.c_void_p
         te, td = [], []
+        for t_ in (ta, tb):
+            t_.set_phase_timing(a.phase_timing)
+            t_.phases(reset=True)
         for _ in range(a.reps):
             t0 = time.perf_counter()
             rc = lib.wg_tunn_encapsulate_batch(ta._h, n, vp(src_p.ctypes.data), vp(lens.ctypes.data),
@@ -76,6 +89,7 @@ def main():
             te.append(t1 - t0)
             td.append(t2 - t1)
         ok = bool(np.array_equal(back.reshape(n, S)[:, :P], v[:, :P]))
+        ph_e, ph_d = ta.phases(reset=True), tb.phases(reset=True)
         if a.register:
             for arr in (src, wire, back):
                 ctx.unregister_host(arr.ctypes.data)
@@ -85,7 +99,10 @@ def main():
                           "encap_gbps": round(n * P * 8 / e / 1e9, 1),
                           "decap_gbps": round(n * P * 8 / d / 1e9, 1),
                           "roundtrip_gbps": round(n * P * 8 / (e + d) / 1e9, 1),
-                          "mpps_roundtrip": round(n / (e + d) / 1e6, 3)}), flush=True)
+                          "mpps_roundtrip": round(n / (e + d) / 1e6, 3),
+                          "env": {k: v for k, v in os.environ.items() if k.startswith("WG_TUNN_")},
+                          "phases_encap_per_call_us": per_call(ph_e),
+                          "phases_decap_per_call_us": per_call(ph_d)}), flush=True)
     ta.close()
     tb.close()
 
