@@ -108,21 +108,22 @@ int wg_tunn_stats(const wg_tunn *t, uint64_t *tx_bytes, uint64_t *rx_bytes);
  * current slot is empty or its timer is not newer (mod.rs:528-542).  Default 0. */
 int wg_tunn_set_time(wg_tunn *t, uint64_t now);
 
-/* Direct (copy-free) batches: when the caller's buffers are registered with
- * wg_gpu_register_host (include/neptun_gpu.h) and every packet of an
- * encapsulate batch has 16-byte-aligned src and dst inside registered ranges,
- * the AEAD kernel reads the plaintext from and writes the datagram to the
- * caller's buffers directly over PCIe (no staging copies); decapsulate /
- * decrypt batches read registered datagrams directly (their plaintext is still
- * staged: the replay decision that gates the write to dst comes after the
- * GPU).  Results are identical either way.
+/* Registered (copy-free) batches: when the caller's buffers are registered with
+ * wg_gpu_register_host (include/neptun_gpu.h), no host thread copies packet bytes:
+ * see "Data movement" below.  Results are identical either way.
  *
- * Data movement (both modes, WG_TUNN_ZEROCOPY=1 selects kernels that read and
- * write pinned host memory over PCIe instead): a batch flows in chunks through
- * pinned staging; each chunk is copied to the device by the copy engines
- * (registered datagrams in contiguous runs straight from the caller's memory),
- * opened / sealed in HBM and copied back.  The host copies run on a pool of
- * WG_TUNN_THREADS threads (default: the CPUs this process may use, at most 16). */
+ * Data movement.  A batch flows in chunks (WG_TUNN_CHUNK_KB, default 16 MiB) through
+ * WG_TUNN_SETS (default 2) staging sets.  Registered buffers (one engine): the inputs
+ * go to HBM as 2D copy-engine runs straight from the caller's memory, the AEAD runs
+ * in HBM, and a scatter kernel writes every packet's output bytes into the caller's
+ * registered destination (decapsulate: on per-chunk speculated replay decisions,
+ * repaired after the real in-order pass; WG_TUNN_DMA=0 instead has the AEAD kernels
+ * read -- and, for encapsulate with 16-byte-aligned buffers, write -- the caller's
+ * registered memory directly over PCIe).  Other buffers: the host copies packets into pinned
+ * staging (streaming stores, WG_TUNN_NT=0 for memcpy) on a pool of WG_TUNN_THREADS
+ * threads (default: the CPUs this process may use, at most 16), the kernels read and
+ * write that staging over PCIe (WG_TUNN_ZEROCOPY=0: explicit copies to and from
+ * HBM instead), and the pool copies the results out. */
 /* sending counter of the current session / replay state of a ring slot (for tests) */
 int wg_tunn_session_counters(const wg_tunn *t, uint32_t ring_slot, uint64_t *sending_counter,
                              wg_replay *window);
@@ -161,6 +162,8 @@ typedef struct wg_tunn_phases {
   double decide_us;       /* in-order replay window pass (decapsulate; one thread) */
   double copy_out_us;     /* validation + results out of staging into dst (pool) */
   double dev_h2d_us, dev_kernel_us, dev_d2h_us;  /* device time per stage, summed over chunks */
+  double pack_spec_us;    /* of pack_us: speculated decisions + output jobs (registered decapsulate) */
+  double pack_runs_us;    /* of pack_us: input DMA runs found and enqueued (registered buffers) */
 } wg_tunn_phases;
 int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out);
 int wg_tunn_reset_phases(wg_tunn *t);

@@ -430,6 +430,8 @@ struct Staging {
   // registered caller memory) or deferred until the in-order decisions (mid hook)
   bool in_dma = false, out_dma = false, defer_out = false;
   hipEvent_t done2 = nullptr;  // the deferred outputs (mid) have landed
+  bool spec_ok = false;        // decapsulate DMA: outputs scattered on speculated decisions
+  uint32_t nsc = 0;            // ... that many scatter jobs (h_sc)
   uint8_t stage = 0;           // run_chunks: kIdle / kSubmitted / kOutputs / kReady
   unsigned host_flags = hipHostMallocDefault;  // + hipHostMallocNumaUser on NUMA-bound engines
 };
@@ -551,6 +553,8 @@ struct wg_tunn {
   std::vector<uint64_t> ctr_all, ctr;  // datagram counters: per packet / per selected packet
   std::vector<uint8_t> act;     // per selected packet: what lands in dst (open_selected)
   std::vector<uint8_t> out_dma; // per selected packet: its dst bytes were DMA'd (no host copy)
+  std::vector<uint8_t> spec;    // per selected packet: speculated to land in dst (DMA decapsulate)
+  wg_replay spec_window[WG_N_SESSIONS];  // the speculation's replay windows (this call)
 };
 
 namespace {
@@ -833,6 +837,8 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
     TUNN_HIP(hipEventSynchronize(S.done), "tunn: chunk wait");
     E.ph.wait_us += now_us() - a;
     const int mr = (int)mid(E.chunks[c], S);
+    if (mr == -2)
+      return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: a speculated replay decision was not kept", hipSuccess);
     if (mr < 0) return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: output copies", hipGetLastError());
     if (mr > 0) {  // outputs that waited for the in-order decisions
       if (S.timed) TUNN_HIP(hipEventRecord(S.ev[3], S.stream), "tunn: event");  // (d2h incl. the decide gap)
@@ -992,14 +998,15 @@ uint64_t validate(const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
 //    batch size (a 16M-packet batch over 2 GPUs needs no more than 1 GPU does).
 constexpr uint8_t kFinish = 0x80;
 
-template <class Decide, class Finish>
+template <class Decide, class Finish, class Speculate>
 int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *len,
-                  uint8_t *const *dst, Decide decide, Finish finish) {
+                  uint8_t *const *dst, Decide decide, Finish finish, Speculate speculate) {
   const bool multi = t->eng.size() > 1;
   auto size = [&](size_t k) { return round128(len[t->sel[k]]); };
   if (!multi) split(t, size);
   t->act.assign(t->sel.size(), 0);
   t->out_dma.assign(t->sel.size(), 0);
+  t->spec.assign(t->sel.size(), 0);
   const bool nt = nt_copies();
   std::atomic<uint64_t> rx{0};
   auto copy_out = [&](Engine &E, const Chunk &ch, Staging &S) {
@@ -1058,8 +1065,35 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     auto pack = [&](const Chunk &ch, Staging &S) {
       const size_t m = ch.k1 - ch.k0;
       if (dma) {
-        S.defer_out = true;  // plaintexts move once the replay window has decided (mid)
+        // speculate the in-order decisions as if every tag checks out (speculate(k),
+        // packet order): what is predicted to land in dst is scattered into it right
+        // after the kernel, with no host round trip.  The prediction never lands a
+        // packet the real decisions would not (a failed tag only removes replay
+        // marks, so the speculative window is the stricter one); mid() repairs the
+        // packets it missed, and the kernel has zeroed failed plaintexts already,
+        // which is what lands for them (session.rs:290-296).
         const size_t j0 = ch.k0 - E.k0;
+        const double ta = now_us();
+        uint32_t nsc = 0;
+        bool spec_ok = true;
+        for (size_t k = ch.k0; k < ch.k1; ++k) {
+          const bool lands = speculate(k);
+          t->spec[k] = lands;
+          if (!lands) continue;
+          const size_t j = k - E.k0;
+          if (!E.reg_out[j]) {
+            spec_ok = false;
+            continue;
+          }
+          const uint32_t P = len[t->sel[k]] - WG_DATA_OVERHEAD_SZ;
+          const uint32_t o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
+          S.h_sc[nsc++] = Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE};
+        }
+        S.spec_ok = spec_ok;
+        S.nsc = spec_ok ? nsc : 0u;
+        S.defer_out = !spec_ok;  // else the plaintexts move once the replay window has decided (mid)
+        const double tb = now_us();
+        E.ph.pack_spec_us += tb - ta;
         bool all = true;
         for (size_t j = j0; j < j0 + m && all; ++j) all = E.reg_in[j];
         S.in_dma = all && make_runs(
@@ -1067,6 +1101,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
             [&](size_t k) { return len[t->sel[k]]; }, [&](size_t k) { return E.off[k - E.k0]; },
             max_runs(m), E.runs);
         if (S.in_dma && copy_runs(E.runs, S.d_in, true, S.stream) != hipSuccess) S.in_dma = false;
+        E.ph.pack_runs_us += now_us() - tb;
       }
       E.pool->run(m, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
@@ -1086,9 +1121,39 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     // dst -- plaintext + tag bytes, or ring's zeros + tag on a tag failure -- with
     // the scatter kernel straight into the registered dst buffers; packets whose
     // dst is not registered take the chunk's staging copy instead
+    // the speculated scatter goes right behind the kernel on the chunk's stream
+    auto post = [&](const Chunk &, Staging &S) -> int {
+      if (!dma || !S.spec_ok || !S.nsc) return 0;
+      hipLaunchKernelGGL(scatter_kernel, dim3((S.nsc + 3u) / 4u), dim3(256), 0, S.stream, S.h_sc, S.nsc,
+                         (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
+      S.out_dma = hipGetLastError() == hipSuccess;
+      if (!S.out_dma) S.nsc = 0;
+      return 0;
+    };
     auto mid = [&](const Chunk &ch, Staging &S) -> int {
       if (multi) return 0;  // decided after every engine is back
       decide_range(ch.k0, ch.k1, S, 0);
+      if (dma && S.spec_ok) {
+        // the real decisions against the speculated ones: repair what was missed
+        uint32_t nrep = 0;
+        for (size_t k = ch.k0; k < ch.k1; ++k) {
+          const bool lands = (t->act[k] & 3) != 0;
+          if (!lands) {
+            if (t->spec[k] && S.nsc) return -2;  // (cannot happen: see pack)
+            continue;
+          }
+          t->out_dma[k] = 1;
+          if (t->spec[k] && S.nsc) continue;
+          const size_t j = k - E.k0;
+          const uint32_t P = len[t->sel[k]] - WG_DATA_OVERHEAD_SZ;
+          const uint32_t o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
+          S.h_sc[nrep++] = Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE};
+        }
+        if (!nrep) return 0;
+        hipLaunchKernelGGL(scatter_kernel, dim3((nrep + 3u) / 4u), dim3(256), 0, S.stream, S.h_sc, nrep,
+                           (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
+        return hipGetLastError() == hipSuccess ? 1 : -1;
+      }
       if (!S.defer_out) return 0;
       uint32_t nsc = 0;
       bool rest = false;
@@ -1117,7 +1182,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       if (multi) return;
       copy_out(E, ch, S);
     };
-    return run_chunks(E, false, pack, unpack, direct, false, NoHook(), mid);
+    return run_chunks(E, false, pack, unpack, direct, false, post, mid);
   };
   int rc = WG_RC_OK;
   if (!multi) {
@@ -1371,6 +1436,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
     auto pack = [&](const Chunk &ch, Staging &S) {
       const size_t m = ch.k1 - ch.k0;
       if (dma) {  // the whole chunk's plaintexts as DMA runs when they form few of them
+        const double tb = now_us();
         const size_t j0 = ch.k0 - E.k0;
         bool all = true;
         for (size_t j = j0; j < j0 + m && all; ++j) all = E.reg_in[j];
@@ -1379,6 +1445,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
             [&](size_t k) { return src[t->sel[k]]; }, [&](size_t k) { return src_len[t->sel[k]]; },
             [&](size_t k) { return E.off[k - E.k0] + WG_DATA_OFFSET; }, max_runs(m), E.runs);
         if (S.in_dma && copy_runs(E.runs, S.d_in, true, S.stream) != hipSuccess) S.in_dma = false;
+        E.ph.pack_runs_us += now_us() - tb;
       }
       E.pool->run(m, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
@@ -1488,6 +1555,7 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
     }
   pc.checks_done();
   if (t->sel.empty()) return WG_RC_OK;
+  for (int r = 0; r < WG_N_SESSIONS; ++r) t->spec_window[r] = t->sessions[r].window;
   // pass 2 (sequential, packet order, per chunk as it returns): replay window,
   // stats; validation and the byte copies follow on the pools
   return open_selected(
@@ -1511,6 +1579,12 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
         wg_tunn_result &r = res[t->sel[k]];
         std::memset(&r, 0, sizeof r);
         return validate(pt, P, r);
+      },
+      [&](size_t k) -> bool {  // the same decision with every tag assumed good
+        wg_replay &w = t->spec_window[(t->slot[k] - t->first_slot) / 2];
+        if (wg_replay_will_accept(&w, t->ctr[k])) return false;
+        (void)wg_replay_mark_did_receive(&w, t->ctr[k]);
+        return true;
       });
 }
 
@@ -1564,7 +1638,8 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
         const uint64_t rx = validate(pt, P, r);
         if (r.kind == WG_TUNN_DONE) set_err(r, WG_STATUS_UNEXPECTED_PACKET);  // mod.rs:412
         return rx;
-      });
+      },
+      [](size_t) { return true; });  // (no replay window: every opened packet lands)
 }
 
 int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out) {
@@ -1580,6 +1655,8 @@ int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out) {
     out->dev_h2d_us += p.dev_h2d_us;
     out->dev_kernel_us += p.dev_kernel_us;
     out->dev_d2h_us += p.dev_d2h_us;
+    out->pack_spec_us += p.pack_spec_us;
+    out->pack_runs_us += p.pack_runs_us;
   }
   return WG_RC_OK;
 }

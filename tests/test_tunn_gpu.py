@@ -600,6 +600,15 @@ def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
             elif r < 0.015:
                 d[4:8] = struct.pack("<I", local + 8)
             dgs.append(bytes(d))
+        # a forged copy of a counter first, the real packet later: the forgery must not
+        # mark the counter, so the real one is accepted (the DMA path's speculation --
+        # every tag good -- calls it a duplicate and has to repair it)
+        for at in range(100, n - 10, 997):
+            ctr = struct.unpack_from("<Q", dgs[at + 7], 8)[0]
+            forged = bytearray(dgs[at + 7])
+            forged[-1] ^= 0x80
+            dgs[at] = bytes(forged)
+            assert struct.unpack_from("<Q", dgs[at], 8)[0] == ctr
         return dgs
 
     for outside in (False, True):
