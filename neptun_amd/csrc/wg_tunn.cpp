@@ -532,6 +532,15 @@ struct Engine {
   bool zc = true;                    // this batch's chunks run zero-copy kernels (else explicit copies)
   std::vector<uint8_t> reg_in, reg_out;  // per packet of the share: host buffer registered (DMA runs)
   std::vector<Run> runs;             // scratch
+  // DMA batches (run_dma): batch-sized pinned descriptors / statuses / scatter jobs, the
+  // chunks' input runs, one completion event per chunk, and the repair path's staging
+  wg_packet_desc *b_desc = nullptr;
+  int32_t *b_st = nullptr;
+  Scatter *b_jobs = nullptr;
+  size_t b_cap = 0;
+  std::vector<std::vector<Run>> chunk_runs;
+  std::vector<hipEvent_t> cev;
+  Staging aux;
 };
 
 }  // namespace
@@ -940,6 +949,103 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
   return advance(nc, nc, true);
 }
 
+// DMA batch (registered buffers, one engine): unlike the staged pipeline, the host
+// never waits for a chunk before enqueueing the next -- every chunk's input runs,
+// descriptor copy, AEAD kernel, output scatter and status copy go onto the streams
+// at once (the chunks take the staging sets round robin, and the streams' own order
+// keeps a set's device buffers from being reused early), with the descriptors,
+// statuses and scatter jobs in batch-sized pinned arrays; the host then takes each
+// chunk's results in order as its event completes, overlapping the later chunks.
+// fill(ch, j0, jobs) writes the chunk's descriptors (E.b_desc + j0) and scatter jobs;
+// done(ch, j0) consumes its statuses (E.b_st + j0).  Returns 1 (nothing done) when the
+// batch does not qualify: a packet outside registered memory, or inputs that do not
+// form few enough runs.
+hipError_t reserve_batch(Engine &E, size_t n) {
+  if (n <= E.b_cap) return hipSuccess;
+  (void)hipHostFree(E.b_desc);
+  (void)hipHostFree(E.b_st);
+  (void)hipHostFree(E.b_jobs);
+  E.b_desc = nullptr;
+  E.b_st = nullptr;
+  E.b_jobs = nullptr;
+  E.b_cap = 0;
+  const unsigned fl = E.st[0].host_flags;
+  hipError_t e;
+  if ((e = hipHostMalloc(&E.b_desc, n * sizeof(wg_packet_desc), fl)) != hipSuccess) return e;
+  if ((e = hipHostMalloc(&E.b_st, n * 4, fl)) != hipSuccess) return e;
+  if ((e = hipHostMalloc(&E.b_jobs, n * sizeof(Scatter), fl)) != hipSuccess) return e;
+  E.b_cap = n;
+  return hipSuccess;
+}
+
+template <class InHost, class InLen, class Fill, class Done>
+int run_dma(Engine &E, bool seal, InHost in_host, InLen in_len, Fill fill, Done done) {
+  // (seal: the plaintext goes 16 bytes into its staging slot, NepTUN's layout; open: the datagram at 0)
+  const uint64_t in_shift = seal ? WG_DATA_OFFSET : 0u;
+  const size_t nc = E.chunks.size(), n = E.k1 - E.k0;
+  if (!nc) return WG_RC_OK;
+  // the inputs of every chunk as runs (else the staged pipeline takes the batch)
+  E.chunk_runs.resize(nc);
+  size_t max_bytes = 0, max_m = 0;
+  for (size_t c = 0; c < nc; ++c) {
+    const Chunk &ch = E.chunks[c];
+    if (!make_runs(
+            ch.k0, ch.k1, [](size_t) { return true; }, in_host, in_len,
+            [&](size_t k) { return E.off[k - E.k0] + in_shift; }, max_runs(ch.k1 - ch.k0), E.chunk_runs[c]))
+      return 1;
+    max_bytes = std::max(max_bytes, ch.bytes);
+    max_m = std::max(max_m, ch.k1 - ch.k0);
+  }
+  PipelineDrain drain_guard(E);
+  const size_t sets = pipeline_sets();
+  TUNN_HIP(reserve_batch(E, n), "tunn: batch arrays");
+  for (size_t q = 0; q < sets; ++q) TUNN_HIP(reserve(E.st[q], max_bytes + 128, max_m), "tunn: staging");
+  while (E.cev.size() < nc) {
+    hipEvent_t ev;
+    TUNN_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "tunn: event");
+    E.cev.push_back(ev);
+  }
+  E.ph.chunks += nc;
+  size_t next_done = 0;
+  auto finish_one = [&](size_t c) {
+    const Chunk &ch = E.chunks[c];
+    done(ch, ch.k0 - E.k0);
+  };
+  for (size_t c = 0; c < nc; ++c) {
+    const Chunk &ch = E.chunks[c];
+    const size_t m = ch.k1 - ch.k0, j0 = ch.k0 - E.k0;
+    Staging &S = E.st[c % sets];
+    const double pa = now_us();
+    fill(ch, j0);
+    const double pb = now_us();
+    E.ph.pack_us += pb - pa;
+    TUNN_HIP(copy_runs(E.chunk_runs[c], S.d_in, true, S.stream), "tunn: input runs");
+    TUNN_HIP(hipMemcpyAsync(S.d_desc, E.b_desc + j0, m * sizeof(wg_packet_desc), hipMemcpyHostToDevice,
+                            S.stream),
+             "tunn: descs H2D");
+    const int rc = seal ? wg_gpu_seal_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out, S.d_st, S.stream)
+                        : wg_gpu_open_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out, S.d_st, S.stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((m + 3) / 4)), dim3(256), 0, S.stream, E.b_jobs + j0,
+                       (uint32_t)m, (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
+    TUNN_HIP(hipGetLastError(), "tunn: scatter launch");
+    TUNN_HIP(hipMemcpyAsync(E.b_st + j0, S.d_st, m * 4, hipMemcpyDeviceToHost, S.stream), "tunn: status D2H");
+    TUNN_HIP(hipEventRecord(E.cev[c], S.stream), "tunn: event");
+    S.busy = true;
+    E.ph.submit_us += now_us() - pb;
+    if (const int rc2 = injected_failure(c)) return rc2;
+    // take whatever has landed meanwhile, in order
+    while (next_done < c && hipEventQuery(E.cev[next_done]) == hipSuccess) finish_one(next_done++);
+  }
+  while (next_done < nc) {
+    const double a = now_us();
+    TUNN_HIP(hipEventSynchronize(E.cev[next_done]), "tunn: chunk wait");
+    E.ph.wait_us += now_us() - a;
+    finish_one(next_done++);
+  }
+  return WG_RC_OK;
+}
+
 // parse_incoming_packet (mod.rs:139-199): 1 = data, 0 = handshake/cookie, <0 = -InvalidPacket
 int parse_kind(const uint8_t *d, uint32_t L) {
   if (L < 4) return -WG_STATUS_INVALID_PACKET;
@@ -1009,7 +1115,8 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
   t->spec.assign(t->sel.size(), 0);
   const bool nt = nt_copies();
   std::atomic<uint64_t> rx{0};
-  auto copy_out = [&](Engine &E, const Chunk &ch, Staging &S) {
+  // what lands in dst from pinned staging (pt: the plaintext there), then finish
+  auto copy_out = [&](Engine &E, const Chunk &ch, const uint8_t *h_out, const wg_packet_desc *h_desc) {
     const double a = now_us();
     E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
       uint64_t my_rx = 0;
@@ -1019,10 +1126,10 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
         if (!a) continue;
         const uint32_t i = t->sel[k];
         const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
-        // plaintext (or ring's zeros): DMA'd into dst already, else in the pinned staging
+        // plaintext (or ring's zeros): scattered into dst already, else in the pinned staging
         const bool in_dst = t->out_dma[k];
-        const uint8_t *pt = in_dst ? dst[i] : S.h_out + S.h_desc[kk].dst_off;
-        if (!in_dst) {  // (the scatter kernel wrote plaintext and tag bytes itself)
+        const uint8_t *pt = in_dst ? dst[i] : h_out + h_desc[kk].dst_off;
+        if (!in_dst) {
           if ((a & 3) == 1) copy_bytes(dst[i], pt, P, nt);
           else std::memset(dst[i], 0, P);
           std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
@@ -1033,77 +1140,116 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     });
     E.ph.copy_out_us += now_us() - a;
   };
-  auto decide_range = [&](size_t k0, size_t k1, const Staging &S, size_t kk0) {
+  auto decide_range = [&](size_t k0, size_t k1, const int32_t *st) {
     const double a = now_us();
-    for (size_t k = k0; k < k1; ++k) t->act[k] = decide(k, S, kk0 + (k - k0));
+    for (size_t k = k0; k < k1; ++k) t->act[k] = decide(k, st[k - k0]);
     t->ph.decide_us += now_us() - a;
   };
+  // DMA batch (registered datagrams and destinations, one engine): run_dma with the
+  // replay decisions speculated per chunk (every tag assumed good) so the plaintexts
+  // are scattered into dst right behind the kernel.  The speculation never lands a
+  // packet the real decisions would not -- a failed tag only removes replay marks, so
+  // the speculative window is the stricter one -- and the kernel has zeroed a failed
+  // packet's plaintext already, which is what lands for it (session.rs:290-296).  The
+  // packets it missed (a counter the speculation saw taken by a packet whose tag then
+  // failed) are opened again from their datagrams into E.aux's pinned staging and
+  // copied out by the host.
+  auto dma_batch = [&](Engine &E) -> int {
+    if (multi || !dma_possible(t, E)) return 1;
+    E.ddst.resize(E.k1 - E.k0);
+    uint64_t unused;
+    for (size_t k = E.k0; k < E.k1; ++k) {
+      const uint32_t i = t->sel[k];
+      if (!dev_addr(E, datagram[i], len[i], unused) ||
+          !dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0]))
+        return 1;
+    }
+    make_chunks(E, size);
+    int err = WG_RC_OK;  // a chunk's results could not be taken (reported after the batch)
+    auto fill = [&](const Chunk &ch, size_t j0) {
+      const double a = now_us();
+      for (size_t k = ch.k0; k < ch.k1; ++k) t->spec[k] = speculate(k);  // (in packet order)
+      E.ph.pack_spec_us += now_us() - a;
+      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+        for (size_t kk = lo; kk < hi; ++kk) {
+          const size_t k = ch.k0 + kk, j = j0 + kk;
+          const uint32_t i = t->sel[k];
+          const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ, o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
+          E.b_desc[j] = wg_packet_desc{E.off[j], o, 0, len[i], t->slot[k]};
+          // plaintext then the received tag (ct||tag lands in dst, session.rs:287-289)
+          E.b_jobs[j] = t->spec[k] ? Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE} : Scatter{0, 0, 0, 0, 0};
+        }
+      });
+    };
+    auto done = [&](const Chunk &ch, size_t j0) -> void {
+      if (err) return;
+      decide_range(ch.k0, ch.k1, E.b_st + j0);
+      std::vector<size_t> rep;
+      for (size_t k = ch.k0; k < ch.k1; ++k) {
+        const bool lands = (t->act[k] & 3) != 0;
+        if (lands && !t->spec[k]) rep.push_back(k);
+        t->out_dma[k] = lands && t->spec[k];
+        if (!lands && t->spec[k]) {  // (cannot happen: see above)
+          err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: a speculated replay decision was not kept", hipSuccess);
+          return;
+        }
+      }
+      if (!rep.empty()) {
+        // open the missed packets again into pinned staging; their decisions stand
+        Staging &A = E.aux;
+        uint64_t bytes = 0;
+        for (size_t k : rep) bytes += round128(len[t->sel[k]]);
+        if (const hipError_t e = reserve(A, bytes + 128, rep.size()); e != hipSuccess) {
+          err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair staging", e);
+          return;
+        }
+        uint64_t o = 0;
+        for (size_t r = 0; r < rep.size(); ++r) {
+          const uint32_t i = t->sel[rep[r]];
+          std::memcpy(A.h_in + o, datagram[i], len[i]);
+          A.h_desc[r] = wg_packet_desc{o, o + WG_DATA_OFFSET, 0, len[i], t->slot[rep[r]]};
+          o += round128(len[i]);
+        }
+        if (const int rc = wg_gpu_open_batch(E.ctx, A.h_desc, (uint32_t)rep.size(), A.h_in, A.h_out, A.h_st,
+                                             A.stream)) {
+          err = rc;
+          return;
+        }
+        if (const hipError_t e = hipStreamSynchronize(A.stream); e != hipSuccess) {
+          err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair open", e);
+          return;
+        }
+        for (size_t r = 0; r < rep.size(); ++r) {
+          const size_t k = rep[r];
+          const uint32_t i = t->sel[k];
+          const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
+          if ((t->act[k] & 3) == 1) std::memcpy(dst[i], A.h_out + A.h_desc[r].dst_off, P);
+          else std::memset(dst[i], 0, P);
+          std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
+          t->out_dma[k] = 1;  // (in dst now)
+        }
+      }
+      copy_out(E, ch, nullptr, nullptr);
+    };
+    const int r = run_dma(
+        E, false, [&](size_t k) { return datagram[t->sel[k]]; }, [&](size_t k) { return len[t->sel[k]]; },
+        fill, done);
+    return r ? r : err;
+  };
   auto engine_job = [&](Engine &E) -> int {
-    // DMA runs (one engine, registered buffers): datagrams in, plaintexts out by 2D copies
-    const bool dma = !multi && dma_possible(t, E);
-    E.zc = zero_copy() && !dma;
+    if (const int r = dma_batch(E); r != 1) return r;
+    E.zc = zero_copy();
     make_chunks(E, size, multi ? ~size_t(0) : 0);
     // direct input (zero-copy): every datagram 16-byte aligned inside registered memory
-    bool direct = !dma && direct_possible(E);
+    bool direct = direct_possible(E);
     E.dsrc.resize(E.k1 - E.k0);
     for (size_t k = E.k0; direct && k < E.k1; ++k) {
       const uint32_t i = t->sel[k];
       direct = (reinterpret_cast<uint64_t>(datagram[i]) & 15u) == 0 &&
                dev_addr(E, datagram[i], len[i], E.dsrc[k - E.k0]);
     }
-    if (dma) {
-      E.reg_in.assign(E.k1 - E.k0, 0);
-      E.reg_out.assign(E.k1 - E.k0, 0);
-      E.ddst.resize(E.k1 - E.k0);
-      uint64_t unused;
-      for (size_t k = E.k0; k < E.k1; ++k) {
-        const uint32_t i = t->sel[k];
-        E.reg_in[k - E.k0] = dev_addr(E, datagram[i], len[i], unused);
-        E.reg_out[k - E.k0] = dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0]);
-      }
-    }
     auto pack = [&](const Chunk &ch, Staging &S) {
-      const size_t m = ch.k1 - ch.k0;
-      if (dma) {
-        // speculate the in-order decisions as if every tag checks out (speculate(k),
-        // packet order): what is predicted to land in dst is scattered into it right
-        // after the kernel, with no host round trip.  The prediction never lands a
-        // packet the real decisions would not (a failed tag only removes replay
-        // marks, so the speculative window is the stricter one); mid() repairs the
-        // packets it missed, and the kernel has zeroed failed plaintexts already,
-        // which is what lands for them (session.rs:290-296).
-        const size_t j0 = ch.k0 - E.k0;
-        const double ta = now_us();
-        uint32_t nsc = 0;
-        bool spec_ok = true;
-        for (size_t k = ch.k0; k < ch.k1; ++k) {
-          const bool lands = speculate(k);
-          t->spec[k] = lands;
-          if (!lands) continue;
-          const size_t j = k - E.k0;
-          if (!E.reg_out[j]) {
-            spec_ok = false;
-            continue;
-          }
-          const uint32_t P = len[t->sel[k]] - WG_DATA_OVERHEAD_SZ;
-          const uint32_t o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
-          S.h_sc[nsc++] = Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE};
-        }
-        S.spec_ok = spec_ok;
-        S.nsc = spec_ok ? nsc : 0u;
-        S.defer_out = !spec_ok;  // else the plaintexts move once the replay window has decided (mid)
-        const double tb = now_us();
-        E.ph.pack_spec_us += tb - ta;
-        bool all = true;
-        for (size_t j = j0; j < j0 + m && all; ++j) all = E.reg_in[j];
-        S.in_dma = all && make_runs(
-            ch.k0, ch.k1, [](size_t) { return true; }, [&](size_t k) { return datagram[t->sel[k]]; },
-            [&](size_t k) { return len[t->sel[k]]; }, [&](size_t k) { return E.off[k - E.k0]; },
-            max_runs(m), E.runs);
-        if (S.in_dma && copy_runs(E.runs, S.d_in, true, S.stream) != hipSuccess) S.in_dma = false;
-        E.ph.pack_runs_us += now_us() - tb;
-      }
-      E.pool->run(m, [&](size_t lo, size_t hi) {
+      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = k - E.k0;
           const uint32_t i = t->sel[k];
@@ -1111,78 +1257,21 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
             // dst is staging: the replay decision comes after the GPU (session.rs:279-300)
             S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
           } else {
-            if (!S.in_dma) copy_bytes(S.h_in + E.off[j], datagram[i], len[i], nt);
+            copy_bytes(S.h_in + E.off[j], datagram[i], len[i], nt);
             S.h_desc[kk] = wg_packet_desc{E.off[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
           }
         }
       });
     };
-    // statuses are back: decide in packet order, then (DMA) move what lands in
-    // dst -- plaintext + tag bytes, or ring's zeros + tag on a tag failure -- with
-    // the scatter kernel straight into the registered dst buffers; packets whose
-    // dst is not registered take the chunk's staging copy instead
-    // the speculated scatter goes right behind the kernel on the chunk's stream
-    auto post = [&](const Chunk &, Staging &S) -> int {
-      if (!dma || !S.spec_ok || !S.nsc) return 0;
-      hipLaunchKernelGGL(scatter_kernel, dim3((S.nsc + 3u) / 4u), dim3(256), 0, S.stream, S.h_sc, S.nsc,
-                         (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
-      S.out_dma = hipGetLastError() == hipSuccess;
-      if (!S.out_dma) S.nsc = 0;
+    // statuses are back: decide in packet order (the copies follow in unpack)
+    auto mid = [&](const Chunk &ch, Staging &S) -> int {
+      if (!multi) decide_range(ch.k0, ch.k1, S.h_st);  // (several engines: decided after all are back)
       return 0;
     };
-    auto mid = [&](const Chunk &ch, Staging &S) -> int {
-      if (multi) return 0;  // decided after every engine is back
-      decide_range(ch.k0, ch.k1, S, 0);
-      if (dma && S.spec_ok) {
-        // the real decisions against the speculated ones: repair what was missed
-        uint32_t nrep = 0;
-        for (size_t k = ch.k0; k < ch.k1; ++k) {
-          const bool lands = (t->act[k] & 3) != 0;
-          if (!lands) {
-            if (t->spec[k] && S.nsc) return -2;  // (cannot happen: see pack)
-            continue;
-          }
-          t->out_dma[k] = 1;
-          if (t->spec[k] && S.nsc) continue;
-          const size_t j = k - E.k0;
-          const uint32_t P = len[t->sel[k]] - WG_DATA_OVERHEAD_SZ;
-          const uint32_t o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
-          S.h_sc[nrep++] = Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE};
-        }
-        if (!nrep) return 0;
-        hipLaunchKernelGGL(scatter_kernel, dim3((nrep + 3u) / 4u), dim3(256), 0, S.stream, S.h_sc, nrep,
-                           (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
-        return hipGetLastError() == hipSuccess ? 1 : -1;
-      }
-      if (!S.defer_out) return 0;
-      uint32_t nsc = 0;
-      bool rest = false;
-      for (size_t k = ch.k0; k < ch.k1; ++k) {
-        if (!(t->act[k] & 3)) continue;
-        const size_t j = k - E.k0;
-        if (!E.reg_out[j]) {
-          rest = true;
-          continue;
-        }
-        const uint32_t P = len[t->sel[k]] - WG_DATA_OVERHEAD_SZ;
-        const uint32_t o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
-        S.h_sc[nsc++] = Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE};
-        t->out_dma[k] = 1;
-      }
-      if (nsc) {
-        hipLaunchKernelGGL(scatter_kernel, dim3((nsc + 3u) / 4u), dim3(256), 0, S.stream, S.h_sc, nsc,
-                           (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
-        if (hipGetLastError() != hipSuccess) return -1;
-      }
-      if (rest && hipMemcpyAsync(S.h_out, S.d_out, ch.bytes, hipMemcpyDeviceToHost, S.stream) != hipSuccess)
-        return -1;
-      return 1;
-    };
     auto unpack = [&](const Chunk &ch, Staging &S) {
-      if (multi) return;
-      copy_out(E, ch, S);
+      if (!multi) copy_out(E, ch, S.h_out, S.h_desc);
     };
-    return run_chunks(E, false, pack, unpack, direct, false, post, mid);
+    return run_chunks(E, false, pack, unpack, direct, false, NoHook(), mid);
   };
   int rc = WG_RC_OK;
   if (!multi) {
@@ -1201,9 +1290,9 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       // one chunk per engine, its results still in staging set 0; decided in
       // packet order (engine ranges are contiguous and ordered)
       for (Engine *E : t->eng)
-        if (!E->chunks.empty()) decide_range(E->k0, E->k1, E->st[0], 0);
+        if (!E->chunks.empty()) decide_range(E->k0, E->k1, E->st[0].h_st);
       rc = for_engines(t, [&](Engine &E) -> int {
-        if (!E.chunks.empty()) copy_out(E, E.chunks[0], E.st[0]);
+        if (!E.chunks.empty()) copy_out(E, E.chunks[0], E.st[0].h_out, E.st[0].h_desc);
         return WG_RC_OK;
       });
       a = b;
@@ -1218,6 +1307,13 @@ void destroy_engine(Engine *E) {
   delete E->driver;  // joins the driver thread first
   {
     DevGuard g(E->device);
+    if (E->aux.stream) (void)hipStreamSynchronize(E->aux.stream);
+    (void)hipHostFree(E->b_desc);
+    (void)hipHostFree(E->b_st);
+    (void)hipHostFree(E->b_jobs);
+    for (hipEvent_t ev : E->cev) (void)hipEventDestroy(ev);
+    free_buffers(E->aux);
+    if (E->aux.stream) (void)hipStreamDestroy(E->aux.stream);
     for (auto &S : E->st) {
       if (S.stream) (void)hipStreamSynchronize(S.stream);
       free_buffers(S);
@@ -1250,6 +1346,10 @@ int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out) {
       destroy_engine(E);
       return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", e);
     }
+  }
+  if (hipStreamCreateWithFlags(&E->aux.stream, hipStreamNonBlocking) != hipSuccess) {
+    destroy_engine(E);
+    return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", hipGetLastError());
   }
   E->pool = new (std::nothrow) Pool(pool_workers(engines), E->numa);
   if (multi && E->pool) E->driver = new (std::nothrow) Driver(E->numa);
@@ -1406,13 +1506,61 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   split(t, size);
   const bool nt = nt_copies();
   const int rc = for_engines(t, [&](Engine &E) -> int {
-    // DMA runs: registered src / dst moved by 2D copies (explicit-copy chunks)
-    const bool dma = dma_possible(t, E);
-    E.zc = zero_copy() && !dma;
+    E.zc = zero_copy();
+    // registered src and dst (one engine): the DMA batch -- plaintexts in as runs, the
+    // datagrams scattered straight into dst, no host copies and no waits between chunks
+    if (dma_possible(t, E)) {
+      bool all = true;
+      E.ddst.resize(E.k1 - E.k0);
+      uint64_t unused;
+      for (size_t k = E.k0; k < E.k1 && all; ++k) {
+        const uint32_t i = t->sel[k];
+        all = dev_addr(E, src[i], src_len[i], unused) &&
+              dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[k - E.k0]);
+      }
+      if (all) {
+        make_chunks(E, size);
+        auto fill = [&](const Chunk &ch, size_t j0) {
+          E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+            for (size_t kk = lo; kk < hi; ++kk) {
+              const size_t k = ch.k0 + kk, j = j0 + kk;
+              const uint32_t i = t->sel[k];
+              E.b_desc[j] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr0 + k, src_len[i], slot};
+              E.b_jobs[j] = Scatter{E.ddst[j], (uint32_t)E.off[j], src_len[i] + WG_DATA_OVERHEAD_SZ, 0, 0};
+            }
+          });
+        };
+        auto done = [&](const Chunk &ch, size_t j0) {
+          const double a = now_us();
+          std::atomic<uint64_t> tx{0};
+          E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+            uint64_t my_tx = 0;
+            for (size_t kk = lo; kk < hi; ++kk) {
+              const uint32_t i = t->sel[ch.k0 + kk];
+              if (E.b_st[j0 + kk] != WG_STATUS_OK) {  // the GPU path has no other failure mode
+                set_err(res[i], WG_STATUS_CRYPTO_FAILED);
+                continue;
+              }
+              std::memset(&res[i], 0, sizeof res[i]);
+              res[i].kind = WG_TUNN_WRITE_TO_NETWORK;
+              res[i].len = src_len[i] + WG_DATA_OVERHEAD_SZ;
+              my_tx += res[i].len;  // mod.rs:321
+            }
+            tx.fetch_add(my_tx, std::memory_order_relaxed);
+          });
+          E.tx += tx.load();
+          E.ph.copy_out_us += now_us() - a;
+        };
+        const int r = run_dma(
+            E, true, [&](size_t k) { return src[t->sel[k]]; }, [&](size_t k) { return src_len[t->sel[k]]; },
+            fill, done);
+        if (r != 1) return r;
+      }
+    }
     // direct mode (zero-copy, WG_TUNN_DMA=0): src and dst of every packet 16-byte aligned
     // inside memory registered on this engine -> the kernel reads the caller's plaintext and
     // writes the caller's datagram over PCIe, no host copies at all
-    bool direct = !dma && direct_possible(E);
+    bool direct = direct_possible(E);
     E.dsrc.resize(E.k1 - E.k0);
     E.ddst.resize(E.k1 - E.k0);
     for (size_t k = E.k0; direct && k < E.k1; ++k) {
@@ -1422,59 +1570,20 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
                dev_addr(E, src[i], src_len[i], E.dsrc[j]) &&
                dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[j]);
     }
-    if (dma) {
-      E.reg_in.assign(E.k1 - E.k0, 0);
-      E.reg_out.assign(E.k1 - E.k0, 0);
-      uint64_t unused;
-      for (size_t k = E.k0; k < E.k1; ++k) {
-        const uint32_t i = t->sel[k];
-        E.reg_in[k - E.k0] = dev_addr(E, src[i], src_len[i], unused);
-        E.reg_out[k - E.k0] = dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[k - E.k0]);
-      }
-    }
     make_chunks(E, size, direct ? ~size_t(0) : 0);
     auto pack = [&](const Chunk &ch, Staging &S) {
-      const size_t m = ch.k1 - ch.k0;
-      if (dma) {  // the whole chunk's plaintexts as DMA runs when they form few of them
-        const double tb = now_us();
-        const size_t j0 = ch.k0 - E.k0;
-        bool all = true;
-        for (size_t j = j0; j < j0 + m && all; ++j) all = E.reg_in[j];
-        S.in_dma = all && make_runs(
-            ch.k0, ch.k1, [](size_t) { return true; },
-            [&](size_t k) { return src[t->sel[k]]; }, [&](size_t k) { return src_len[t->sel[k]]; },
-            [&](size_t k) { return E.off[k - E.k0] + WG_DATA_OFFSET; }, max_runs(m), E.runs);
-        if (S.in_dma && copy_runs(E.runs, S.d_in, true, S.stream) != hipSuccess) S.in_dma = false;
-        E.ph.pack_runs_us += now_us() - tb;
-      }
-      E.pool->run(m, [&](size_t lo, size_t hi) {
+      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = k - E.k0;
           const uint32_t i = t->sel[k];
           if (direct) {
             S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.ddst[j], ctr0 + k, src_len[i], slot};
           } else {
-            if (!S.in_dma)
-              copy_bytes(S.h_in + E.off[j] + WG_DATA_OFFSET, src[i], src_len[i], nt);  // NepTUN slot layout
+            copy_bytes(S.h_in + E.off[j] + WG_DATA_OFFSET, src[i], src_len[i], nt);  // NepTUN slot layout
             S.h_desc[kk] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr0 + k, src_len[i], slot};
           }
         }
       });
-    };
-    // the datagrams straight into registered dst (the seal has no in-order decision)
-    auto post = [&](const Chunk &ch, Staging &S) {
-      if (!dma) return 0;
-      const size_t m = ch.k1 - ch.k0, j0 = ch.k0 - E.k0;
-      bool all = true;
-      for (size_t j = j0; j < j0 + m && all; ++j) all = E.reg_out[j];
-      if (!all) return 0;  // (the chunk's datagrams go through pinned staging)
-      for (size_t kk = 0; kk < m; ++kk)
-        S.h_sc[kk] = Scatter{E.ddst[j0 + kk], (uint32_t)E.off[j0 + kk],
-                             src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ, 0, 0};
-      hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((m + 3) / 4)), dim3(256), 0, S.stream, S.h_sc,
-                         (uint32_t)m, (const uint8_t *)S.d_out, (const uint8_t *)S.d_out);
-      S.out_dma = hipGetLastError() == hipSuccess;
-      return 0;
     };
     auto unpack = [&](const Chunk &ch, Staging &S) {
       const double a = now_us();
@@ -1487,7 +1596,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
             continue;
           }
           // the whole dst[..P+32]: header, ciphertext, tag (dst[16..] held src before)
-          if (!direct && !S.out_dma) copy_bytes(dst[i], S.h_out + S.h_desc[kk].dst_off, w, nt);
+          if (!direct) copy_bytes(dst[i], S.h_out + S.h_desc[kk].dst_off, w, nt);
           std::memset(&res[i], 0, sizeof res[i]);
           res[i].kind = WG_TUNN_WRITE_TO_NETWORK;
           res[i].len = w;
@@ -1497,7 +1606,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
         if (S.h_st[kk] == WG_STATUS_OK) E.tx += src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
       E.ph.copy_out_us += now_us() - a;
     };
-    return run_chunks(E, true, pack, unpack, direct, direct, post);
+    return run_chunks(E, true, pack, unpack, direct, direct);
   });
   for (Engine *E : t->eng) t->tx_bytes += E->tx;
   return rc;
@@ -1560,14 +1669,13 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
   // stats; validation and the byte copies follow on the pools
   return open_selected(
       t, datagram, len, dst,
-      [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
+      [&](size_t k, int32_t g_st) -> uint8_t {
         const uint32_t i = t->sel[k];
         const uint64_t ctr = t->ctr[k];
         const uint32_t ring = (t->slot[k] - t->first_slot) / 2;
         Session &s = t->sessions[ring];
         int32_t e = wg_replay_will_accept(&s.window, ctr);  // session.rs:279
         if (e) { set_err(res[i], e); return 0; }
-        const int32_t g_st = S.h_st[kk];
         if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }
         e = wg_replay_mark_did_receive(&s.window, ctr);  // session.rs:300, :192-199
         if (e) { set_err(res[i], e); return 1; }
@@ -1626,9 +1734,8 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
   pc.checks_done();
   return open_selected(
       t, datagram, len, dst,
-      [&](size_t k, const Staging &S, size_t kk) -> uint8_t {
+      [&](size_t k, int32_t g_st) -> uint8_t {
         const uint32_t i = t->sel[k];
-        const int32_t g_st = S.h_st[kk];
         if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }
         return 1 | kFinish;
       },
