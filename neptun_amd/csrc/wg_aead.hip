@@ -1621,20 +1621,30 @@ __device__ __forceinline__ void strided_body(const StridedParams &prm) {
     }
     bool hdr_ready = false;  // (WG_OPEN_HDR_PREFETCH) this group's headers already in the tag park
     (void)hdr_ready;
+    uint32_t g_first = blockIdx.x, g_end = groups, g_step = gridDim.x;
 #if WG_XCD_CONTIG
-    const GroupWalk walk(groups, true);
-#define WALK_STEP walk.step
-#define WALK_END walk.end
-    for (uint32_t grp = walk.first; grp < walk.end; grp += walk.step) {
-#else
-#define WALK_STEP gridDim.x
-#define WALK_END groups
-    for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    {
+      const GroupWalk walk(groups, true);
+      g_first = walk.first;
+      g_end = walk.end;
+      g_step = walk.step;
+    }
 #endif
-      const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
+    // spread launch (WG_SPREAD): one pass over this workgroup's share [s_lo, s_hi) of the full waves
+    const uint32_t s_lo = prm.spread ? spread_lo(prm.n / 64u, blockIdx.x, gridDim.x) : 0u;
+    const uint32_t s_hi = prm.spread ? spread_lo(prm.n / 64u, blockIdx.x + 1u, gridDim.x) : 0u;
+    if (prm.spread) {
+      g_first = 0u;
+      g_end = 1u;
+      g_step = 1u;
+    }
+#define WALK_STEP g_step
+#define WALK_END g_end
+    for (uint32_t grp = g_first; grp < g_end; grp += g_step) {
+      const uint32_t pkt0 = prm.spread ? (s_lo + wave) * 64u : (grp * kWaves + wave) * 64u;
       // only the last group can be partial, and it is this workgroup's last
       // iteration: a wave without packets ends (ended waves leave the barrier)
-      if (pkt0 + 64u > prm.n) return;
+      if (prm.spread ? s_lo + wave >= s_hi : pkt0 + 64u > prm.n) return;
 #if WG_OPEN_HDR_PREFETCH
       // open: this lane's datagram in the wave's next group (0: none), whose header
       // run_wave may prefetch into the tag park
@@ -1744,18 +1754,32 @@ __device__ __forceinline__ void desc_sync_body(const DescParams &prm) {
     for (int j = 0; j < 8; ++j) sk.k[j] = __builtin_amdgcn_readfirstlane(w[j]);
     sk.sidx = __builtin_amdgcn_readfirstlane(prm.key_index[0]);
   }
+  uint32_t g_first = blockIdx.x, g_end = groups, g_step = gridDim.x;
   // (a plan's order is length-sorted: contiguous ranges would hand whole XCDs the
   // long packets, so only unordered launches may take the XCD walk)
 #if WG_XCD_CONTIG
-  const GroupWalk walk(groups, kAffine);
-  for (uint32_t grp = walk.first; grp < walk.end; grp += walk.step) {
-#else
-  for (uint32_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+  {
+    const GroupWalk walk(groups, kAffine);
+    g_first = walk.first;
+    g_end = walk.end;
+    g_step = walk.step;
+  }
 #endif
-    const uint32_t pkt0 = (grp * kWaves + wave) * 64u;
+  // spread launch (WG_SPREAD): one pass over this workgroup's share [s_lo, s_hi) of
+  // the waves (the last one may be partial)
+  const uint32_t waves_all = (prm.n + 63u) / 64u;
+  const uint32_t s_lo = prm.spread ? spread_lo(waves_all, blockIdx.x, gridDim.x) : 0u;
+  const uint32_t s_hi = prm.spread ? spread_lo(waves_all, blockIdx.x + 1u, gridDim.x) : 0u;
+  if (prm.spread) {
+    g_first = 0u;
+    g_end = 1u;
+    g_step = 1u;
+  }
+  for (uint32_t grp = g_first; grp < g_end; grp += g_step) {
+    const uint32_t pkt0 = prm.spread ? (s_lo + wave) * 64u : (grp * kWaves + wave) * 64u;
     // only the last group can lack waves; it is this workgroup's last iteration
-    if (pkt0 >= prm.n) return;
-    const uint32_t alive = min(kWaves, (prm.n - grp * kWaves * 64u + 63u) / 64u);
+    if (prm.spread ? s_lo + wave >= s_hi : pkt0 >= prm.n) return;
+    const uint32_t alive = prm.spread ? s_hi - s_lo : min(kWaves, (prm.n - grp * kWaves * 64u + 63u) / 64u);
     const uint32_t i = pkt0 + lane;
     uint32_t idx = i;
     PacketJob job;

@@ -34,6 +34,20 @@ constexpr uint32_t kStridedBlocksPerCU = WG_STRIDED_BLOCKS_PER_CU;
 #ifndef WG_DESC_SYNC
 #define WG_DESC_SYNC 1  // descriptor batches with non-null bases use the phase-locked kernel
 #endif
+// Under-filled launches -- fewer waves of 64 packets than the persistent grid has
+// wave slots (8 KiB packets at the bench's step payload, a Tunn chunk of a few
+// thousand packets): the host sizes the grid to the waves and sets `spread`, and
+// every workgroup runs its even share of them (at most a workgroup's waves) in one
+// pass.  Without it the first workgroups take whole groups of a workgroup's waves
+// and the rest of the chip idles (172,544 x 8 KiB: 337 groups on 512 slots, 81 CUs
+// with two workgroups, 175 with one).  0: the plain persistent walk.
+#ifndef WG_SPREAD
+#define WG_SPREAD 1
+#endif
+// first wave of workgroup b of `grid` in a spread launch of `waves` waves
+__host__ __device__ inline uint32_t spread_lo(uint32_t waves, uint32_t b, uint32_t grid) {
+  return (uint32_t)(((uint64_t)waves * b) / grid);
+}
 
 struct StridedParams {
   const uint8_t *keys;        // device key table, 32 B per slot
@@ -46,6 +60,7 @@ struct StridedParams {
   uint32_t n, len, key_slot;
   uint32_t pad_tail;          // 1: zero-fill each output to its 128-byte line end (slot padding)
   uint32_t full_in;           // 1: input runs are whole 128-byte lines (launch_strided)
+  uint32_t spread;            // 1: under-filled launch, even wave shares in one pass (WG_SPREAD)
 };
 
 struct DescParams {
@@ -57,6 +72,7 @@ struct DescParams {
   uint8_t *dst;
   int32_t *status;
   uint32_t n, key_slots;
+  uint32_t spread;  // as StridedParams::spread (persistent descriptor kernels)
 };
 
 template <bool kSeal, bool kTail> __global__ void aead_strided_kernel(StridedParams prm);

@@ -172,6 +172,20 @@ int wg_gpu_set_keys(wg_gpu_ctx *ctx, uint32_t first_slot, uint32_t n, const uint
   return WG_RC_OK;
 }
 
+// Persistent grid for `waves` waves of 64 packets (strided / phase-locked descriptor
+// kernels): kStridedBlocksPerCU workgroups per CU walking workgroup-sized groups, or,
+// when the waves do not fill those slots, one workgroup per slot (at most one per
+// wave) with an even share each (`spread`, wg_aead_kernels.h WG_SPREAD)
+static dim3 persistent_grid(const wg_gpu_ctx *ctx, uint32_t waves, uint32_t &spread) {
+  const uint32_t slots = ctx->cus * wg::kStridedBlocksPerCU, per_block = wg::kStridedThreads / 64u;
+  if (WG_SPREAD && waves <= per_block * slots) {
+    spread = 1u;
+    return dim3(std::min(waves, slots));
+  }
+  spread = 0u;
+  return dim3(std::min((waves + per_block - 1u) / per_block, slots));
+}
+
 static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
                        const uint32_t *order, uint32_t n, const uint8_t *src, uint8_t *dst,
                        int32_t *status, void *stream) {
@@ -180,13 +194,12 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
   if (n == 0) return WG_RC_OK;
   DeviceGuard g(ctx->device);
   wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, order, src, dst, status, n,
-                     ctx->key_slots};
+                     ctx->key_slots, 0u};
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (WG_DESC_SYNC && src && dst) {
     // phase-locked, persistent (wg_aead.hip aead_desc_sync_kernel); its compact
     // per-packet tables hold buffer-relative offsets, hence non-null bases
-    const uint32_t groups = (n + wg::kStridedThreads - 1) / wg::kStridedThreads;
-    const dim3 grid(std::min(groups, ctx->cus * wg::kStridedBlocksPerCU));
+    const dim3 grid = persistent_grid(ctx, (n + 63u) / 64u, prm.spread);
     // unordered launches may hold affine workgroups (fixed slots, one length);
     // a plan's permutation gathers packets from all over the batch
     const bool affine = WG_DESC_AFFINE && order == nullptr;
@@ -273,7 +286,7 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
   if (n == 0) return WG_RC_OK;
   DeviceGuard g(ctx->device);
   wg::StridedParams prm{ctx->d_keys, ctx->d_key_index, src, dst, status, src_stride,
-                        dst_stride, counter_base, n, len, key_slot, 0u, 0u};
+                        dst_stride, counter_base, n, len, key_slot, 0u, 0u, 0u};
   // open into plaintext slots that start on 128-byte boundaries: the text
   // run grid keeps every output line whole (wg_aead.hip Ranges)
   const bool text_grid = WG_TEXT_GRID && !seal && ((uintptr_t)dst % 128u) == 0 && dst_stride % 128u == 0;
@@ -297,12 +310,11 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     prm.full_in = in_origin % 128u == 0 && src_stride % 128u == 0;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const uint32_t full_waves = n / 64u, waves_per_block = wg::kStridedThreads / 64u;
+  const uint32_t full_waves = n / 64u;
   if (full_waves) {
     // persistent: kStridedBlocksPerCU resident workgroups per CU walk the
     // workgroup-sized packet groups (wg_aead.hip aead_strided_kernel)
-    const uint32_t groups = (full_waves + waves_per_block - 1) / waves_per_block;
-    const dim3 grid(std::min(groups, ctx->cus * wg::kStridedBlocksPerCU));
+    const dim3 grid = persistent_grid(ctx, full_waves, prm.spread);
     if (seal)
       hipLaunchKernelGGL((wg::aead_strided_kernel<true, false>), grid, dim3(wg::kStridedThreads),
                          0, s, prm);

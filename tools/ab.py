@@ -116,7 +116,7 @@ def main():
     paths = sys.argv[1:]
     if os.environ.get("AB_CONFIG", "2") != "2":
         return main_desc(paths, int(os.environ["AB_CONFIG"]))
-    n, P, S = 1 << 20, int(os.environ.get("AB_SIZE", 1350)), 0
+    n, P, S = int(os.environ.get("AB_N", 1 << 20)), int(os.environ.get("AB_SIZE", 1350)), 0
     oo = int(os.environ.get("AB_OPEN_OFF", 16))  # open's plaintext offset in its output slot
     wo = int(os.environ.get("AB_WIRE_OFF", 0))   # seal's datagram offset in its wire slot
     S = int(os.environ.get("AB_STRIDE", 0)) or synth.round_up(P + 32, 128)
