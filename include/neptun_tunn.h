@@ -163,7 +163,8 @@ typedef struct wg_tunn_phases {
   double copy_out_us;     /* validation + results out of staging into dst (pool) */
   double dev_h2d_us, dev_kernel_us, dev_d2h_us;  /* device time per stage, summed over chunks */
   double pack_spec_us;    /* of pack_us: speculated decisions + output jobs (registered decapsulate) */
-  double pack_runs_us;    /* of pack_us: input DMA runs found and enqueued (registered buffers) */
+  double prep_us;         /* registered (DMA) batches: device addresses, chunks and input runs,
+                             before the first chunk is enqueued */
 } wg_tunn_phases;
 int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out);
 int wg_tunn_reset_phases(wg_tunn *t);

@@ -172,6 +172,48 @@ void copy_bytes(uint8_t *dst, const uint8_t *src, size_t n, bool nt) {
   _mm_sfence();  // streaming stores are weakly ordered: visible before the DMA / caller reads
 }
 
+// DMA batches' output (WG_TUNN_DMA_OUT, read per call): "direct" -- the AEAD kernel
+// stores each packet's output straight into the caller's registered dst; "scatter" --
+// into HBM staging, then a scatter kernel copies it out.  Default: direct for
+// decapsulate, scatter for encapsulate (the seal kernel's 8-packets-per-store pattern
+// writes host memory slower than the scatter kernel's contiguous per-packet stores,
+// while open's direct stores beat staging + scatter: DESIGN.md section 4)
+bool dma_direct_out(bool seal) {
+  const char *e = std::getenv("WG_TUNN_DMA_OUT");
+  if (e && std::strcmp(e, "scatter") == 0) return false;
+  if (e && std::strcmp(e, "direct") == 0) return true;
+  return !seal;
+}
+
+// The chunk's output base for direct output: the lowest of the n device addresses
+// addr(j) (each with its extent ext(j)), or 0 when direct output cannot take the chunk
+// -- an address not 16-byte aligned (the descriptor kernels' alignment rule) or a span
+// the kernels' per-packet offsets cannot hold (2^43 bytes, 16-byte units in 40 bits)
+template <class Addr, class Ext>
+uint64_t direct_base(size_t n, Addr addr, Ext ext) {
+  uint64_t lo = ~0ull, hi = 0;
+  for (size_t j = 0; j < n; ++j) {
+    const uint64_t a = addr(j);
+    if (a & 15u) return 0;
+    lo = std::min(lo, a);
+    hi = std::max(hi, a + ext(j));
+  }
+  return n && hi - lo < (1ull << 43) ? lo : 0;
+}
+
+// Direct-output DMA batches on a copy stream and a kernel stream (WG_TUNN_DMA_STREAMS=0:
+// every stage of a chunk on its staging set's stream), read per call
+bool dma_streams() {
+  const char *e = std::getenv("WG_TUNN_DMA_STREAMS");
+  return !e || std::atoi(e) != 0;
+}
+
+// DMA batches' chunk ramp (make_chunks; WG_TUNN_RAMP=0 turns it off), read per call
+bool dma_ramp() {
+  const char *e = std::getenv("WG_TUNN_RAMP");
+  return !e || std::atoi(e) != 0;
+}
+
 size_t chunk_bytes() {  // staging bytes per pipeline chunk (WG_TUNN_CHUNK_KB overrides, per call)
   const char *e = std::getenv("WG_TUNN_CHUNK_KB");
   return e ? std::max<size_t>(64, (size_t)std::atol(e)) << 10 : size_t(16) << 20;
@@ -268,8 +310,9 @@ class Pool {
     for (auto &t : th_) t.join();
   }
   unsigned size() const { return (unsigned)th_.size() + 1; }
-  void run(size_t n, const std::function<void(size_t, size_t)> &fn) {
-    const unsigned parts = (unsigned)std::min<size_t>(size(), std::max<size_t>(n / 64, 1));
+  // (grain: the fewest items worth a part of their own)
+  void run(size_t n, const std::function<void(size_t, size_t)> &fn, size_t grain = 64) {
+    const unsigned parts = (unsigned)std::min<size_t>(size(), std::max<size_t>(n / std::max<size_t>(grain, 1), 1));
     if (parts <= 1) {
       if (n) fn(0, n);
       return;
@@ -500,6 +543,31 @@ struct Chunk {
   size_t k0, k1, bytes;
 };
 
+// Stable parallel compaction: emit(o, i) for every i in [0, n) with keep(i), o its
+// rank among them, in blocks on the pool (count, prefix, fill); returns the count.
+template <class Keep, class Emit>
+size_t compact(Pool &pool, size_t n, Keep keep, Emit emit) {
+  const size_t blocks = std::max<size_t>(1, std::min<size_t>(256, n / 2048));
+  std::vector<size_t> cnt(blocks + 1, 0);
+  auto lo_of = [&](size_t b) { return n * b / blocks; };
+  pool.run(blocks, [&](size_t b0, size_t b1) {
+    for (size_t b = b0; b < b1; ++b) {
+      size_t c = 0;
+      for (size_t i = lo_of(b); i < lo_of(b + 1); ++i) c += keep(i) ? 1 : 0;
+      cnt[b + 1] = c;
+    }
+  }, 1);
+  for (size_t b = 0; b < blocks; ++b) cnt[b + 1] += cnt[b];
+  pool.run(blocks, [&](size_t b0, size_t b1) {
+    for (size_t b = b0; b < b1; ++b) {
+      size_t o = cnt[b];
+      for (size_t i = lo_of(b); i < lo_of(b + 1); ++i)
+        if (keep(i)) emit(o++, i);
+    }
+  }, 1);
+  return cnt[blocks];
+}
+
 // copy threads per engine incl. its driver: WG_TUNN_THREADS, else the CPUs this
 // process may run on (its affinity mask, not the machine: a GPU box grants a job a
 // share of a larger host) split over the engines, at most 16
@@ -540,6 +608,18 @@ struct Engine {
   size_t b_cap = 0;
   std::vector<std::vector<Run>> chunk_runs;
   std::vector<hipEvent_t> cev;
+  // DMA batches' copy and kernel streams (direct output): the input copies of chunk
+  // c + 1 run under chunk c's kernel; per-chunk events order a chunk's stages and a
+  // staging set's reuse
+  hipStream_t dq[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> ev_in;
+  // direct-output chunks (the AEAD kernel writes the caller's registered dst itself):
+  // per chunk 1 = direct, 0 = staged + scatter; and a pinned sink for the plaintext of
+  // packets whose speculated decision keeps them out of dst (never read back)
+  std::vector<uint8_t> chunk_direct;
+  uint8_t *sink = nullptr;
+  uint64_t sink_dev = 0;
+  size_t sink_cap = 0;
   Staging aux;
 };
 
@@ -624,8 +704,17 @@ inline void set_err(wg_tunn_result &r, int32_t st) {
 
 // device address of [p, p + n) inside memory registered with wg_gpu_register_host
 // on this engine's context (E.reg: the batch's snapshot of its ranges)
-bool dev_addr(const Engine &E, const void *p, uint64_t n, uint64_t &dev) {
+// (hint: the range the caller's previous lookup hit, tried first -- consecutive packets
+// of a pool mostly share one)
+bool dev_addr(const Engine &E, const void *p, uint64_t n, uint64_t &dev, size_t &hint) {
   const uint64_t a = reinterpret_cast<uint64_t>(p);
+  if (hint < E.reg.size() / 3) {
+    const uint64_t *r = &E.reg[3 * hint];
+    if (a >= r[0] && a + n <= r[0] + r[1]) {
+      dev = r[2] + (a - r[0]);
+      return true;
+    }
+  }
   size_t lo = 0, hi = E.reg.size() / 3;  // first range with host > a
   while (lo < hi) {
     const size_t mid = (lo + hi) / 2;
@@ -636,22 +725,66 @@ bool dev_addr(const Engine &E, const void *p, uint64_t n, uint64_t &dev) {
   const uint64_t *r = &E.reg[3 * (lo - 1)];
   if (a + n > r[0] + r[1]) return false;
   dev = r[2] + (a - r[0]);
+  hint = lo - 1;
   return true;
 }
+bool dev_addr(const Engine &E, const void *p, uint64_t n, uint64_t &dev) {
+  size_t hint = ~size_t(0);
+  return dev_addr(E, p, n, dev, hint);
+}
 
-// cut the engine's selected packets (staging size `size(k)` each) into pipeline chunks
+// every packet of the engine's share passes ok(k, hint_a, hint_b) -- on the pool
+template <class Ok>
+bool all_packets(Engine &E, Ok ok) {
+  std::atomic<bool> all{true};
+  E.pool->run(E.k1 - E.k0, [&](size_t lo, size_t hi) {
+    size_t ha = ~size_t(0), hb = ~size_t(0);
+    for (size_t j = lo; j < hi && all.load(std::memory_order_relaxed); ++j)
+      if (!ok(E.k0 + j, ha, hb)) all.store(false, std::memory_order_relaxed);
+  });
+  return all.load();
+}
+
+// cut the engine's selected packets (staging size `size(k)` each) into pipeline chunks;
+// ramp (DMA batches, whose input copies of chunk c + 1 run under chunk c's kernel): the
+// first chunks grow 1/8, 1/4, 1/2 of the limit and the tail is re-cut into halving
+// pieces down to 1/8, so that the copy with no kernel under it at the start and the
+// kernel with no copy under it at the end are short
 template <class SizeFn>
-void make_chunks(Engine &E, SizeFn size, size_t limit = 0) {
+void make_chunks(Engine &E, SizeFn size, size_t limit = 0, bool ramp = false) {
   if (!limit) limit = chunk_bytes();
+  const size_t floor = std::max<size_t>(limit / 8, 1);
+  auto lim = [&](size_t idx) { return ramp && idx < 3 ? std::max(floor, limit >> (3 - idx)) : limit; };
   E.chunks.clear();
   E.off.resize(E.k1 - E.k0);
   size_t k0 = E.k0, bytes = 0;
   for (size_t k = E.k0; k < E.k1; ++k) {
     const uint64_t b = size(k);
-    if (bytes && bytes + b > limit) {
+    if (bytes && bytes + b > lim(E.chunks.size())) {
       E.chunks.push_back(Chunk{k0, k, bytes});
       k0 = k;
       bytes = 0;
+    }
+    E.off[k - E.k0] = bytes;
+    bytes += b;
+  }
+  if (k0 < E.k1) E.chunks.push_back(Chunk{k0, E.k1, bytes});
+  if (!ramp || E.chunks.size() < 4) return;
+  // re-cut the last two chunks: each piece half of what is left, until 1/8 of the limit
+  const size_t a = E.chunks[E.chunks.size() - 2].k0;
+  size_t left = E.chunks[E.chunks.size() - 2].bytes + E.chunks.back().bytes;
+  E.chunks.resize(E.chunks.size() - 2);
+  k0 = a;
+  bytes = 0;
+  size_t target = left > 2 * floor ? left / 2 : left;
+  for (size_t k = a; k < E.k1; ++k) {
+    const uint64_t b = size(k);
+    if (bytes && bytes + b > target) {
+      E.chunks.push_back(Chunk{k0, k, bytes});
+      left -= bytes;
+      k0 = k;
+      bytes = 0;
+      target = left > 2 * floor ? left / 2 : left;
     }
     E.off[k - E.k0] = bytes;
     bytes += b;
@@ -808,6 +941,8 @@ struct PipelineDrain {
         S.busy = false;
         S.stage = 0;
       }
+    for (hipStream_t q : E.dq)
+      if (q) (void)hipStreamSynchronize(q);
   }
 };
 
@@ -956,10 +1091,32 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
 // keeps a set's device buffers from being reused early), with the descriptors,
 // statuses and scatter jobs in batch-sized pinned arrays; the host then takes each
 // chunk's results in order as its event completes, overlapping the later chunks.
-// fill(ch, j0, jobs) writes the chunk's descriptors (E.b_desc + j0) and scatter jobs;
-// done(ch, j0) consumes its statuses (E.b_st + j0).  Returns 1 (nothing done) when the
+// fill(ch, j0, d_out) writes the chunk's descriptors (E.b_desc + j0) and scatter jobs
+// and returns the AEAD kernel's dst base: d_out (the set's HBM staging; descriptors hold
+// staging offsets, scatter jobs copy out) or a host base (direct output: descriptors
+// hold the caller's dst relative to it, no jobs); done(ch, j0) consumes its statuses
+// (E.b_st + j0).  Returns 1 (nothing done) when the
 // batch does not qualify: a packet outside registered memory, or inputs that do not
 // form few enough runs.
+// the direct-output sink, at least `bytes` (pinned, device-mapped); false on failure
+bool grow_sink(Engine &E, size_t bytes) {
+  bytes = std::max<size_t>(bytes, 65536);
+  if (bytes <= E.sink_cap) return true;
+  (void)hipHostFree(E.sink);
+  E.sink = nullptr;
+  E.sink_cap = 0;
+  void *p = nullptr, *d = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocMapped) != hipSuccess) return false;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipHostFree(p);
+    return false;
+  }
+  E.sink = static_cast<uint8_t *>(p);
+  E.sink_dev = reinterpret_cast<uint64_t>(d);
+  E.sink_cap = bytes;
+  return true;
+}
+
 hipError_t reserve_batch(Engine &E, size_t n) {
   if (n <= E.b_cap) return hipSuccess;
   (void)hipHostFree(E.b_desc);
@@ -979,7 +1136,7 @@ hipError_t reserve_batch(Engine &E, size_t n) {
 }
 
 template <class InHost, class InLen, class Fill, class Done>
-int run_dma(Engine &E, bool seal, InHost in_host, InLen in_len, Fill fill, Done done) {
+int run_dma(Engine &E, bool seal, double t_prep, InHost in_host, InLen in_len, Fill fill, Done done) {
   // (seal: the plaintext goes 16 bytes into its staging slot, NepTUN's layout; open: the datagram at 0)
   const uint64_t in_shift = seal ? WG_DATA_OFFSET : 0u;
   const size_t nc = E.chunks.size(), n = E.k1 - E.k0;
@@ -987,25 +1144,34 @@ int run_dma(Engine &E, bool seal, InHost in_host, InLen in_len, Fill fill, Done 
   // the inputs of every chunk as runs (else the staged pipeline takes the batch)
   E.chunk_runs.resize(nc);
   size_t max_bytes = 0, max_m = 0;
-  for (size_t c = 0; c < nc; ++c) {
-    const Chunk &ch = E.chunks[c];
-    if (!make_runs(
-            ch.k0, ch.k1, [](size_t) { return true; }, in_host, in_len,
-            [&](size_t k) { return E.off[k - E.k0] + in_shift; }, max_runs(ch.k1 - ch.k0), E.chunk_runs[c]))
-      return 1;
+  for (const Chunk &ch : E.chunks) {
     max_bytes = std::max(max_bytes, ch.bytes);
     max_m = std::max(max_m, ch.k1 - ch.k0);
   }
+  std::atomic<bool> runs_ok{true};
+  E.pool->run(nc, [&](size_t lo, size_t hi) {
+    for (size_t c = lo; c < hi; ++c) {
+      const Chunk &ch = E.chunks[c];
+      if (!make_runs(
+              ch.k0, ch.k1, [](size_t) { return true; }, in_host, in_len,
+              [&](size_t k) { return E.off[k - E.k0] + in_shift; }, max_runs(ch.k1 - ch.k0), E.chunk_runs[c]))
+        runs_ok.store(false, std::memory_order_relaxed);
+    }
+  }, 1);
+  if (!runs_ok.load()) return 1;
   PipelineDrain drain_guard(E);
+  const bool split_streams = dma_streams();
   const size_t sets = pipeline_sets();
   TUNN_HIP(reserve_batch(E, n), "tunn: batch arrays");
   for (size_t q = 0; q < sets; ++q) TUNN_HIP(reserve(E.st[q], max_bytes + 128, max_m), "tunn: staging");
-  while (E.cev.size() < nc) {
-    hipEvent_t ev;
-    TUNN_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "tunn: event");
-    E.cev.push_back(ev);
-  }
+  for (auto *v : {&E.cev, &E.ev_in})
+    while (v->size() < nc) {
+      hipEvent_t ev;
+      TUNN_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "tunn: event");
+      v->push_back(ev);
+    }
   E.ph.chunks += nc;
+  E.ph.prep_us += now_us() - t_prep;
   size_t next_done = 0;
   auto finish_one = [&](size_t c) {
     const Chunk &ch = E.chunks[c];
@@ -1016,21 +1182,37 @@ int run_dma(Engine &E, bool seal, InHost in_host, InLen in_len, Fill fill, Done 
     const size_t m = ch.k1 - ch.k0, j0 = ch.k0 - E.k0;
     Staging &S = E.st[c % sets];
     const double pa = now_us();
-    fill(ch, j0);
+    uint8_t *const out_base = fill(ch, j0, S.d_out);
+    const bool scatter = out_base == S.d_out;
     const double pb = now_us();
     E.ph.pack_us += pb - pa;
-    TUNN_HIP(copy_runs(E.chunk_runs[c], S.d_in, true, S.stream), "tunn: input runs");
-    TUNN_HIP(hipMemcpyAsync(S.d_desc, E.b_desc + j0, m * sizeof(wg_packet_desc), hipMemcpyHostToDevice,
-                            S.stream),
-             "tunn: descs H2D");
-    const int rc = seal ? wg_gpu_seal_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out, S.d_st, S.stream)
-                        : wg_gpu_open_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out, S.d_st, S.stream);
+    // Direct output: the input copies on the copy stream, the kernel on the kernel
+    // stream, so that chunk c + 1's copies run under chunk c's kernel (the two move
+    // data in opposite directions).  Staged output: input copies, kernel and scatter
+    // on the set's stream (the scatter and the next chunk's kernel on different
+    // streams could share a hardware queue and serialise anyway).  Either way a set's
+    // reuse by chunk c waits for chunk c - sets.
+    const bool split = split_streams && !scatter;
+    hipStream_t qi = split ? E.dq[0] : S.stream, qk = split ? E.dq[1] : S.stream;
+    if (c >= sets) TUNN_HIP(hipStreamWaitEvent(qi, E.cev[c - sets], 0), "tunn: set reuse");
+    TUNN_HIP(copy_runs(E.chunk_runs[c], S.d_in, true, qi), "tunn: input runs");
+    if (split) {
+      TUNN_HIP(hipEventRecord(E.ev_in[c], qi), "tunn: event");
+      TUNN_HIP(hipStreamWaitEvent(qk, E.ev_in[c], 0), "tunn: event wait");
+    }
+    // the kernel reads the descriptors from, and writes the statuses into, the pinned
+    // batch arrays itself: no small copies, which the copy engine would take in
+    // submission order -- chunk c + 1's descriptors behind chunk c's statuses, i.e.
+    // behind chunk c's kernel
+    const int rc = seal ? wg_gpu_seal_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk)
+                        : wg_gpu_open_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk);
     if (rc) return rc;
-    hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((m + 3) / 4)), dim3(256), 0, S.stream, E.b_jobs + j0,
-                       (uint32_t)m, (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
-    TUNN_HIP(hipGetLastError(), "tunn: scatter launch");
-    TUNN_HIP(hipMemcpyAsync(E.b_st + j0, S.d_st, m * 4, hipMemcpyDeviceToHost, S.stream), "tunn: status D2H");
-    TUNN_HIP(hipEventRecord(E.cev[c], S.stream), "tunn: event");
+    if (scatter) {
+      hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((m + 3) / 4)), dim3(256), 0, qk, E.b_jobs + j0,
+                         (uint32_t)m, (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
+      TUNN_HIP(hipGetLastError(), "tunn: scatter launch");
+    }
+    TUNN_HIP(hipEventRecord(E.cev[c], qk), "tunn: event");
     S.busy = true;
     E.ph.submit_us += now_us() - pb;
     if (const int rc2 = injected_failure(c)) return rc2;
@@ -1133,6 +1315,8 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
           if ((a & 3) == 1) copy_bytes(dst[i], pt, P, nt);
           else std::memset(dst[i], 0, P);
           std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
+        } else if (t->out_dma[k] == 2) {  // direct output: the kernel wrote the plaintext only
+          std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
         }
         if (a & kFinish) my_rx += finish(k, in_dst ? dst[i] : pt, P);
       }
@@ -1155,40 +1339,65 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
   // failed) are opened again from their datagrams into E.aux's pinned staging and
   // copied out by the host.
   auto dma_batch = [&](Engine &E) -> int {
+    const double t_prep = now_us();
     if (multi || !dma_possible(t, E)) return 1;
     E.ddst.resize(E.k1 - E.k0);
-    uint64_t unused;
-    for (size_t k = E.k0; k < E.k1; ++k) {
-      const uint32_t i = t->sel[k];
-      if (!dev_addr(E, datagram[i], len[i], unused) ||
-          !dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0]))
-        return 1;
-    }
-    make_chunks(E, size);
+    if (!all_packets(E, [&](size_t k, size_t &ha, size_t &hb) {
+          const uint32_t i = t->sel[k];
+          uint64_t unused;
+          return dev_addr(E, datagram[i], len[i], unused, ha) &&
+                 dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0], hb);
+        }))
+      return 1;
+    make_chunks(E, size, 0, dma_ramp());
     int err = WG_RC_OK;  // a chunk's results could not be taken (reported after the batch)
-    auto fill = [&](const Chunk &ch, size_t j0) {
+    const bool direct_out = dma_direct_out(false);
+    E.chunk_direct.assign(E.chunks.size(), 0);
+    auto fill = [&](const Chunk &ch, size_t j0, uint8_t *d_out) -> uint8_t * {
       const double a = now_us();
-      for (size_t k = ch.k0; k < ch.k1; ++k) t->spec[k] = speculate(k);  // (in packet order)
+      const size_t m = ch.k1 - ch.k0;
+      uint32_t pmax = 0;
+      for (size_t k = ch.k0; k < ch.k1; ++k) {  // (in packet order)
+        t->spec[k] = speculate(k);
+        if (!t->spec[k]) pmax = std::max(pmax, len[t->sel[k]] - (uint32_t)WG_DATA_OVERHEAD_SZ);
+      }
       E.ph.pack_spec_us += now_us() - a;
-      E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+      // direct output: the open kernel writes the plaintext of every packet the
+      // speculation lands straight into its dst (the tag follows from the host, in
+      // copy_out), and that of the others into the pinned sink
+      uint64_t base = 0;
+      if (direct_out && (pmax <= E.sink_cap || grow_sink(E, pmax))) {
+        auto addr = [&](size_t kk) { return t->spec[ch.k0 + kk] ? E.ddst[j0 + kk] : E.sink_dev; };
+        auto ext = [&](size_t kk) { return (uint64_t)len[t->sel[ch.k0 + kk]] - WG_DATA_OVERHEAD_SZ; };
+        base = direct_base(m, addr, ext);
+      }
+      E.chunk_direct[&ch - E.chunks.data()] = base != 0;
+      E.pool->run(m, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = j0 + kk;
           const uint32_t i = t->sel[k];
           const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ, o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
-          E.b_desc[j] = wg_packet_desc{E.off[j], o, 0, len[i], t->slot[k]};
-          // plaintext then the received tag (ct||tag lands in dst, session.rs:287-289)
-          E.b_jobs[j] = t->spec[k] ? Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE} : Scatter{0, 0, 0, 0, 0};
+          if (base) {
+            E.b_desc[j] = wg_packet_desc{E.off[j], (t->spec[k] ? E.ddst[j] : E.sink_dev) - base, 0, len[i],
+                                         t->slot[k]};
+          } else {
+            E.b_desc[j] = wg_packet_desc{E.off[j], o, 0, len[i], t->slot[k]};
+            // plaintext then the received tag (ct||tag lands in dst, session.rs:287-289)
+            E.b_jobs[j] = t->spec[k] ? Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE} : Scatter{0, 0, 0, 0, 0};
+          }
         }
       });
+      return base ? reinterpret_cast<uint8_t *>(base) : d_out;
     };
     auto done = [&](const Chunk &ch, size_t j0) -> void {
       if (err) return;
       decide_range(ch.k0, ch.k1, E.b_st + j0);
       std::vector<size_t> rep;
+      const uint8_t landed = E.chunk_direct[&ch - E.chunks.data()] ? 2 : 1;  // 2: the tag still to write
       for (size_t k = ch.k0; k < ch.k1; ++k) {
         const bool lands = (t->act[k] & 3) != 0;
         if (lands && !t->spec[k]) rep.push_back(k);
-        t->out_dma[k] = lands && t->spec[k];
+        t->out_dma[k] = lands && t->spec[k] ? landed : 0;
         if (!lands && t->spec[k]) {  // (cannot happen: see above)
           err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: a speculated replay decision was not kept", hipSuccess);
           return;
@@ -1232,7 +1441,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       copy_out(E, ch, nullptr, nullptr);
     };
     const int r = run_dma(
-        E, false, [&](size_t k) { return datagram[t->sel[k]]; }, [&](size_t k) { return len[t->sel[k]]; },
+        E, false, t_prep, [&](size_t k) { return datagram[t->sel[k]]; }, [&](size_t k) { return len[t->sel[k]]; },
         fill, done);
     return r ? r : err;
   };
@@ -1308,6 +1517,12 @@ void destroy_engine(Engine *E) {
   {
     DevGuard g(E->device);
     if (E->aux.stream) (void)hipStreamSynchronize(E->aux.stream);
+    for (hipStream_t q : E->dq)
+      if (q) (void)hipStreamSynchronize(q);
+    for (hipStream_t q : E->dq)
+      if (q) (void)hipStreamDestroy(q);
+    (void)hipHostFree(E->sink);
+    for (hipEvent_t ev : E->ev_in) (void)hipEventDestroy(ev);
     (void)hipHostFree(E->b_desc);
     (void)hipHostFree(E->b_st);
     (void)hipHostFree(E->b_jobs);
@@ -1351,6 +1566,12 @@ int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out) {
     destroy_engine(E);
     return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", hipGetLastError());
   }
+  for (hipStream_t &q : E->dq)
+    if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) {
+      q = nullptr;
+      destroy_engine(E);
+      return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", hipGetLastError());
+    }
   E->pool = new (std::nothrow) Pool(pool_workers(engines), E->numa);
   if (multi && E->pool) E->driver = new (std::nothrow) Driver(E->numa);
   if (!E->pool || (multi && !E->driver)) {
@@ -1469,34 +1690,38 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   PhaseCall pc(t, n);
   Session &s = t->sessions[t->current % WG_N_SESSIONS];  // mod.rs:310
   const uint32_t slot = t->first_slot + 2 * (uint32_t)(t->current % WG_N_SESSIONS) + 1;
-  // pass 1 (host, in order): checks and counter reservation
-  t->sel.clear();
-  std::vector<uint32_t> copy_only;  // packets whose src is copied to dst[16..] but not sealed
-  for (uint32_t i = 0; i < n; ++i) {
-    if ((uint64_t)src_len[i] + WG_DATA_OFFSET > dst_cap[i]) {  // encapsulate: dst[16..len+16]
-      set_err(res[i], WG_STATUS_INVALID_LENGTH);
-      continue;
+  // pass 1 (stateless checks, on the pool; the counters are reserved below, once)
+  t->code.resize(n);
+  const bool live = s.live;
+  t->eng[0]->pool->run(n, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      t->code[i] = -1;
+      if ((uint64_t)src_len[i] + WG_DATA_OFFSET > dst_cap[i]) {  // encapsulate: dst[16..len+16]
+        set_err(res[i], WG_STATUS_INVALID_LENGTH);
+        continue;
+      }
+      if (!live) {  // no session: the CPU Tunn queues the packet and starts a handshake
+        std::memset(&res[i], 0, sizeof res[i]);
+        res[i].kind = WG_TUNN_NOT_DATA;
+        res[i].status = WG_STATUS_NO_CURRENT_SESSION;
+      } else if ((uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ > dst_cap[i]) {  // session.rs:210-217
+        set_err(res[i], WG_STATUS_INCORRECT_PACKET_LENGTH);
+      } else {
+        // until its chunk comes back a selected packet reads as failed (a batch that
+        // errors part-way leaves no stale or zeroed results behind)
+        set_err(res[i], WG_STATUS_CRYPTO_FAILED);
+        t->code[i] = 0;
+        continue;
+      }
+      // mod.rs:296-299 copies src into dst[16..] before looking at the session
+      std::memcpy(dst[i] + WG_DATA_OFFSET, src[i], src_len[i]);
     }
-    if (!s.live) {  // no session: the CPU Tunn queues the packet and starts a handshake
-      std::memset(&res[i], 0, sizeof res[i]);
-      res[i].kind = WG_TUNN_NOT_DATA;
-      res[i].status = WG_STATUS_NO_CURRENT_SESSION;
-      copy_only.push_back(i);
-      continue;
-    }
-    if ((uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ > dst_cap[i]) {  // session.rs:210-217
-      set_err(res[i], WG_STATUS_INCORRECT_PACKET_LENGTH);
-      copy_only.push_back(i);
-      continue;
-    }
-    t->sel.push_back(i);
-  }
-  // mod.rs:296-299 copies src into dst[16..] before looking at the session
-  for (uint32_t i : copy_only) std::memcpy(dst[i] + WG_DATA_OFFSET, src[i], src_len[i]);
+  });
+  t->sel.resize(n);
+  t->sel.resize(compact(
+      *t->eng[0]->pool, n, [&](size_t i) { return t->code[i] >= 0; },
+      [&](size_t o, size_t i) { t->sel[o] = (uint32_t)i; }));
   if (t->sel.empty()) return WG_RC_OK;
-  // until its chunk comes back a selected packet reads as failed (a batch that
-  // errors part-way leaves no stale or zeroed results behind)
-  for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);
   // one fetch_add per batch (session.rs:219), BEFORE the split: every engine's
   // packets carry counters ctr0 + k, disjoint across GPUs
   const uint64_t ctr0 = s.sending_counter;
@@ -1509,26 +1734,40 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
     E.zc = zero_copy();
     // registered src and dst (one engine): the DMA batch -- plaintexts in as runs, the
     // datagrams scattered straight into dst, no host copies and no waits between chunks
+    const double t_prep = now_us();
     if (dma_possible(t, E)) {
-      bool all = true;
       E.ddst.resize(E.k1 - E.k0);
-      uint64_t unused;
-      for (size_t k = E.k0; k < E.k1 && all; ++k) {
+      const bool all = all_packets(E, [&](size_t k, size_t &ha, size_t &hb) {
         const uint32_t i = t->sel[k];
-        all = dev_addr(E, src[i], src_len[i], unused) &&
-              dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[k - E.k0]);
-      }
+        uint64_t unused;
+        return dev_addr(E, src[i], src_len[i], unused, ha) &&
+               dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[k - E.k0], hb);
+      });
       if (all) {
-        make_chunks(E, size);
-        auto fill = [&](const Chunk &ch, size_t j0) {
-          E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
+        make_chunks(E, size, 0, dma_ramp());
+        const bool direct_out = dma_direct_out(true);
+        auto fill = [&](const Chunk &ch, size_t j0, uint8_t *d_out) -> uint8_t * {
+          const size_t m = ch.k1 - ch.k0;
+          // direct output: the seal kernel writes each datagram into the caller's dst
+          const uint64_t base = direct_out ? direct_base(
+                                                 m, [&](size_t kk) { return E.ddst[j0 + kk]; },
+                                                 [&](size_t kk) {
+                                                   return (uint64_t)src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
+                                                 })
+                                           : 0;
+          E.pool->run(m, [&](size_t lo, size_t hi) {
             for (size_t kk = lo; kk < hi; ++kk) {
               const size_t k = ch.k0 + kk, j = j0 + kk;
               const uint32_t i = t->sel[k];
-              E.b_desc[j] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr0 + k, src_len[i], slot};
-              E.b_jobs[j] = Scatter{E.ddst[j], (uint32_t)E.off[j], src_len[i] + WG_DATA_OVERHEAD_SZ, 0, 0};
+              if (base) {
+                E.b_desc[j] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.ddst[j] - base, ctr0 + k, src_len[i], slot};
+              } else {
+                E.b_desc[j] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr0 + k, src_len[i], slot};
+                E.b_jobs[j] = Scatter{E.ddst[j], (uint32_t)E.off[j], src_len[i] + WG_DATA_OVERHEAD_SZ, 0, 0};
+              }
             }
           });
+          return base ? reinterpret_cast<uint8_t *>(base) : d_out;
         };
         auto done = [&](const Chunk &ch, size_t j0) {
           const double a = now_us();
@@ -1552,7 +1791,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
           E.ph.copy_out_us += now_us() - a;
         };
         const int r = run_dma(
-            E, true, [&](size_t k) { return src[t->sel[k]]; }, [&](size_t k) { return src_len[t->sel[k]]; },
+            E, true, t_prep, [&](size_t k) { return src[t->sel[k]]; }, [&](size_t k) { return src_len[t->sel[k]]; },
             fill, done);
         if (r != 1) return r;
       }
@@ -1653,15 +1892,19 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
       t->ctr_all[i] = ld64(d + 8);
     }
   });
-  t->sel.clear();
-  t->slot.clear();
-  t->ctr.clear();
-  for (uint32_t i = 0; i < n; ++i)
-    if (t->code[i] >= 0) {
-      t->sel.push_back(i);
-      t->slot.push_back((uint32_t)t->code[i]);
-      t->ctr.push_back(t->ctr_all[i]);
-    }
+  t->sel.resize(n);
+  t->slot.resize(n);
+  t->ctr.resize(n);
+  const size_t nsel = compact(
+      *t->eng[0]->pool, n, [&](size_t i) { return t->code[i] >= 0; },
+      [&](size_t o, size_t i) {
+        t->sel[o] = (uint32_t)i;
+        t->slot[o] = (uint32_t)t->code[i];
+        t->ctr[o] = t->ctr_all[i];
+      });
+  t->sel.resize(nsel);
+  t->slot.resize(nsel);
+  t->ctr.resize(nsel);
   pc.checks_done();
   if (t->sel.empty()) return WG_RC_OK;
   for (int r = 0; r < WG_N_SESSIONS; ++r) t->spec_window[r] = t->sessions[r].window;
@@ -1763,7 +2006,7 @@ int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out) {
     out->dev_kernel_us += p.dev_kernel_us;
     out->dev_d2h_us += p.dev_d2h_us;
     out->pack_spec_us += p.pack_spec_us;
-    out->pack_runs_us += p.pack_runs_us;
+    out->prep_us += p.prep_us;
   }
   return WG_RC_OK;
 }

@@ -37,7 +37,7 @@ class Phases(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("chunks", ctypes.c_uint64), ("packets", ctypes.c_uint64)] + [
         (f, ctypes.c_double) for f in ("total_us", "checks_us", "pack_us", "submit_us", "wait_us",
                                        "decide_us", "copy_out_us", "dev_h2d_us", "dev_kernel_us",
-                                       "dev_d2h_us", "pack_spec_us", "pack_runs_us")]
+                                       "dev_d2h_us", "pack_spec_us", "prep_us")]
 
     def as_dict(self):
         return {f: (round(getattr(self, f), 1) if isinstance(getattr(self, f), float) else getattr(self, f))

@@ -551,11 +551,15 @@ class SlotArena(Arena):
         self.lens = np.array([len(b) for b in blobs] + [0] * (n - len(blobs)), np.uint32)
 
 
-@pytest.mark.parametrize("dma", ["1", "0"])
+@pytest.mark.parametrize("dma", ["1", "1-scatter", "1-direct", "1-nested", "0"])
 def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
-    """Registered packet pools with fixed slots (WG_TUNN_DMA=1: 2D DMA runs in and out,
-    the plaintext copied to dst only after the in-order replay decisions; 0: the
-    zero-copy direct kernels), several chunks per batch: mostly 1350-byte packets in
+    """Registered packet pools with fixed slots (WG_TUNN_DMA=1: DMA batches -- input runs
+    copied to HBM, then the AEAD kernel writes each packet the speculated replay
+    decisions land straight into its dst (direct) or into staging with a scatter kernel
+    copying it out: "1" the defaults (encapsulate scatter, decapsulate direct),
+    "1-scatter" / "1-direct" both operations one way, "1-nested" every stage of a chunk
+    on one stream; 0: the zero-copy direct kernels), several chunks per batch: mostly
+    1350-byte packets in
     order, with a sprinkle of other lengths (runs break), replays, too-old counters,
     tampered tags (ring's zeros land in dst), wrong indices and keepalives; one batch
     with a dst outside the registered pool (that chunk falls back to staging).
@@ -563,7 +567,11 @@ def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
     import ctypes
 
     import numpy as np
-    monkeypatch.setenv("WG_TUNN_DMA", dma)
+    monkeypatch.setenv("WG_TUNN_DMA", dma[0])
+    if dma in ("1-scatter", "1-direct"):
+        monkeypatch.setenv("WG_TUNN_DMA_OUT", dma[2:])
+    if dma == "1-nested":
+        monkeypatch.setenv("WG_TUNN_DMA_STREAMS", "0")
     monkeypatch.setenv("WG_TUNN_CHUNK_KB", "2048")
     rng = random.Random(55)
     tm, tg, sessions = make_pair(gpu, rng)
@@ -579,7 +587,7 @@ def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
     res_g = tg.encapsulate_ptrs(a_src.ptrs, a_src.lens, a_dst.ptrs, caps)
     check_same(res_g, res_m, [bytearray(a_dst.get(k, slot)) for k in range(n)], dm, "slot encap")
     ph = tg.phases(reset=True)
-    assert ph["calls"] == 1 and ph["packets"] == n and ph["chunks"] >= (4 if dma == "1" else 1)
+    assert ph["calls"] == 1 and ph["packets"] == n and ph["chunks"] >= (4 if dma[0] == "1" else 1)
     # inbound: the peer's traffic on session 0, in order with damage sprinkled in
     local, peer, rk, sk = sessions[0]
     state = {"c": 0}
