@@ -909,7 +909,7 @@ hipError_t copy_runs(const std::vector<Run> &runs, uint8_t *dev_base, bool h2d, 
   }
   return hipSuccess;
 }
-size_t max_runs(size_t m) { return std::max<size_t>(4, m / 16); }
+size_t max_runs(size_t m) { return std::max<size_t>(16, m / 16); }  // (16: the ramp's small chunks)
 
 bool dma_possible(wg_tunn *t, Engine &E) {
   if (!dma_runs() || t->eng.size() != 1) return false;
