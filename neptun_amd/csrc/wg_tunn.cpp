@@ -208,10 +208,11 @@ bool dma_streams() {
   return !e || std::atoi(e) != 0;
 }
 
-// DMA batches' chunk ramp (make_chunks; WG_TUNN_RAMP=0 turns it off), read per call
+// DMA batches' chunk ramp (make_chunks; WG_TUNN_RAMP=1 turns it on: it measured
+// nothing, profiles/r04u_tunn_ramp_ab.jsonl), read per call
 bool dma_ramp() {
   const char *e = std::getenv("WG_TUNN_RAMP");
-  return !e || std::atoi(e) != 0;
+  return e && std::atoi(e) != 0;
 }
 
 size_t chunk_bytes() {  // staging bytes per pipeline chunk (WG_TUNN_CHUNK_KB overrides, per call)
@@ -733,16 +734,38 @@ bool dev_addr(const Engine &E, const void *p, uint64_t n, uint64_t &dev) {
   return dev_addr(E, p, n, dev, hint);
 }
 
-// every packet of the engine's share passes ok(k, hint_a, hint_b) -- on the pool
+// every selected packet k in [a, b) passes ok(k, hint_a, hint_b) -- on the pool
 template <class Ok>
-bool all_packets(Engine &E, Ok ok) {
+bool all_packets(Engine &E, size_t a, size_t b, Ok ok) {
   std::atomic<bool> all{true};
-  E.pool->run(E.k1 - E.k0, [&](size_t lo, size_t hi) {
+  E.pool->run(b - a, [&](size_t lo, size_t hi) {
     size_t ha = ~size_t(0), hb = ~size_t(0);
     for (size_t j = lo; j < hi && all.load(std::memory_order_relaxed); ++j)
-      if (!ok(E.k0 + j, ha, hb)) all.store(false, std::memory_order_relaxed);
+      if (!ok(a + j, ha, hb)) all.store(false, std::memory_order_relaxed);
   });
   return all.load();
+}
+template <class Ok>
+bool all_packets(Engine &E, Ok ok) {
+  return all_packets(E, E.k0, E.k1, ok);
+}
+
+// append the selected packets [a, b) to the engine's chunks (E.off indexed from E.k0)
+template <class SizeFn>
+void append_chunks(Engine &E, SizeFn size, size_t a, size_t b, size_t limit) {
+  E.off.resize(b - E.k0);
+  size_t k0 = a, bytes = 0;
+  for (size_t k = a; k < b; ++k) {
+    const uint64_t x = size(k);
+    if (bytes && bytes + x > limit) {
+      E.chunks.push_back(Chunk{k0, k, bytes});
+      k0 = k;
+      bytes = 0;
+    }
+    E.off[k - E.k0] = bytes;
+    bytes += x;
+  }
+  if (k0 < b) E.chunks.push_back(Chunk{k0, b, bytes});
 }
 
 // cut the engine's selected packets (staging size `size(k)` each) into pipeline chunks;
@@ -797,6 +820,12 @@ void make_chunks(Engine &E, SizeFn size, size_t limit = 0, bool ramp = false) {
 template <class SizeFn>
 void split(wg_tunn *t, SizeFn size, size_t a = 0, size_t b = ~size_t(0)) {
   const size_t n = std::min(b, t->sel.size()), E = t->eng.size();
+  if (E == 1) {
+    t->eng[0]->k0 = a;
+    t->eng[0]->k1 = n;
+    t->eng[0]->tx = 0;
+    return;
+  }
   uint64_t total = 0;
   for (size_t k = a; k < n; ++k) total += size(k);
   size_t k = a;
@@ -1135,49 +1164,67 @@ hipError_t reserve_batch(Engine &E, size_t n) {
   return hipSuccess;
 }
 
-template <class InHost, class InLen, class Fill, class Done>
-int run_dma(Engine &E, bool seal, double t_prep, InHost in_host, InLen in_len, Fill fill, Done done) {
+// more() runs once, right after chunk 0 is enqueued: 0 -- it appended chunks (the rest
+// of a batch whose selection was cut short to start the device early), 1 -- nothing to
+// add, 2 -- the rest cannot take a DMA batch.  Returns WG_RC_OK, an error, 1 (the batch
+// does not qualify, nothing done) or 2 (the chunks [0, E.chunks.size()) are done and
+// the selected packets from E.k1 on are left for the caller).  n_cap bounds the
+// packets of the whole batch (the batch arrays are sized for it up front).
+template <class InHost, class InLen, class Fill, class Done, class More>
+int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, InLen in_len, Fill fill, Done done,
+            More more) {
   // (seal: the plaintext goes 16 bytes into its staging slot, NepTUN's layout; open: the datagram at 0)
   const uint64_t in_shift = seal ? WG_DATA_OFFSET : 0u;
-  const size_t nc = E.chunks.size(), n = E.k1 - E.k0;
-  if (!nc) return WG_RC_OK;
+  const size_t nc0 = E.chunks.size(), n = E.k1 - E.k0;
+  if (!nc0) return WG_RC_OK;
+  const bool may_grow = n_cap > n;
   // the inputs of every chunk as runs (else the staged pipeline takes the batch)
-  E.chunk_runs.resize(nc);
-  size_t max_bytes = 0, max_m = 0;
+  // the input runs of chunks [c0, c1) (false: too many runs for copies)
+  auto build_runs = [&](size_t c0, size_t c1) {
+    E.chunk_runs.resize(c1);
+    std::atomic<bool> runs_ok{true};
+    E.pool->run(c1 - c0, [&](size_t lo, size_t hi) {
+      for (size_t c = c0 + lo; c < c0 + hi; ++c) {
+        const Chunk &ch = E.chunks[c];
+        if (!make_runs(
+                ch.k0, ch.k1, [](size_t) { return true; }, in_host, in_len,
+                [&](size_t k) { return E.off[k - E.k0] + in_shift; }, max_runs(ch.k1 - ch.k0), E.chunk_runs[c]))
+          runs_ok.store(false, std::memory_order_relaxed);
+      }
+    }, 1);
+    return runs_ok.load();
+  };
+  // staging: the chunks there are, or a full chunk when more may come (the sets are
+  // in use by then: they cannot grow)
+  size_t max_bytes = may_grow ? chunk_bytes() : 0, max_m = may_grow ? chunk_bytes() / 128 + 1 : 0;
   for (const Chunk &ch : E.chunks) {
     max_bytes = std::max(max_bytes, ch.bytes);
     max_m = std::max(max_m, ch.k1 - ch.k0);
   }
-  std::atomic<bool> runs_ok{true};
-  E.pool->run(nc, [&](size_t lo, size_t hi) {
-    for (size_t c = lo; c < hi; ++c) {
-      const Chunk &ch = E.chunks[c];
-      if (!make_runs(
-              ch.k0, ch.k1, [](size_t) { return true; }, in_host, in_len,
-              [&](size_t k) { return E.off[k - E.k0] + in_shift; }, max_runs(ch.k1 - ch.k0), E.chunk_runs[c]))
-        runs_ok.store(false, std::memory_order_relaxed);
-    }
-  }, 1);
-  if (!runs_ok.load()) return 1;
+  if (!build_runs(0, nc0)) return 1;
   PipelineDrain drain_guard(E);
   const bool split_streams = dma_streams();
   const size_t sets = pipeline_sets();
-  TUNN_HIP(reserve_batch(E, n), "tunn: batch arrays");
+  TUNN_HIP(reserve_batch(E, std::max(n, n_cap)), "tunn: batch arrays");
   for (size_t q = 0; q < sets; ++q) TUNN_HIP(reserve(E.st[q], max_bytes + 128, max_m), "tunn: staging");
-  for (auto *v : {&E.cev, &E.ev_in})
-    while (v->size() < nc) {
-      hipEvent_t ev;
-      TUNN_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "tunn: event");
-      v->push_back(ev);
-    }
-  E.ph.chunks += nc;
+  auto events = [&](size_t count) -> hipError_t {
+    for (auto *v : {&E.cev, &E.ev_in})
+      while (v->size() < count) {
+        hipEvent_t ev;
+        if (const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming); e != hipSuccess) return e;
+        v->push_back(ev);
+      }
+    return hipSuccess;
+  };
+  TUNN_HIP(events(nc0), "tunn: event");
   E.ph.prep_us += now_us() - t_prep;
+  bool left_over = false;  // more() left the rest of the batch to the caller
   size_t next_done = 0;
   auto finish_one = [&](size_t c) {
     const Chunk &ch = E.chunks[c];
     done(ch, ch.k0 - E.k0);
   };
-  for (size_t c = 0; c < nc; ++c) {
+  for (size_t c = 0; c < E.chunks.size(); ++c) {
     const Chunk &ch = E.chunks[c];
     const size_t m = ch.k1 - ch.k0, j0 = ch.k0 - E.k0;
     Staging &S = E.st[c % sets];
@@ -1216,16 +1263,37 @@ int run_dma(Engine &E, bool seal, double t_prep, InHost in_host, InLen in_len, F
     S.busy = true;
     E.ph.submit_us += now_us() - pb;
     if (const int rc2 = injected_failure(c)) return rc2;
+    if (c == 0) {  // the rest of the batch (chunk 0 is on the device meanwhile)
+      const double a = now_us();
+      const size_t had = E.chunks.size(), k_had = E.k1;
+      const int mr = more();
+      if (mr == 0) {
+        bool fits = true;
+        for (size_t x = had; x < E.chunks.size(); ++x)
+          fits = fits && E.chunks[x].bytes <= max_bytes && E.chunks[x].k1 - E.chunks[x].k0 <= max_m;
+        if (!fits || !build_runs(had, E.chunks.size())) {
+          E.chunks.resize(had);  // (the rest goes back to the caller)
+          E.k1 = k_had;
+          left_over = true;
+        }
+        TUNN_HIP(events(E.chunks.size()), "tunn: event");
+      } else if (mr == 2) {
+        left_over = true;
+      }
+      E.ph.prep_us += now_us() - a;
+    }
     // take whatever has landed meanwhile, in order
     while (next_done < c && hipEventQuery(E.cev[next_done]) == hipSuccess) finish_one(next_done++);
   }
+  const size_t nc = E.chunks.size();
+  E.ph.chunks += nc;
   while (next_done < nc) {
     const double a = now_us();
     TUNN_HIP(hipEventSynchronize(E.cev[next_done]), "tunn: chunk wait");
     E.ph.wait_us += now_us() - a;
     finish_one(next_done++);
   }
-  return WG_RC_OK;
+  return left_over ? 2 : WG_RC_OK;
 }
 
 // parse_incoming_packet (mod.rs:139-199): 1 = data, 0 = handshake/cookie, <0 = -InvalidPacket
@@ -1286,15 +1354,32 @@ uint64_t validate(const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
 //    batch size (a 16M-packet batch over 2 GPUs needs no more than 1 GPU does).
 constexpr uint8_t kFinish = 0x80;
 
-template <class Decide, class Finish, class Speculate>
+// partial: t->sel holds only the selection of the batch's first packets, and grow()
+// appends the rest (in order) -- so that a registered DMA batch can put its first chunk
+// on the device while the host is still checking the rest (pass 1); every other path
+// grows the selection first.  n_cap: the batch's packet count.
+template <class Decide, class Finish, class Speculate, class Grow>
 int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *len,
-                  uint8_t *const *dst, Decide decide, Finish finish, Speculate speculate) {
+                  uint8_t *const *dst, Decide decide, Finish finish, Speculate speculate, Grow grow,
+                  bool partial, size_t n_cap) {
   const bool multi = t->eng.size() > 1;
+  if (partial && (multi || !dma_runs())) {
+    grow();
+    partial = false;
+  }
   auto size = [&](size_t k) { return round128(len[t->sel[k]]); };
   if (!multi) split(t, size);
   t->act.assign(t->sel.size(), 0);
   t->out_dma.assign(t->sel.size(), 0);
   t->spec.assign(t->sel.size(), 0);
+  auto grow_all = [&]() {  // the full selection, and the per-packet state sized for it
+    if (!partial) return;
+    grow();
+    partial = false;
+    t->act.resize(t->sel.size(), 0);
+    t->out_dma.resize(t->sel.size(), 0);
+    t->spec.resize(t->sel.size(), 0);
+  };
   const bool nt = nt_copies();
   std::atomic<uint64_t> rx{0};
   // what lands in dst from pinned staging (pt: the plaintext there), then finish
@@ -1338,17 +1423,24 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
   // packets it missed (a counter the speculation saw taken by a packet whose tag then
   // failed) are opened again from their datagrams into E.aux's pinned staging and
   // copied out by the host.
+  auto registered = [&](Engine &E, size_t a, size_t b) {  // datagrams and dsts of [a, b)
+    E.ddst.resize(b - E.k0);
+    return all_packets(E, a, b, [&](size_t k, size_t &ha, size_t &hb) {
+      const uint32_t i = t->sel[k];
+      uint64_t unused;
+      return dev_addr(E, datagram[i], len[i], unused, ha) &&
+             dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0], hb);
+    });
+  };
   auto dma_batch = [&](Engine &E) -> int {
     const double t_prep = now_us();
-    if (multi || !dma_possible(t, E)) return 1;
-    E.ddst.resize(E.k1 - E.k0);
-    if (!all_packets(E, [&](size_t k, size_t &ha, size_t &hb) {
-          const uint32_t i = t->sel[k];
-          uint64_t unused;
-          return dev_addr(E, datagram[i], len[i], unused, ha) &&
-                 dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0], hb);
-        }))
+    if (multi || !dma_possible(t, E) || !registered(E, E.k0, E.k1)) {
+      if (partial) {  // not for a DMA batch after all: the staged path takes the whole selection
+        grow_all();
+        split(t, size);
+      }
       return 1;
+    }
     make_chunks(E, size, 0, dma_ramp());
     int err = WG_RC_OK;  // a chunk's results could not be taken (reported after the batch)
     const bool direct_out = dma_direct_out(false);
@@ -1440,13 +1532,34 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       }
       copy_out(E, ch, nullptr, nullptr);
     };
+    auto more = [&]() -> int {
+      if (!partial) return 1;
+      const size_t had = t->sel.size();
+      grow_all();
+      if (t->sel.size() == had) return 1;
+      if (!registered(E, had, t->sel.size())) return 2;
+      append_chunks(E, size, had, t->sel.size(), chunk_bytes());
+      E.k1 = t->sel.size();
+      E.chunk_direct.resize(E.chunks.size(), 0);
+      return 0;
+    };
     const int r = run_dma(
-        E, false, t_prep, [&](size_t k) { return datagram[t->sel[k]]; }, [&](size_t k) { return len[t->sel[k]]; },
-        fill, done);
-    return r ? r : err;
+        E, false, t_prep, n_cap, [&](size_t k) { return datagram[t->sel[k]]; },
+        [&](size_t k) { return len[t->sel[k]]; }, fill, done, more);
+    if (r == 1 && partial) {  // (nothing was done)
+      grow_all();
+      split(t, size);
+    }
+    return err ? err : r;
   };
   auto engine_job = [&](Engine &E) -> int {
-    if (const int r = dma_batch(E); r != 1) return r;
+    if (const int r = dma_batch(E); r == 2) {  // the rest of the batch: staged
+      grow_all();
+      E.k0 = E.k1;
+      E.k1 = t->sel.size();
+    } else if (r != 1) {
+      return r;
+    }
     E.zc = zero_copy();
     make_chunks(E, size, multi ? ~size_t(0) : 0);
     // direct input (zero-copy): every datagram 16-byte aligned inside registered memory
@@ -1791,8 +1904,8 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
           E.ph.copy_out_us += now_us() - a;
         };
         const int r = run_dma(
-            E, true, t_prep, [&](size_t k) { return src[t->sel[k]]; }, [&](size_t k) { return src_len[t->sel[k]]; },
-            fill, done);
+            E, true, t_prep, 0, [&](size_t k) { return src[t->sel[k]]; },
+            [&](size_t k) { return src_len[t->sel[k]]; }, fill, done, [] { return 1; });
         if (r != 1) return r;
       }
     }
@@ -1860,51 +1973,71 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
   PhaseCall pc(t, n);
   // pass 1 (stateless checks, reference order; on the pool): parse, session, dst
   // size, index -- and each datagram's counter, so the in-order pass never reads
-  // the datagrams again
+  // the datagrams again.  Over packets [lo, hi), appending to the selection.
   t->code.resize(n);
   t->ctr_all.resize(n);
-  t->eng[0]->pool->run(n, [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) {
-      const uint8_t *d = datagram[i];
-      const uint32_t L = len[i];
-      std::memset(&res[i], 0, sizeof res[i]);
-      t->code[i] = -1;
-      if (L == 0) {  // "repeated call": send_queued_packet is the CPU Tunn's business
-        res[i].kind = WG_TUNN_NOT_DATA;
-        continue;
+  t->sel.clear();
+  t->slot.clear();
+  t->ctr.clear();
+  auto pass1 = [&](size_t lo0, size_t hi0) {
+    t->eng[0]->pool->run(hi0 - lo0, [&](size_t lo, size_t hi) {
+      for (size_t i = lo0 + lo; i < lo0 + hi; ++i) {
+        const uint8_t *d = datagram[i];
+        const uint32_t L = len[i];
+        std::memset(&res[i], 0, sizeof res[i]);
+        t->code[i] = -1;
+        if (L == 0) {  // "repeated call": send_queued_packet is the CPU Tunn's business
+          res[i].kind = WG_TUNN_NOT_DATA;
+          continue;
+        }
+        const int pk = parse_kind(d, L);
+        if (pk < 0) { set_err(res[i], -pk); continue; }
+        if (pk == 0) {  // handshake init / response / cookie (mod.rs:150-181)
+          res[i].kind = WG_TUNN_NOT_DATA;
+          continue;
+        }
+        const uint32_t ridx = ld32(d + 4);
+        const Session &s = t->sessions[ridx % WG_N_SESSIONS];
+        int32_t e = WG_STATUS_OK;
+        if (!s.live) e = WG_STATUS_NO_CURRENT_SESSION;                                 // mod.rs:553-556
+        else if ((uint64_t)dst_cap[i] < L - WG_DATA_OFFSET) e = WG_STATUS_DESTINATION_BUFFER_TOO_SMALL;  // session.rs:271
+        else if (ridx != s.receiving_index) e = WG_STATUS_WRONG_INDEX;                // session.rs:275
+        if (e) { set_err(res[i], e); continue; }
+        // until its chunk returns a selected packet reads as failed
+        set_err(res[i], WG_STATUS_CRYPTO_FAILED);
+        t->code[i] = (int32_t)(t->first_slot + 2 * (ridx % WG_N_SESSIONS));
+        t->ctr_all[i] = ld64(d + 8);
       }
-      const int pk = parse_kind(d, L);
-      if (pk < 0) { set_err(res[i], -pk); continue; }
-      if (pk == 0) {  // handshake init / response / cookie (mod.rs:150-181)
-        res[i].kind = WG_TUNN_NOT_DATA;
-        continue;
-      }
-      const uint32_t ridx = ld32(d + 4);
-      const Session &s = t->sessions[ridx % WG_N_SESSIONS];
-      int32_t e = WG_STATUS_OK;
-      if (!s.live) e = WG_STATUS_NO_CURRENT_SESSION;                                 // mod.rs:553-556
-      else if ((uint64_t)dst_cap[i] < L - WG_DATA_OFFSET) e = WG_STATUS_DESTINATION_BUFFER_TOO_SMALL;  // session.rs:271
-      else if (ridx != s.receiving_index) e = WG_STATUS_WRONG_INDEX;                // session.rs:275
-      if (e) { set_err(res[i], e); continue; }
-      // until its chunk returns a selected packet reads as failed
-      set_err(res[i], WG_STATUS_CRYPTO_FAILED);
-      t->code[i] = (int32_t)(t->first_slot + 2 * (ridx % WG_N_SESSIONS));
-      t->ctr_all[i] = ld64(d + 8);
-    }
-  });
-  t->sel.resize(n);
-  t->slot.resize(n);
-  t->ctr.resize(n);
-  const size_t nsel = compact(
-      *t->eng[0]->pool, n, [&](size_t i) { return t->code[i] >= 0; },
-      [&](size_t o, size_t i) {
-        t->sel[o] = (uint32_t)i;
-        t->slot[o] = (uint32_t)t->code[i];
-        t->ctr[o] = t->ctr_all[i];
-      });
-  t->sel.resize(nsel);
-  t->slot.resize(nsel);
-  t->ctr.resize(nsel);
+    });
+    const size_t had = t->sel.size();
+    t->sel.resize(had + (hi0 - lo0));
+    t->slot.resize(t->sel.size());
+    t->ctr.resize(t->sel.size());
+    const size_t got = compact(
+        *t->eng[0]->pool, hi0 - lo0, [&](size_t j) { return t->code[lo0 + j] >= 0; },
+        [&](size_t o, size_t j) {
+          const size_t i = lo0 + j;
+          t->sel[had + o] = (uint32_t)i;
+          t->slot[had + o] = (uint32_t)t->code[i];
+          t->ctr[had + o] = t->ctr_all[i];
+        });
+    t->sel.resize(had + got);
+    t->slot.resize(had + got);
+    t->ctr.resize(had + got);
+  };
+  // a large batch checks its first sixteenth first: a registered DMA batch puts that
+  // part's first chunk on the device while pass 1 covers the rest (open_selected)
+  const size_t n0 = n >= 16384 && dma_runs() && t->eng.size() == 1 ? n / 16 : n;
+  pass1(0, n0);
+  bool grown = n0 == n;
+  auto grow = [&]() {
+    if (grown) return;
+    grown = true;
+    const double a = now_us();
+    pass1(n0, n);
+    t->ph.checks_us += now_us() - a;
+  };
+  if (t->sel.empty()) grow();
   pc.checks_done();
   if (t->sel.empty()) return WG_RC_OK;
   for (int r = 0; r < WG_N_SESSIONS; ++r) t->spec_window[r] = t->sessions[r].window;
@@ -1936,7 +2069,8 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
         if (wg_replay_will_accept(&w, t->ctr[k])) return false;
         (void)wg_replay_mark_did_receive(&w, t->ctr[k]);
         return true;
-      });
+      },
+      grow, !grown, n);
 }
 
 int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
@@ -1989,7 +2123,8 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
         if (r.kind == WG_TUNN_DONE) set_err(r, WG_STATUS_UNEXPECTED_PACKET);  // mod.rs:412
         return rx;
       },
-      [](size_t) { return true; });  // (no replay window: every opened packet lands)
+      [](size_t) { return true; },  // (no replay window: every opened packet lands)
+      [] {}, false, n);
 }
 
 int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out) {

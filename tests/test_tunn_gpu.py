@@ -551,18 +551,20 @@ class SlotArena(Arena):
         self.lens = np.array([len(b) for b in blobs] + [0] * (n - len(blobs)), np.uint32)
 
 
-@pytest.mark.parametrize("dma", ["1", "1-scatter", "1-direct", "1-nested", "0"])
+@pytest.mark.parametrize("dma", ["1", "1-scatter", "1-direct", "1-nested", "1-early", "0"])
 def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
     """Registered packet pools with fixed slots (WG_TUNN_DMA=1: DMA batches -- input runs
     copied to HBM, then the AEAD kernel writes each packet the speculated replay
     decisions land straight into its dst (direct) or into staging with a scatter kernel
     copying it out: "1" the defaults (encapsulate scatter, decapsulate direct),
     "1-scatter" / "1-direct" both operations one way, "1-nested" every stage of a chunk
-    on one stream; 0: the zero-copy direct kernels), several chunks per batch: mostly
-    1350-byte packets in
-    order, with a sprinkle of other lengths (runs break), replays, too-old counters,
-    tampered tags (ring's zeros land in dst), wrong indices and keepalives; one batch
-    with a dst outside the registered pool (that chunk falls back to staging).
+    on one stream, "1-early" a batch large enough (20,000) for decapsulate to put its
+    first chunk on the device before pass 1 has seen the rest; 0: the zero-copy direct
+    kernels), several chunks per batch: mostly 1350-byte packets in order, with a
+    sprinkle of other lengths (runs break), replays, too-old counters, tampered tags
+    (ring's zeros land in dst), wrong indices and keepalives; one batch with a dst
+    outside the registered pool (that batch, or with "1-early" the rest of it after the
+    first sixteenth, falls back to staging).
     Results, dst bytes, windows and stats equal the sequential model's."""
     import ctypes
 
@@ -575,7 +577,7 @@ def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
     monkeypatch.setenv("WG_TUNN_CHUNK_KB", "2048")
     rng = random.Random(55)
     tm, tg, sessions = make_pair(gpu, rng)
-    n, slot = 6000, 1536
+    n, slot = (20000 if dma == "1-early" else 6000), 1536
     srcs = [ipv4(rng, 1350 if rng.random() > 0.02 else rng.choice([64, 1349, 700])) for _ in range(n)]
     a_src, a_dst = SlotArena(srcs, slot), SlotArena([], slot, n)
     for a in (a_src, a_dst):
