@@ -114,12 +114,17 @@ int wg_tunn_set_time(wg_tunn *t, uint64_t now);
  *
  * Data movement.  A batch flows in chunks (WG_TUNN_CHUNK_KB, default 16 MiB) through
  * WG_TUNN_SETS (default 2) staging sets.  Registered buffers (one engine): the inputs
- * go to HBM as 2D copy-engine runs straight from the caller's memory, the AEAD runs
- * in HBM, and a scatter kernel writes every packet's output bytes into the caller's
- * registered destination (decapsulate: on per-chunk speculated replay decisions,
- * repaired after the real in-order pass; WG_TUNN_DMA=0 instead has the AEAD kernels
+ * go to HBM as 2D copy-engine runs straight from the caller's memory (on their own
+ * stream, under the previous chunk's kernel; WG_TUNN_DMA_STREAMS=0: one stream), the
+ * AEAD kernel reads them in HBM and its descriptors / statuses in pinned memory, and
+ * the outputs reach the caller's registered destinations either from the AEAD kernel
+ * itself (decapsulate's default: on per-chunk speculated replay decisions, repaired
+ * after the real in-order pass; needs 16-byte-aligned destinations) or through a
+ * scatter kernel (encapsulate's default); WG_TUNN_DMA_OUT=direct|scatter overrides
+ * both.  A decapsulate batch of 16,384 packets or more starts its first chunk after
+ * pass 1 of its first sixteenth.  WG_TUNN_DMA=0 instead has the AEAD kernels
  * read -- and, for encapsulate with 16-byte-aligned buffers, write -- the caller's
- * registered memory directly over PCIe).  Other buffers: the host copies packets into pinned
+ * registered memory directly over PCIe.  Other buffers: the host copies packets into pinned
  * staging (streaming stores, WG_TUNN_NT=0 for memcpy) on a pool of WG_TUNN_THREADS
  * threads (default: the CPUs this process may use, at most 16), the kernels read and
  * write that staging over PCIe (WG_TUNN_ZEROCOPY=0: explicit copies to and from
