@@ -1803,42 +1803,62 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   PhaseCall pc(t, n);
   Session &s = t->sessions[t->current % WG_N_SESSIONS];  // mod.rs:310
   const uint32_t slot = t->first_slot + 2 * (uint32_t)(t->current % WG_N_SESSIONS) + 1;
-  // pass 1 (stateless checks, on the pool; the counters are reserved below, once)
+  // pass 1 (stateless checks, on the pool; the counters are reserved below) over
+  // packets [lo, hi), appending to the selection
   t->code.resize(n);
+  t->sel.clear();
   const bool live = s.live;
-  t->eng[0]->pool->run(n, [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) {
-      t->code[i] = -1;
-      if ((uint64_t)src_len[i] + WG_DATA_OFFSET > dst_cap[i]) {  // encapsulate: dst[16..len+16]
-        set_err(res[i], WG_STATUS_INVALID_LENGTH);
-        continue;
+  auto pass1 = [&](size_t lo0, size_t hi0) {
+    t->eng[0]->pool->run(hi0 - lo0, [&](size_t lo, size_t hi) {
+      for (size_t i = lo0 + lo; i < lo0 + hi; ++i) {
+        t->code[i] = -1;
+        if ((uint64_t)src_len[i] + WG_DATA_OFFSET > dst_cap[i]) {  // encapsulate: dst[16..len+16]
+          set_err(res[i], WG_STATUS_INVALID_LENGTH);
+          continue;
+        }
+        if (!live) {  // no session: the CPU Tunn queues the packet and starts a handshake
+          std::memset(&res[i], 0, sizeof res[i]);
+          res[i].kind = WG_TUNN_NOT_DATA;
+          res[i].status = WG_STATUS_NO_CURRENT_SESSION;
+        } else if ((uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ > dst_cap[i]) {  // session.rs:210-217
+          set_err(res[i], WG_STATUS_INCORRECT_PACKET_LENGTH);
+        } else {
+          // until its chunk comes back a selected packet reads as failed (a batch that
+          // errors part-way leaves no stale or zeroed results behind)
+          set_err(res[i], WG_STATUS_CRYPTO_FAILED);
+          t->code[i] = 0;
+          continue;
+        }
+        // mod.rs:296-299 copies src into dst[16..] before looking at the session
+        std::memcpy(dst[i] + WG_DATA_OFFSET, src[i], src_len[i]);
       }
-      if (!live) {  // no session: the CPU Tunn queues the packet and starts a handshake
-        std::memset(&res[i], 0, sizeof res[i]);
-        res[i].kind = WG_TUNN_NOT_DATA;
-        res[i].status = WG_STATUS_NO_CURRENT_SESSION;
-      } else if ((uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ > dst_cap[i]) {  // session.rs:210-217
-        set_err(res[i], WG_STATUS_INCORRECT_PACKET_LENGTH);
-      } else {
-        // until its chunk comes back a selected packet reads as failed (a batch that
-        // errors part-way leaves no stale or zeroed results behind)
-        set_err(res[i], WG_STATUS_CRYPTO_FAILED);
-        t->code[i] = 0;
-        continue;
-      }
-      // mod.rs:296-299 copies src into dst[16..] before looking at the session
-      std::memcpy(dst[i] + WG_DATA_OFFSET, src[i], src_len[i]);
-    }
-  });
-  t->sel.resize(n);
-  t->sel.resize(compact(
-      *t->eng[0]->pool, n, [&](size_t i) { return t->code[i] >= 0; },
-      [&](size_t o, size_t i) { t->sel[o] = (uint32_t)i; }));
-  if (t->sel.empty()) return WG_RC_OK;
+    });
+    const size_t had = t->sel.size();
+    t->sel.resize(had + (hi0 - lo0));
+    t->sel.resize(had + compact(
+        *t->eng[0]->pool, hi0 - lo0, [&](size_t j) { return t->code[lo0 + j] >= 0; },
+        [&](size_t o, size_t j) { t->sel[had + o] = (uint32_t)(lo0 + j); }));
+  };
   // one fetch_add per batch (session.rs:219), BEFORE the split: every engine's
-  // packets carry counters ctr0 + k, disjoint across GPUs
+  // packets carry counters ctr0 + k (k: the packet's rank in the selection), disjoint
+  // across GPUs.  A large batch on one engine checks its first sixteenth first, so that
+  // a registered DMA batch puts that part's first chunk on the device while pass 1
+  // covers the rest; the reservation grows with the selection.
   const uint64_t ctr0 = s.sending_counter;
-  s.sending_counter += t->sel.size();
+  const size_t n0 = n >= 16384 && dma_runs() && t->eng.size() == 1 ? n / 16 : n;
+  pass1(0, n0);
+  bool partial = n0 < n;
+  auto grow = [&]() {
+    if (!partial) return;
+    partial = false;
+    const double a = now_us();
+    pass1(n0, n);
+    s.sending_counter = ctr0 + t->sel.size();
+    t->ph.checks_us += now_us() - a;
+  };
+  s.sending_counter = ctr0 + t->sel.size();
+  if (t->sel.empty()) grow();
+  if (t->sel.empty()) return WG_RC_OK;
   pc.checks_done();
   auto size = [&](size_t k) { return round128((uint64_t)src_len[t->sel[k]] + WG_DATA_OVERHEAD_SZ); };
   split(t, size);
@@ -1848,14 +1868,24 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
     // registered src and dst (one engine): the DMA batch -- plaintexts in as runs, the
     // datagrams scattered straight into dst, no host copies and no waits between chunks
     const double t_prep = now_us();
-    if (dma_possible(t, E)) {
-      E.ddst.resize(E.k1 - E.k0);
-      const bool all = all_packets(E, [&](size_t k, size_t &ha, size_t &hb) {
+    auto registered = [&](size_t a, size_t b) {  // srcs and dsts of [a, b)
+      E.ddst.resize(b - E.k0);
+      return all_packets(E, a, b, [&](size_t k, size_t &ha, size_t &hb) {
         const uint32_t i = t->sel[k];
         uint64_t unused;
         return dev_addr(E, src[i], src_len[i], unused, ha) &&
                dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[k - E.k0], hb);
       });
+    };
+    auto grow_all = [&]() {  // the full selection on this (the only) engine
+      if (!partial) return;
+      grow();
+      split(t, size);
+    };
+    int left = 1;  // run_dma's verdict: 1 nothing done, 2 the packets from E.k1 on are left
+    if (!dma_possible(t, E)) grow_all();
+    if (dma_possible(t, E)) {
+      const bool all = registered(E.k0, E.k1);
       if (all) {
         make_chunks(E, size, 0, dma_ramp());
         const bool direct_out = dma_direct_out(true);
@@ -1903,11 +1933,28 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
           E.tx += tx.load();
           E.ph.copy_out_us += now_us() - a;
         };
-        const int r = run_dma(
-            E, true, t_prep, 0, [&](size_t k) { return src[t->sel[k]]; },
-            [&](size_t k) { return src_len[t->sel[k]]; }, fill, done, [] { return 1; });
-        if (r != 1) return r;
+        auto more = [&]() -> int {
+          if (!partial) return 1;
+          const size_t had = t->sel.size();
+          grow();
+          if (t->sel.size() == had) return 1;
+          if (!registered(had, t->sel.size())) return 2;
+          append_chunks(E, size, had, t->sel.size(), chunk_bytes());
+          E.k1 = t->sel.size();
+          return 0;
+        };
+        left = run_dma(
+            E, true, t_prep, n, [&](size_t k) { return src[t->sel[k]]; },
+            [&](size_t k) { return src_len[t->sel[k]]; }, fill, done, more);
+        if (left != 1 && left != 2) return left;
       }
+    }
+    if (left == 2) {  // the rest of the batch takes the paths below
+      grow();
+      E.k0 = E.k1;
+      E.k1 = t->sel.size();
+    } else {
+      grow_all();
     }
     // direct mode (zero-copy, WG_TUNN_DMA=0): src and dst of every packet 16-byte aligned
     // inside memory registered on this engine -> the kernel reads the caller's plaintext and
