@@ -19,10 +19,13 @@
  * the receive buffer overflows, so the sender keeps at most W datagrams in
  * flight (W from the socket's effective SO_RCVBUF).
  *
- *   udp_gateway IN OUT [B] [PAIRS]   -> one JSON line on stdout
+ *   udp_gateway IN OUT [B] [PAIRS] [reg]   -> one JSON line on stdout
  * PAIRS > 1 runs that many independent peers side by side (own Tunns, sockets
  * and threads, one GPU context), the way NepTUN serves peers on its n_threads
- * event loops.
+ * event loops.  "reg": the packet pools (the TUN read buffers the plaintexts land
+ * in, the datagram buffers, the decrypted-packet buffers) are one slab registered
+ * with wg_gpu_register_host, as INTEGRATION.md advises -- the batches then take the
+ * library's DMA path instead of host copies through pinned staging.
  * IN : "NGW1" | u32 n | u32 a_idx | u32 b_idx | k1[32] | k2[32] | n x (u32 len | bytes)
  * OUT: "NGWO" | u32 sent | sent x (u32 len | datagram)
  *             | u32 recv | recv x (u32 len | datagram | wg_tunn_result | u32 dst_len | dst bytes)
@@ -305,6 +308,7 @@ int main(int argc, char **argv) {
    * threads) share the input -- NepTUN's per-peer Mutex<Tunn> + n_threads
    * event loops; the output file is written for pairs == 1 only */
   const uint32_t pairs = argc > 4 && atoi(argv[4]) > 0 ? (uint32_t)atoi(argv[4]) : 1;
+  const int reg = argc > 5 && strcmp(argv[5], "reg") == 0;
   wg_gpu_ctx *ctx = NULL;
   CHECK(wg_gpu_ctx_create(0, 32 * pairs, &ctx));
   const uint32_t n = in.n;
@@ -316,13 +320,23 @@ int main(int argc, char **argv) {
   uint32_t max_len = 0;
   for (uint32_t i = 0; i < n; ++i) max_len = in.len[i] > max_len ? in.len[i] : max_len;
   const uint32_t slot = (max_len + 64 + 63) & ~63u;
-  uint8_t *slabs = malloc((size_t)3 * n * slot + 1);
-  memset(slabs, 0, (size_t)3 * n * slot + 1);
+  /* (4 regions: datagrams sent, datagrams received, decrypted packets, and -- with
+   * "reg" -- the TUN read pool the plaintexts sit in; page-aligned for registration) */
+  const size_t slab_bytes = ((size_t)4 * n * slot + 4095) & ~(size_t)4095;
+  uint8_t *slabs = aligned_alloc(4096, slab_bytes);
+  if (!slabs) return 1;
+  memset(slabs, 0, slab_bytes);
   for (uint32_t i = 0; i < n; ++i) {
     sent[i] = slabs + (size_t)i * slot;
     rx[i] = slabs + ((size_t)n + i) * slot;
     dst[i] = slabs + ((size_t)2 * n + i) * slot;
+    if (reg) {  /* the read pool: each plaintext in its slot, as a TUN read leaves it */
+      uint8_t *b = slabs + ((size_t)3 * n + i) * slot;
+      memcpy(b, in.pkt[i], in.len[i]);
+      in.pkt[i] = b;
+    }
   }
+  if (reg) CHECK(wg_gpu_register_host(ctx, slabs, slab_bytes));
   gw_t *gs = calloc(pairs, sizeof *gs);
   int rcvbuf = 0;
   for (uint32_t p = 0; p < pairs; ++p) {
@@ -402,15 +416,16 @@ int main(int argc, char **argv) {
     fclose(f);
   }
   printf("{\"packets\": %u, \"sent\": %u, \"received\": %u, \"lost\": %u, \"batch\": %u, "
-         "\"pairs\": %u, \"window\": %u, \"rcvbuf\": %d, \"seconds\": %.6f, \"ip_bytes\": %llu, "
+         "\"pairs\": %u, \"registered\": %d, \"window\": %u, \"rcvbuf\": %d, \"seconds\": %.6f, \"ip_bytes\": %llu, "
          "\"socket_to_socket_gbps\": %.3f, \"thread_seconds\": {\"encapsulate\": %.4f, "
          "\"sendmmsg\": %.4f, \"window_wait\": %.4f, \"recvmmsg\": %.4f, \"decapsulate\": %.4f}}\n",
-         n, nsent, nrx, nsent - nrx, batch, pairs, gs[0].window, rcvbuf, secs,
+         n, nsent, nrx, nsent - nrx, batch, pairs, reg, gs[0].window, rcvbuf, secs,
          (unsigned long long)bytes, bytes * 8.0 / secs / 1e9, te, ts, tw, tr, td);
   for (uint32_t p = 0; p < pairs; ++p) {
     wg_tunn_destroy(gs[p].a);
     wg_tunn_destroy(gs[p].b);
   }
+  if (reg) CHECK(wg_gpu_unregister_host(ctx, slabs));
   wg_gpu_ctx_destroy(ctx);
   return 0;
 }

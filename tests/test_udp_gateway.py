@@ -83,7 +83,10 @@ def test_udp_gateway_builds_and_fails_loudly_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-def test_udp_gateway_64k_packets_match_sequential_tunn(tmp_path, torch_cuda):
+@pytest.mark.parametrize("pools", ["plain", "reg"])
+def test_udp_gateway_64k_packets_match_sequential_tunn(tmp_path, torch_cuda, pools):
+    """64 Ki mixed-length packets through the gateway; "reg": its packet pools registered
+    (the library's DMA path where a batch's packets form runs, staging elsewhere)."""
     exe = build(tmp_path)
     rng = random.Random(61)
     a_idx, b_idx = 0x00C0FE01, 0x00BEEF02
@@ -94,8 +97,8 @@ def test_udp_gateway_64k_packets_match_sequential_tunn(tmp_path, torch_cuda):
         pkts[i] = b""  # keepalives
     inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
     write_input(inp, pkts, a_idx, b_idx, k1, k2)
-    r = subprocess.run([exe, str(inp), str(out), "1024"], capture_output=True, text=True,
-                       timeout=300)
+    r = subprocess.run([exe, str(inp), str(out), "1024", "1"] + (["reg"] if pools == "reg" else []),
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     print(summary)

@@ -7,7 +7,8 @@ batch sizes (the reference's default is 50, packet_workers.rs:27).
     python tools/bench_gateway.py [N] [P] [batch ...]   -> JSON lines
 
 GW_PAIRS="1 2 4 8" also sweeps the number of independent peers (Tunn pairs,
-socket pairs and worker threads) sharing the N packets at each batch size.
+socket pairs and worker threads) sharing the N packets at each batch size;
+GW_REG="0 1" also runs each with the packet pools registered (the DMA path).
 """
 import json
 import os
@@ -36,14 +37,14 @@ def main():
         inp = os.path.join(d, "in.bin")
         write_input(inp, [ipv4(rng, P) for _ in range(n)], 11, 22, rng.randbytes(32), rng.randbytes(32))
         pairs = [int(p) for p in os.environ.get("GW_PAIRS", "1").split()]
-        for b in batches:
-            for p in pairs:
-                r = subprocess.run([exe, inp, os.path.join(d, "out.bin"), str(b), str(p)],
-                                   capture_output=True, text=True, timeout=600)
-                line = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {
-                    "error": r.stderr[-300:], "batch": b, "pairs": p}
-                line["packet_bytes"] = P
-                print(json.dumps(line), flush=True)
+        regs = [int(x) for x in os.environ.get("GW_REG", "0").split()]
+        for b, p, reg in ((b, p, reg) for b in batches for p in pairs for reg in regs):
+            r = subprocess.run([exe, inp, os.path.join(d, "out.bin"), str(b), str(p)] + (["reg"] if reg else []),
+                               capture_output=True, text=True, timeout=600)
+            line = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {
+                "error": r.stderr[-300:], "batch": b, "pairs": p, "registered": reg}
+            line["packet_bytes"] = P
+            print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
