@@ -295,7 +295,7 @@ void bind_thread_to_node(int node) {
 // on the workers and the calling thread, and returns when all are done.
 class Pool {
  public:
-  Pool(unsigned workers, int node) {
+  Pool(unsigned workers, int node) : spin_ns_(spin_ns()) {
     for (unsigned i = 0; i < workers; ++i)
       th_.emplace_back([this, i, node] {
         bind_thread_to_node(node);
@@ -306,6 +306,7 @@ class Pool {
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
+      agen_.store(~0ull, std::memory_order_release);
     }
     cv_.notify_all();
     for (auto &t : th_) t.join();
@@ -318,27 +319,56 @@ class Pool {
       if (n) fn(0, n);
       return;
     }
+    bool wake;
     {
       std::lock_guard<std::mutex> lk(mu_);
       fn_ = &fn;
       n_ = n;
       parts_ = parts;
-      pending_ = parts - 1;
+      pending_.store(parts - 1, std::memory_order_relaxed);
       ++gen_;
+      agen_.store(gen_, std::memory_order_release);
+      wake = sleepers_ > 0;
     }
-    cv_.notify_all();
+    if (wake) cv_.notify_all();
     fn(0, n / parts);  // part 0 on the caller
-    std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [this] { return pending_ == 0; });
+    // the other parts: spin briefly (the workers are usually still spinning too), then block
+    const auto t0 = std::chrono::steady_clock::now();
+    while (pending_.load(std::memory_order_acquire) != 0) {
+      if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() >
+          spin_ns_) {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_.load(std::memory_order_acquire) == 0; });
+        break;
+      }
+      _mm_pause();
+    }
+    std::lock_guard<std::mutex> lk(mu_);
     fn_ = nullptr;
   }
 
  private:
+  // Workers spin this long for the next job before they block on the condition variable
+  // (WG_TUNN_SPIN_US, default 20): a batch call runs several pool steps back to back,
+  // and a blocked worker's wake-up costs tens of microseconds on a loaded host.
+  static int64_t spin_ns() {
+    const char *e = std::getenv("WG_TUNN_SPIN_US");
+    return (e ? std::max(0, std::atoi(e)) : 20) * 1000ll;
+  }
   void loop(unsigned id) {
     uint64_t seen = 0;
     for (;;) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (agen_.load(std::memory_order_acquire) == seen &&
+             std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() <
+                 spin_ns_)
+        _mm_pause();
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (!stop_ && gen_ == seen) {
+        ++sleepers_;
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        --sleepers_;
+      }
       if (stop_) return;
       seen = gen_;
       if (id >= parts_) continue;
@@ -346,17 +376,22 @@ class Pool {
       const size_t lo = n_ * id / parts_, hi = n_ * (id + 1) / parts_;
       lk.unlock();
       (*fn)(lo, hi);
-      lk.lock();
-      if (--pending_ == 0) done_.notify_one();
+      if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        lk.lock();  // (the caller may be about to block on done_)
+        done_.notify_one();
+      }
     }
   }
+  const int64_t spin_ns_;
   std::vector<std::thread> th_;
   std::mutex mu_;
   std::condition_variable cv_, done_;
   const std::function<void(size_t, size_t)> *fn_ = nullptr;
   size_t n_ = 0;
-  unsigned parts_ = 0, pending_ = 0;
+  unsigned parts_ = 0, sleepers_ = 0;
+  std::atomic<unsigned> pending_{0};
   uint64_t gen_ = 0;
+  std::atomic<uint64_t> agen_{0};
   bool stop_ = false;
 };
 
