@@ -126,7 +126,8 @@ int wg_tunn_set_time(wg_tunn *t, uint64_t now);
  * read -- and, for encapsulate with 16-byte-aligned buffers, write -- the caller's
  * registered memory directly over PCIe.  Other buffers: the host copies packets into pinned
  * staging (streaming stores, WG_TUNN_NT=0 for memcpy) on a pool of WG_TUNN_THREADS
- * threads (default: the CPUs this process may use, at most 16), the kernels read and
+ * threads (default: the CPUs this process may use, at most 16; they spin
+ * WG_TUNN_SPIN_US, default 20, before blocking between steps), the kernels read and
  * write that staging over PCIe (WG_TUNN_ZEROCOPY=0: explicit copies to and from
  * HBM instead), and the pool copies the results out. */
 /* sending counter of the current session / replay state of a ring slot (for tests) */
