@@ -656,6 +656,7 @@ struct Engine {
   uint8_t *sink = nullptr;
   uint64_t sink_dev = 0;
   size_t sink_cap = 0;
+  std::vector<void *> sink_old;  // outgrown sinks: kernels in flight may still write them
   Staging aux;
 };
 
@@ -1164,9 +1165,9 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
 // form few enough runs.
 // the direct-output sink, at least `bytes` (pinned, device-mapped); false on failure
 bool grow_sink(Engine &E, size_t bytes) {
-  bytes = std::max<size_t>(bytes, 65536);
+  bytes = std::max<size_t>(bytes, 65536);  // (a UDP datagram's plaintext always fits)
   if (bytes <= E.sink_cap) return true;
-  (void)hipHostFree(E.sink);
+  if (E.sink) E.sink_old.push_back(E.sink);  // freed with the engine, after its streams drain
   E.sink = nullptr;
   E.sink_cap = 0;
   void *p = nullptr, *d = nullptr;
@@ -1670,6 +1671,7 @@ void destroy_engine(Engine *E) {
     for (hipStream_t q : E->dq)
       if (q) (void)hipStreamDestroy(q);
     (void)hipHostFree(E->sink);
+    for (void *p : E->sink_old) (void)hipHostFree(p);
     for (hipEvent_t ev : E->ev_in) (void)hipEventDestroy(ev);
     (void)hipHostFree(E->b_desc);
     (void)hipHostFree(E->b_st);
