@@ -118,10 +118,12 @@ int wg_tunn_set_time(wg_tunn *t, uint64_t now);
  * stream, under the previous chunk's kernel; WG_TUNN_DMA_STREAMS=0: one stream), the
  * AEAD kernel reads them in HBM and its descriptors / statuses in pinned memory, and
  * the outputs reach the caller's registered destinations either from the AEAD kernel
- * itself (decapsulate's default: on per-chunk speculated replay decisions, repaired
- * after the real in-order pass; needs 16-byte-aligned destinations) or through a
- * scatter kernel (encapsulate's default); WG_TUNN_DMA_OUT=direct|scatter overrides
- * both.  A decapsulate batch of 16,384 packets or more starts its first chunk after
+ * itself (decapsulate: on per-chunk speculated replay decisions, repaired after the
+ * real in-order pass) or through a scatter kernel: by default the kernel where its
+ * 128-byte output runs sit on whole lines of host memory -- encapsulate's datagram at a
+ * 128-byte boundary, decapsulate's plaintext 16 bytes past one -- and the scatter
+ * elsewhere; WG_TUNN_DMA_OUT=direct|scatter forces either (direct needs 16-byte-aligned
+ * destinations).  A decapsulate batch of 16,384 packets or more starts its first chunk after
  * pass 1 of its first sixteenth.  WG_TUNN_DMA=0 instead has the AEAD kernels
  * read -- and, for encapsulate with 16-byte-aligned buffers, write -- the caller's
  * registered memory directly over PCIe.  Other buffers: the host copies packets into pinned

@@ -80,6 +80,7 @@ struct DeviceGuard {
 // shared with wg_pipe.cpp / wg_tunn.cpp
 int wg_pipe_fail(int rc, const char *what, hipError_t e) { return fail(rc, what, e); }
 int wg_ctx_device(const wg_gpu_ctx *ctx) { return ctx->device; }
+bool wg_ctx_slot_padding(const wg_gpu_ctx *ctx) { return ctx->pad_slots; }
 // snapshot of the registered ranges as (host, bytes, dev) triples, sorted by host
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out) {
   std::lock_guard<std::mutex> lk(ctx->mu);

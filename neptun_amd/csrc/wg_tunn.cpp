@@ -49,6 +49,7 @@
 
 int wg_pipe_fail(int rc, const char *what, hipError_t e);  // wg_gpu.cpp
 int wg_ctx_device(const wg_gpu_ctx *ctx);                   // wg_gpu.cpp
+bool wg_ctx_slot_padding(const wg_gpu_ctx *ctx);            // wg_gpu.cpp
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out);  // wg_gpu.cpp
 
 // ---------------------------------------------------------------------------
@@ -174,31 +175,44 @@ void copy_bytes(uint8_t *dst, const uint8_t *src, size_t n, bool nt) {
 
 // DMA batches' output (WG_TUNN_DMA_OUT, read per call): "direct" -- the AEAD kernel
 // stores each packet's output straight into the caller's registered dst; "scatter" --
-// into HBM staging, then a scatter kernel copies it out.  Default: direct for
-// decapsulate, scatter for encapsulate (the seal kernel's 8-packets-per-store pattern
-// writes host memory slower than the scatter kernel's contiguous per-packet stores,
-// while open's direct stores beat staging + scatter: DESIGN.md section 4)
-bool dma_direct_out(bool seal) {
+// into HBM staging, then a scatter kernel copies it out; unset -- direct for the chunks
+// whose output runs sit on whole 128-byte lines of host memory (seal: the datagram at a
+// line start; open, whose wire grid starts 16 bytes before the plaintext: dst at 16 past
+// a line start), scatter for the others.  The kernels store 128-byte runs of 8 packets
+// per instruction: on whole lines that writes host memory faster than the scatter's
+// contiguous per-packet stores, across line boundaries slower (DESIGN.md section 4,
+// profiles/r04al_align.jsonl).  Returns 0 scatter, 1 direct, 2 auto.
+int dma_out_mode() {
   const char *e = std::getenv("WG_TUNN_DMA_OUT");
-  if (e && std::strcmp(e, "scatter") == 0) return false;
-  if (e && std::strcmp(e, "direct") == 0) return true;
-  return !seal;
+  if (e && std::strcmp(e, "scatter") == 0) return 0;
+  if (e && std::strcmp(e, "direct") == 0) return 1;
+  return 2;
 }
 
 // The chunk's output base for direct output: the lowest of the n device addresses
 // addr(j) (each with its extent ext(j)), or 0 when direct output cannot take the chunk
-// -- an address not 16-byte aligned (the descriptor kernels' alignment rule) or a span
-// the kernels' per-packet offsets cannot hold (2^43 bytes, 16-byte units in 40 bits)
+// -- an address not 16-byte aligned (the descriptor kernels' alignment rule), with
+// line >= 0 one not `line` bytes past a 128-byte line (auto mode), or a span the
+// kernels' per-packet offsets cannot hold (2^43 bytes, 16-byte units in 40 bits)
 template <class Addr, class Ext>
-uint64_t direct_base(size_t n, Addr addr, Ext ext) {
+uint64_t direct_base(size_t n, Addr addr, Ext ext, int line = -1) {
   uint64_t lo = ~0ull, hi = 0;
   for (size_t j = 0; j < n; ++j) {
     const uint64_t a = addr(j);
     if (a & 15u) return 0;
+    if (line >= 0 && (a & 127u) != (uint64_t)line) return 0;
     lo = std::min(lo, a);
     hi = std::max(hi, a + ext(j));
   }
   return n && hi - lo < (1ull << 43) ? lo : 0;
+}
+
+// Uniform decapsulate chunks through the strided text-grid open (WG_TUNN_STRIDED=1; off:
+// into line-aligned slots it wrote host memory slower than the descriptor kernels +
+// scatter, 255-261 vs 267-273 Gbit/s, profiles/r04st_*), read per call
+bool dma_strided() {
+  const char *e = std::getenv("WG_TUNN_STRIDED");
+  return e && std::atoi(e) != 0;
 }
 
 // Direct-output DMA batches on a copy stream and a kernel stream (WG_TUNN_DMA_STREAMS=0:
@@ -653,6 +667,14 @@ struct Engine {
   // per chunk 1 = direct, 0 = staged + scatter; and a pinned sink for the plaintext of
   // packets whose speculated decision keeps them out of dst (never read back)
   std::vector<uint8_t> chunk_direct;
+  // decapsulate chunks of one length, one key slot and constant dst strides whose
+  // packets all land: opened by the strided kernel (text grid on line-aligned plaintext
+  // slots) straight into dst -- len == 0: not such a chunk
+  struct StridedOpen {
+    uint32_t len = 0, slot = 0;
+    uint64_t dst = 0, dst_stride = 0;
+  };
+  std::vector<StridedOpen> chunk_strided;
   uint8_t *sink = nullptr;
   uint64_t sink_dev = 0;
   size_t sink_cap = 0;
@@ -1206,9 +1228,11 @@ hipError_t reserve_batch(Engine &E, size_t n) {
 // does not qualify, nothing done) or 2 (the chunks [0, E.chunks.size()) are done and
 // the selected packets from E.k1 on are left for the caller).  n_cap bounds the
 // packets of the whole batch (the batch arrays are sized for it up front).
-template <class InHost, class InLen, class Fill, class Done, class More>
+// launch(c, S, stream) may run chunk c's AEAD itself: it returns -1 when it does not
+// (the descriptor kernels then run), else the launch's rc.
+template <class InHost, class InLen, class Fill, class Done, class More, class Launch>
 int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, InLen in_len, Fill fill, Done done,
-            More more) {
+            More more, Launch launch) {
   // (seal: the plaintext goes 16 bytes into its staging slot, NepTUN's layout; open: the datagram at 0)
   const uint64_t in_shift = seal ? WG_DATA_OFFSET : 0u;
   const size_t nc0 = E.chunks.size(), n = E.k1 - E.k0;
@@ -1287,8 +1311,10 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
     // batch arrays itself: no small copies, which the copy engine would take in
     // submission order -- chunk c + 1's descriptors behind chunk c's statuses, i.e.
     // behind chunk c's kernel
-    const int rc = seal ? wg_gpu_seal_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk)
-                        : wg_gpu_open_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk);
+    int rc = launch(c, S, qk);
+    if (rc < 0)
+      rc = seal ? wg_gpu_seal_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk)
+                : wg_gpu_open_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk);
     if (rc) return rc;
     if (scatter) {
       hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((m + 3) / 4)), dim3(256), 0, qk, E.b_jobs + j0,
@@ -1479,8 +1505,10 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     }
     make_chunks(E, size, 0, dma_ramp());
     int err = WG_RC_OK;  // a chunk's results could not be taken (reported after the batch)
-    const bool direct_out = dma_direct_out(false);
+    const int out_mode = dma_out_mode();
+    const bool strided_ok = out_mode == 2 && !wg_ctx_slot_padding(E.ctx) && dma_strided();
     E.chunk_direct.assign(E.chunks.size(), 0);
+    E.chunk_strided.assign(E.chunks.size(), Engine::StridedOpen{});
     auto fill = [&](const Chunk &ch, size_t j0, uint8_t *d_out) -> uint8_t * {
       const double a = now_us();
       const size_t m = ch.k1 - ch.k0;
@@ -1493,11 +1521,30 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       // direct output: the open kernel writes the plaintext of every packet the
       // speculation lands straight into its dst (the tag follows from the host, in
       // copy_out), and that of the others into the pinned sink
+      const size_t c = &ch - E.chunks.data();
+      // a chunk the strided text-grid open takes: every packet lands, one length and one
+      // key slot, plaintext slots at a constant stride on whole 128-byte lines
+      if (strided_ok && pmax == 0 && m >= 64) {
+        const uint32_t L = len[t->sel[ch.k0]], sl = t->slot[ch.k0];
+        const uint64_t d0 = E.ddst[j0], ds = m > 1 ? E.ddst[j0 + 1] - d0 : 0;
+        bool uni = L >= WG_DATA_OVERHEAD_SZ && d0 % 128 == 0 && ds % 128 == 0 && ds >= L - WG_DATA_OVERHEAD_SZ &&
+                   ds < (1ull << 25) && 63 * ds + L + 64 < (1ull << 31);
+        for (size_t kk = 0; uni && kk < m; ++kk) {
+          const size_t k = ch.k0 + kk;
+          uni = t->spec[k] && len[t->sel[k]] == L && t->slot[k] == sl && E.ddst[j0 + kk] == d0 + kk * ds;
+        }
+        if (uni) {
+          E.chunk_strided[c] = Engine::StridedOpen{L, sl, d0, ds};
+          E.chunk_direct[c] = 1;
+          return reinterpret_cast<uint8_t *>(d0);  // (not d_out: no scatter)
+        }
+      }
       uint64_t base = 0;
-      if (direct_out && (pmax <= E.sink_cap || grow_sink(E, pmax))) {
-        auto addr = [&](size_t kk) { return t->spec[ch.k0 + kk] ? E.ddst[j0 + kk] : E.sink_dev; };
+      // (the sink target sits 16 bytes past a line, like the dsts auto mode takes)
+      if (out_mode != 0 && (pmax + 16 <= E.sink_cap || grow_sink(E, pmax + 16))) {
+        auto addr = [&](size_t kk) { return t->spec[ch.k0 + kk] ? E.ddst[j0 + kk] : E.sink_dev + 16; };
         auto ext = [&](size_t kk) { return (uint64_t)len[t->sel[ch.k0 + kk]] - WG_DATA_OVERHEAD_SZ; };
-        base = direct_base(m, addr, ext);
+        base = direct_base(m, addr, ext, out_mode == 2 ? 16 : -1);
       }
       E.chunk_direct[&ch - E.chunks.data()] = base != 0;
       E.pool->run(m, [&](size_t lo, size_t hi) {
@@ -1506,7 +1553,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
           const uint32_t i = t->sel[k];
           const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ, o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
           if (base) {
-            E.b_desc[j] = wg_packet_desc{E.off[j], (t->spec[k] ? E.ddst[j] : E.sink_dev) - base, 0, len[i],
+            E.b_desc[j] = wg_packet_desc{E.off[j], (t->spec[k] ? E.ddst[j] : E.sink_dev + 16) - base, 0, len[i],
                                          t->slot[k]};
           } else {
             E.b_desc[j] = wg_packet_desc{E.off[j], o, 0, len[i], t->slot[k]};
@@ -1577,11 +1624,20 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       append_chunks(E, size, had, t->sel.size(), chunk_bytes());
       E.k1 = t->sel.size();
       E.chunk_direct.resize(E.chunks.size(), 0);
+      E.chunk_strided.resize(E.chunks.size(), Engine::StridedOpen{});
       return 0;
+    };
+    auto launch = [&](size_t c, Staging &S, hipStream_t q) -> int {
+      if (c >= E.chunk_strided.size() || !E.chunk_strided[c].len) return -1;
+      const Chunk &ch = E.chunks[c];
+      const Engine::StridedOpen &so = E.chunk_strided[c];
+      // (staging offsets: one length, so packet kk sits at kk * round128(len))
+      return wg_gpu_open_strided(E.ctx, (uint32_t)(ch.k1 - ch.k0), so.len, so.slot, S.d_in, round128(so.len),
+                                 reinterpret_cast<uint8_t *>(so.dst), so.dst_stride, E.b_st + (ch.k0 - E.k0), q);
     };
     const int r = run_dma(
         E, false, t_prep, n_cap, [&](size_t k) { return datagram[t->sel[k]]; },
-        [&](size_t k) { return len[t->sel[k]]; }, fill, done, more);
+        [&](size_t k) { return len[t->sel[k]]; }, fill, done, more, launch);
     if (r == 1 && partial) {  // (nothing was done)
       grow_all();
       split(t, size);
@@ -1925,16 +1981,17 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
       const bool all = registered(E.k0, E.k1);
       if (all) {
         make_chunks(E, size, 0, dma_ramp());
-        const bool direct_out = dma_direct_out(true);
+        const int out_mode = dma_out_mode();
         auto fill = [&](const Chunk &ch, size_t j0, uint8_t *d_out) -> uint8_t * {
           const size_t m = ch.k1 - ch.k0;
           // direct output: the seal kernel writes each datagram into the caller's dst
-          const uint64_t base = direct_out ? direct_base(
-                                                 m, [&](size_t kk) { return E.ddst[j0 + kk]; },
-                                                 [&](size_t kk) {
-                                                   return (uint64_t)src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
-                                                 })
-                                           : 0;
+          const uint64_t base = out_mode != 0 ? direct_base(
+                                                    m, [&](size_t kk) { return E.ddst[j0 + kk]; },
+                                                    [&](size_t kk) {
+                                                      return (uint64_t)src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
+                                                    },
+                                                    out_mode == 2 ? 0 : -1)
+                                              : 0;
           E.pool->run(m, [&](size_t lo, size_t hi) {
             for (size_t kk = lo; kk < hi; ++kk) {
               const size_t k = ch.k0 + kk, j = j0 + kk;
@@ -1982,7 +2039,8 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
         };
         left = run_dma(
             E, true, t_prep, n, [&](size_t k) { return src[t->sel[k]]; },
-            [&](size_t k) { return src_len[t->sel[k]]; }, fill, done, more);
+            [&](size_t k) { return src_len[t->sel[k]]; }, fill, done, more,
+            [](size_t, Staging &, hipStream_t) { return -1; });
         if (left != 1 && left != 2) return left;
       }
     }

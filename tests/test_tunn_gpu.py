@@ -646,3 +646,42 @@ def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
     for a in (a_src, a_dst):
         gpu.unregister_host(a.window()[0])
     tg.close()
+
+
+@pytest.mark.parametrize("strided", ["1", "0"])
+def test_registered_uniform_pools_take_the_strided_open(gpu, monkeypatch, strided):
+    """Decapsulate chunks whose packets all land, share one length and sit in line-aligned
+    registered slots go through the strided text-grid open straight into dst (the host
+    adds the tag bytes); tampered tags keep a chunk on that path (ring's zeros land),
+    replays send their chunk to the descriptor kernels.  WG_TUNN_STRIDED=0: every chunk
+    on the descriptor kernels.  Results, dst bytes and stats equal the sequential model's."""
+    import numpy as np
+    monkeypatch.setenv("WG_TUNN_STRIDED", strided)
+    monkeypatch.setenv("WG_TUNN_CHUNK_KB", "2048")
+    rng = random.Random(77)
+    tm, tg, sessions = make_pair(gpu, rng)
+    local, peer, rk, sk = sessions[0]
+    n, slot = 9000, 1536
+    dgs = []
+    for c in range(n):
+        d = bytearray(o.format_packet_data(rk, local, c, ipv4(rng, 1350)))
+        if rng.random() < 0.01:
+            d[rng.randrange(16, len(d))] ^= 0x10  # tampered: still lands (zeros)
+        dgs.append(bytes(d))
+    for at in range(5000, n, 997):  # replays in the second half: those chunks go descriptor
+        dgs[at] = dgs[at - 3]
+    a_in, a_out = SlotArena(dgs, slot), SlotArena([], slot, n)
+    assert int(a_out.ptrs[0]) % 128 == 0
+    for a in (a_in, a_out):
+        gpu.register_host(*a.window())
+    caps = np.full(n, slot, np.uint32)
+    dm = [bytearray(b"\xee" * slot) for _ in range(n)]
+    res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+    res_g = tg.decapsulate_ptrs(a_in.ptrs, a_in.lens, a_out.ptrs, caps)
+    check_same(res_g, res_m, [bytearray(a_out.get(k, slot)) for k in range(n)], dm, f"strided {strided}")
+    kinds = [r[:2] for r in res_m]
+    assert (M.ERR, M.INVALID_AEAD_TAG) in kinds and (M.ERR, M.DUPLICATE_COUNTER) in kinds
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    for a in (a_in, a_out):
+        gpu.unregister_host(a.window()[0])
+    tg.close()

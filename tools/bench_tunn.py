@@ -42,6 +42,9 @@ def main():
                     help="register the packet buffers (direct, copy-free batches)")
     ap.add_argument("--phase-timing", action="store_true",
                     help="also time the device stages with events (wg_tunn_set_phase_timing)")
+    ap.add_argument("--align", type=int, default=-1,
+                    help="place every buffer's slot 0 this many bytes past a 4096-byte boundary "
+                         "(-1: wherever numpy's allocation lands)")
     a = ap.parse_args()
     P = a.P
     ctx = neptun_amd.GpuContext(0, key_slots=64)
@@ -53,13 +56,20 @@ def main():
     tb.install_session(34, 21, k1, k2, True)
     for n in [int(x) for x in a.sizes.split(",")]:
         S = (P + 32 + 63) // 64 * 64
-        src = rng.integers(0, 256, n * S, np.uint8)
+        def place(arr):  # a view of n * S bytes at the requested alignment
+            if a.align < 0:
+                return arr[:n * S]
+            skip = (a.align - arr.ctypes.data) % 4096
+            return arr[skip:skip + n * S]
+        extra = 8192 if a.align >= 0 else 0
+        src_all = rng.integers(0, 256, n * S + extra, np.uint8)
+        src = place(src_all)
         v = src.reshape(n, S)
         v[:, 0] = 0x45
         v[:, 2] = P >> 8
         v[:, 3] = P & 255
-        wire = np.zeros(n * S, np.uint8)
-        back = np.zeros(n * S, np.uint8)
+        wire_all, back_all = np.zeros(n * S + extra, np.uint8), np.zeros(n * S + extra, np.uint8)
+        wire, back = place(wire_all), place(back_all)
         offs = np.arange(n, dtype=np.uint64) * S
         src_p = (src.ctypes.data + offs).astype(np.uint64)
         wire_p = (wire.ctypes.data + offs).astype(np.uint64)
@@ -68,7 +78,7 @@ def main():
         wlens = np.full(n, P + 32, np.uint32)
         caps = np.full(n, S, np.uint32)
         if a.register:
-            for arr in (src, wire, back):
+            for arr in (src_all, wire_all, back_all):
                 ctx.register_host(arr.ctypes.data, arr.nbytes)
         res = (TunnResult * n)()
         vp = ctypes.c_void_p
@@ -97,7 +107,7 @@ def main():
         ok = bool(np.array_equal(back.reshape(n, S)[:, :P], v[:, :P]))
         ph_e, ph_d = ta.phases(reset=True), tb.phases(reset=True)
         if a.register:
-            for arr in (src, wire, back):
+            for arr in (src_all, wire_all, back_all):
                 ctx.unregister_host(arr.ctypes.data)
         e, d = statistics.median(te), statistics.median(td)
         print(json.dumps({"packets": n, "P": P, "registered": a.register, "verified": ok,
@@ -107,6 +117,7 @@ def main():
                           "roundtrip_gbps": round(n * P * 8 / (e + d) / 1e9, 1),
                           "mpps_roundtrip": round(n / (e + d) / 1e6, 3),
                           "env": {k: v for k, v in os.environ.items() if k.startswith("WG_TUNN_")},
+                          "align": a.align if a.align >= 0 else int(wire.ctypes.data % 4096),
                           "phases_encap_per_call_us": per_call(ph_e),
                           "phases_decap_per_call_us": per_call(ph_d)}), flush=True)
     ta.close()
