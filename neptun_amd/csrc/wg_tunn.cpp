@@ -215,8 +215,15 @@ bool dma_strided() {
   return e && std::atoi(e) != 0;
 }
 
-// Direct-output DMA batches on a copy stream and a kernel stream (WG_TUNN_DMA_STREAMS=0:
-// every stage of a chunk on its staging set's stream), read per call
+// the DMA batches' scatter grid cap (WG_TUNN_SCATTER_BLOCKS, default 0: one block per 4
+// jobs), read per call
+uint32_t scatter_blocks() {
+  const char *e = std::getenv("WG_TUNN_SCATTER_BLOCKS");
+  return e ? (uint32_t)std::max(0, std::atoi(e)) : 0u;
+}
+
+// DMA batches on a copy, a kernel and an output stream (WG_TUNN_DMA_STREAMS=0: every
+// stage of a chunk on its staging set's stream), read per call
 bool dma_streams() {
   const char *e = std::getenv("WG_TUNN_DMA_STREAMS");
   return !e || std::atoi(e) != 0;
@@ -478,30 +485,33 @@ struct Scatter {
 __global__ __launch_bounds__(256) void scatter_kernel(const Scatter *__restrict__ jobs, uint32_t m,
                                                       const uint8_t *__restrict__ a_base,
                                                       const uint8_t *__restrict__ b_base) {
-  const uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
-  if (j >= m) return;
-  const Scatter sc = jobs[j];
-  uint8_t *dst = reinterpret_cast<uint8_t *>(sc.dst);
-  const uint8_t *a = a_base + sc.a_off, *b = b_base + sc.b_off;
-  const uint32_t L = sc.a_len + sc.b_len;
-  const bool aligned = (sc.dst & 15u) == 0 && (reinterpret_cast<uintptr_t>(a) & 15u) == 0;
-  for (uint32_t o = 16u * lane; o < L; o += 1024u) {
-    if (aligned && o + 16u <= sc.a_len) {  // a whole piece of segment a
-      *reinterpret_cast<uint4 *>(dst + o) = *reinterpret_cast<const uint4 *>(a + o);
-      continue;
-    }
-    uint8_t v[16];
+  // one wave per job, the grid striding over the jobs: the launch may be capped so that
+  // the next chunk's AEAD kernel finds free CUs beside it (run_dma)
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t j = blockIdx.x * 4u + (threadIdx.x >> 6); j < m; j += gridDim.x * 4u) {
+    const Scatter sc = jobs[j];
+    uint8_t *dst = reinterpret_cast<uint8_t *>(sc.dst);
+    const uint8_t *a = a_base + sc.a_off, *b = b_base + sc.b_off;
+    const uint32_t L = sc.a_len + sc.b_len;
+    const bool aligned = (sc.dst & 15u) == 0 && (reinterpret_cast<uintptr_t>(a) & 15u) == 0;
+    for (uint32_t o = 16u * lane; o < L; o += 1024u) {
+      if (aligned && o + 16u <= sc.a_len) {  // a whole piece of segment a
+        *reinterpret_cast<uint4 *>(dst + o) = *reinterpret_cast<const uint4 *>(a + o);
+        continue;
+      }
+      uint8_t v[16];
 #pragma unroll
-    for (uint32_t q = 0; q < 16u; ++q) {
-      const uint32_t x = o + q;
-      v[q] = x < sc.a_len ? a[x] : (x < L ? b[x - sc.a_len] : 0u);
-    }
-    if ((sc.dst & 15u) == 0 && o + 16u <= L) {
-      uint4 w;
-      __builtin_memcpy(&w, v, 16);
-      *reinterpret_cast<uint4 *>(dst + o) = w;
-    } else {
-      for (uint32_t q = 0; q < 16u && o + q < L; ++q) dst[o + q] = v[q];
+      for (uint32_t q = 0; q < 16u; ++q) {
+        const uint32_t x = o + q;
+        v[q] = x < sc.a_len ? a[x] : (x < L ? b[x - sc.a_len] : 0u);
+      }
+      if ((sc.dst & 15u) == 0 && o + 16u <= L) {
+        uint4 w;
+        __builtin_memcpy(&w, v, 16);
+        *reinterpret_cast<uint4 *>(dst + o) = w;
+      } else {
+        for (uint32_t q = 0; q < 16u && o + q < L; ++q) dst[o + q] = v[q];
+      }
     }
   }
 }
@@ -661,8 +671,8 @@ struct Engine {
   // DMA batches' copy and kernel streams (direct output): the input copies of chunk
   // c + 1 run under chunk c's kernel; per-chunk events order a chunk's stages and a
   // staging set's reuse
-  hipStream_t dq[2] = {nullptr, nullptr};
-  std::vector<hipEvent_t> ev_in;
+  hipStream_t dq[3] = {nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> ev_in, ev_k;
   // direct-output chunks (the AEAD kernel writes the caller's registered dst itself):
   // per chunk 1 = direct, 0 = staged + scatter; and a pinned sink for the plaintext of
   // packets whose speculated decision keeps them out of dst (never read back)
@@ -1264,11 +1274,13 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
   if (!build_runs(0, nc0)) return 1;
   PipelineDrain drain_guard(E);
   const bool split_streams = dma_streams();
+  const uint32_t scatter_cap = scatter_blocks();
+  const bool split_scatter = std::getenv("WG_TUNN_SPLIT_SCATTER") != nullptr;  // (A/B only)
   const size_t sets = pipeline_sets();
   TUNN_HIP(reserve_batch(E, std::max(n, n_cap)), "tunn: batch arrays");
   for (size_t q = 0; q < sets; ++q) TUNN_HIP(reserve(E.st[q], max_bytes + 128, max_m), "tunn: staging");
   auto events = [&](size_t count) -> hipError_t {
-    for (auto *v : {&E.cev, &E.ev_in})
+    for (auto *v : {&E.cev, &E.ev_in, &E.ev_k})
       while (v->size() < count) {
         hipEvent_t ev;
         if (const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming); e != hipSuccess) return e;
@@ -1294,13 +1306,14 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
     const double pb = now_us();
     E.ph.pack_us += pb - pa;
     // Direct output: the input copies on the copy stream, the kernel on the kernel
-    // stream, so that chunk c + 1's copies run under chunk c's kernel (the two move
-    // data in opposite directions).  Staged output: input copies, kernel and scatter
-    // on the set's stream (the scatter and the next chunk's kernel on different
-    // streams could share a hardware queue and serialise anyway).  Either way a set's
-    // reuse by chunk c waits for chunk c - sets.
-    const bool split = split_streams && !scatter;
-    hipStream_t qi = split ? E.dq[0] : S.stream, qk = split ? E.dq[1] : S.stream;
+    // stream, so that chunk c + 1's copies run under chunk c's kernel (the two move data
+    // in opposite directions).  Staged output: copies, kernel and scatter on the set's
+    // stream -- splitting those too (the scatter on a third stream beside the next
+    // chunk's kernel, its grid capped by WG_TUNN_SCATTER_BLOCKS) measured 3-15 % slower
+    // (profiles/r04sc_scatter.jsonl).  WG_TUNN_DMA_STREAMS=0: every stage on the set's
+    // stream.  Either way a set's reuse by chunk c waits for chunk c - sets.
+    const bool split = split_streams && (!scatter || split_scatter);
+    hipStream_t qi = split ? E.dq[0] : S.stream, qk = split ? E.dq[1] : S.stream, qo = split ? E.dq[2] : S.stream;
     if (c >= sets) TUNN_HIP(hipStreamWaitEvent(qi, E.cev[c - sets], 0), "tunn: set reuse");
     TUNN_HIP(copy_runs(E.chunk_runs[c], S.d_in, true, qi), "tunn: input runs");
     if (split) {
@@ -1317,11 +1330,16 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
                 : wg_gpu_open_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk);
     if (rc) return rc;
     if (scatter) {
-      hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((m + 3) / 4)), dim3(256), 0, qk, E.b_jobs + j0,
-                         (uint32_t)m, (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
+      if (split) {
+        TUNN_HIP(hipEventRecord(E.ev_k[c], qk), "tunn: event");
+        TUNN_HIP(hipStreamWaitEvent(qo, E.ev_k[c], 0), "tunn: event wait");
+      }
+      const uint32_t blocks = (uint32_t)((m + 3) / 4);
+      hipLaunchKernelGGL(scatter_kernel, dim3(scatter_cap ? std::min(blocks, scatter_cap) : blocks), dim3(256), 0,
+                         qo, E.b_jobs + j0, (uint32_t)m, (const uint8_t *)S.d_out, (const uint8_t *)S.d_in);
       TUNN_HIP(hipGetLastError(), "tunn: scatter launch");
     }
-    TUNN_HIP(hipEventRecord(E.cev[c], qk), "tunn: event");
+    TUNN_HIP(hipEventRecord(E.cev[c], scatter ? qo : qk), "tunn: event");
     S.busy = true;
     E.ph.submit_us += now_us() - pb;
     if (const int rc2 = injected_failure(c)) return rc2;
@@ -1729,6 +1747,7 @@ void destroy_engine(Engine *E) {
     (void)hipHostFree(E->sink);
     for (void *p : E->sink_old) (void)hipHostFree(p);
     for (hipEvent_t ev : E->ev_in) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : E->ev_k) (void)hipEventDestroy(ev);
     (void)hipHostFree(E->b_desc);
     (void)hipHostFree(E->b_st);
     (void)hipHostFree(E->b_jobs);
