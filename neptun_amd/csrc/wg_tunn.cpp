@@ -1276,9 +1276,14 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
   const bool split_streams = dma_streams();
   const uint32_t scatter_cap = scatter_blocks();
   const bool split_scatter = std::getenv("WG_TUNN_SPLIT_SCATTER") != nullptr;  // (A/B only)
-  const size_t sets = pipeline_sets();
+  // Staging sets (WG_TUNN_SETS overrides): decided by chunk 0's output form -- all kSets
+  // when it takes the scatter, whose copy, kernel and scatter then overlap the neighbours'
+  // (decapsulate into line-aligned slots 263-269 Gbit/s with 2 sets, 278-285 with 4),
+  // 2 for direct output, which 4 sets slowed (profiles/r04se_sets.jsonl, r04f8_*).
+  size_t sets = std::getenv("WG_TUNN_SETS") ? pipeline_sets() : 0;
   TUNN_HIP(reserve_batch(E, std::max(n, n_cap)), "tunn: batch arrays");
-  for (size_t q = 0; q < sets; ++q) TUNN_HIP(reserve(E.st[q], max_bytes + 128, max_m), "tunn: staging");
+  // (each set reserved at its first use in the batch: no chunk of this batch holds it yet)
+  TUNN_HIP(reserve(E.st[0], max_bytes + 128, max_m), "tunn: staging");
   auto events = [&](size_t count) -> hipError_t {
     for (auto *v : {&E.cev, &E.ev_in, &E.ev_k})
       while (v->size() < count) {
@@ -1299,10 +1304,12 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
   for (size_t c = 0; c < E.chunks.size(); ++c) {
     const Chunk &ch = E.chunks[c];
     const size_t m = ch.k1 - ch.k0, j0 = ch.k0 - E.k0;
-    Staging &S = E.st[c % sets];
+    if (c > 0 && c < sets) TUNN_HIP(reserve(E.st[c], max_bytes + 128, max_m), "tunn: staging");
+    Staging &S = E.st[sets ? c % sets : 0];
     const double pa = now_us();
     uint8_t *const out_base = fill(ch, j0, S.d_out);
     const bool scatter = out_base == S.d_out;
+    if (!sets) sets = scatter ? kSets : 2;  // (chunk 0)
     const double pb = now_us();
     E.ph.pack_us += pb - pa;
     // Direct output: the input copies on the copy stream, the kernel on the kernel
