@@ -113,7 +113,8 @@ int wg_tunn_set_time(wg_tunn *t, uint64_t now);
  * see "Data movement" below.  Results are identical either way.
  *
  * Data movement.  A batch flows in chunks (WG_TUNN_CHUNK_KB, default 16 MiB) through
- * WG_TUNN_SETS (default 2) staging sets.  Registered buffers (one engine): the inputs
+ * WG_TUNN_SETS staging sets (default 2; a registered batch whose first chunk takes the
+ * scatter below uses 4).  Registered buffers (one engine): the inputs
  * go to HBM as 2D copy-engine runs straight from the caller's memory (on their own
  * stream, under the previous chunk's kernel; WG_TUNN_DMA_STREAMS=0: one stream), the
  * AEAD kernel reads them in HBM and its descriptors / statuses in pinned memory, and
