@@ -6,8 +6,8 @@ Each round draws a batch size (1 .. 40,000, skewed small; the early start takes 
 a slot size, an output mode (WG_TUNN_DMA_OUT direct / scatter / default), chunk size and
 stream form, encapsulates a batch of mostly-1350-byte packets from registered slots and
 decapsulates the peer's traffic with replays, too-old counters, tampered tags, forged-
-then-real counters, wrong indices and keepalives -- sometimes with destination slots
-shifted off 16-byte alignment (direct output falls back to the scatter) or one dst
+then-real counters, wrong indices and keepalives -- with destination slots on 128-byte
+lines, 16 bytes past one, or 8 bytes off 16-byte alignment (each output mode's case) or one dst
 outside the registered pool (the rest of the batch takes the staged path).  Results,
 every dst byte, replay windows and byte counters must equal the model's.
 
@@ -43,7 +43,9 @@ def main():
     while time.time() < t_end:
         n = rng.choice([1, 7, 64, 500, 3000, 12000, 17000, 26000, 40000])
         slot = rng.choice([1408, 1536, 2048])
-        shift = rng.choice([0, 0, 0, 8])  # dst slots 8 bytes off 16-byte alignment
+        # dst slots on 128-byte lines (0), 16 past one (16), or 8 off 16-byte alignment (8):
+        # the output modes' alignment cases (direct where the runs sit on lines)
+        shift = rng.choice([0, 0, 16, 8])
         env = {"WG_TUNN_DMA_OUT": rng.choice(["direct", "scatter", ""]),
                "WG_TUNN_CHUNK_KB": rng.choice(["", "2048", "8192", "65536"]),
                "WG_TUNN_DMA_STREAMS": rng.choice(["", "0"]),
@@ -62,7 +64,7 @@ def main():
             t.install_session(local, peer, rk, sk, True)
         # outbound
         srcs = [ipv4(rng, 1350 if rng.random() > 0.02 else rng.choice([64, 1349, 700])) for _ in range(n)]
-        a_src, a_dst = SlotArena(srcs, slot), SlotArena([], slot + 16, n)
+        a_src, a_dst = SlotArena(srcs, slot), SlotArena([], slot + 128, n)
         dptrs = a_dst.ptrs + np.uint64(shift)
         for a in (a_src, a_dst):
             gpu.register_host(*a.window())
@@ -93,7 +95,7 @@ def main():
             forged = bytearray(dgs[at + 7])
             forged[-1] ^= 0x80
             dgs[at] = bytes(forged)
-        a_in, a_out = SlotArena(dgs, slot), SlotArena([], slot + 16, n)
+        a_in, a_out = SlotArena(dgs, slot), SlotArena([], slot + 128, n)
         optrs = a_out.ptrs + np.uint64(shift)
         stray = ctypes.create_string_buffer(b"\xee" * slot, slot)
         if stray_at >= 0:
