@@ -73,7 +73,38 @@ typedef struct wg_tunn_result {
 
 typedef struct wg_tunn wg_tunn;
 
-/* A Tunn bound to a GPU context; it uses key slots [first_slot, first_slot + 16). */
+/* Engine: the device side the Tunns of one GPU share -- the host copy pool, the
+ * HIP streams and the pinned / device staging their batches run on.  NepTUN
+ * keeps one Tunn per peer (device/peer.rs:29, Mutex<Tunn>) and its PacketWorkers
+ * serve all peers from one set of worker threads (device/packet_workers.rs:99-287);
+ * so here any number of Tunns attach to one engine without adding a thread or a
+ * stream.  A batch call borrows one of the engine's lanes (a staging pipeline:
+ * streams + staging sets; created on first need, at most WG_ENGINE_LANES,
+ * default 8) for its duration; calls on different Tunns run concurrently up to
+ * that many, then wait for a lane.  The pool's threads (WG_TUNN_THREADS, default
+ * the CPUs this process may use, at most 16) are the engine's, shared by its
+ * lanes: a call that finds the pool busy runs its host steps on its own thread.
+ *   wg_engine_create / wg_engine_destroy: an engine on ctx (destroy fails while
+ *     Tunns are attached);
+ *   wg_tunn_create_on: a Tunn attached to engine e.
+ * wg_tunn_create(ctx, ...) attaches to the context's default engine (made with
+ * the context's first such Tunn, destroyed with its last). */
+typedef struct wg_engine wg_engine;
+int wg_engine_create(wg_gpu_ctx *ctx, wg_engine **out);
+int wg_engine_destroy(wg_engine *e);
+int wg_tunn_create_on(wg_engine *e, uint32_t first_slot, wg_tunn **out);
+/* what an engine holds: attached Tunns, lanes made so far, pool threads (incl. the
+ * calling thread's share: workers + 1), HIP streams made so far */
+typedef struct wg_engine_info {
+  uint32_t tunns, lanes, max_lanes, pool_threads, streams;
+  uint32_t pad;
+} wg_engine_info;
+int wg_engine_get_info(const wg_engine *e, wg_engine_info *out);
+/* the engine a Tunn is attached to (NULL: a multi-GPU Tunn with private engines) */
+wg_engine *wg_tunn_engine(const wg_tunn *t);
+
+/* A Tunn bound to a GPU context's default engine; it uses key slots
+ * [first_slot, first_slot + 16). */
 int wg_tunn_create(wg_gpu_ctx *ctx, uint32_t first_slot, wg_tunn **out);
 int wg_tunn_destroy(wg_tunn *t);
 
@@ -132,7 +163,11 @@ int wg_tunn_set_time(wg_tunn *t, uint64_t now);
  * threads (default: the CPUs this process may use, at most 16; they spin
  * WG_TUNN_SPIN_US, default 20, before blocking between steps), the kernels read and
  * write that staging over PCIe (WG_TUNN_ZEROCOPY=0: explicit copies to and from
- * HBM instead), and the pool copies the results out. */
+ * HBM instead), and the pool copies the results out.
+ * A batch call that returns an error leaves every selected packet's result at
+ * ERR CryptoFailed unless its chunk completed; the destination bytes of such
+ * packets are unspecified (a registered decapsulate may already have written a
+ * plaintext there on a speculated replay decision). */
 /* sending counter of the current session / replay state of a ring slot (for tests) */
 int wg_tunn_session_counters(const wg_tunn *t, uint32_t ring_slot, uint64_t *sending_counter,
                              wg_replay *window);
@@ -145,6 +180,23 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
 int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
                               const uint32_t *len, uint8_t *const *dst, const uint32_t *dst_cap,
                               wg_tunn_result *res);
+/* Multi-peer batches: packet i belongs to tunn[i] (any mix of the engine's
+ * Tunns, in any order) -- the inter-thread batch of NepTUN's PacketWorkers, whose
+ * entries each carry their own peer (packet_workers.rs:178-205) and are then
+ * encapsulated one by one under that peer's Tunn lock (:207-233, device/mod.rs:
+ * 1328-1337).  The results equal the sequential calls tunn[i]->encapsulate /
+ * decapsulate in packet order: each Tunn's sending counters are handed out in
+ * the order of its packets, its replay window and set_current_session see its
+ * packets in order, tx_bytes / rx_bytes go to the packet's Tunn.  Every tunn[i]
+ * must be attached to `e` (else WG_RC_INVALID_ARGUMENT, nothing done).  The call
+ * takes each distinct Tunn's lock (in address order) for its duration, as the
+ * single-Tunn calls take their Tunn's. */
+int wg_tunn_encapsulate_multi(wg_engine *e, uint32_t n, wg_tunn *const *tunn,
+                              const uint8_t *const *src, const uint32_t *src_len,
+                              uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res);
+int wg_tunn_decapsulate_multi(wg_engine *e, uint32_t n, wg_tunn *const *tunn,
+                              const uint8_t *const *datagram, const uint32_t *len,
+                              uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res);
 /* n x Tunn::decrypt(datagram[i], dst[i]) (feature "xray", mod.rs:383-417 ->
  * Session::decrypt_data_packet session.rs:316-353): the first session whose
  * receiving OR sending index equals the header's receiver_idx, opened with the

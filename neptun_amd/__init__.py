@@ -7,7 +7,7 @@ host-side Tunn semantics.  See DESIGN.md.
 from ._native import NeptunGpuError, HEADER_PATH, LIB_PATH, header_functions, load
 from .gpu import DESC_DTYPE, STATUS, GpuContext, GpuPipe
 from . import tunn
-from .tunn import ReplayWindow, Tunn
+from .tunn import Engine, ReplayWindow, Tunn
 
 __all__ = ["NeptunGpuError", "HEADER_PATH", "LIB_PATH", "header_functions", "load", "DESC_DTYPE", "STATUS",
-           "GpuContext", "GpuPipe", "ReplayWindow", "Tunn", "tunn"]
+           "GpuContext", "GpuPipe", "Engine", "ReplayWindow", "Tunn", "tunn"]

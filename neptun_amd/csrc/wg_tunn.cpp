@@ -333,10 +333,13 @@ class Pool {
     for (auto &t : th_) t.join();
   }
   unsigned size() const { return (unsigned)th_.size() + 1; }
-  // (grain: the fewest items worth a part of their own)
+  // (grain: the fewest items worth a part of their own).  The pool belongs to an
+  // engine whose lanes run batches concurrently: a caller that finds it busy with
+  // another lane's step runs its own step on its own thread instead of waiting.
   void run(size_t n, const std::function<void(size_t, size_t)> &fn, size_t grain = 64) {
     const unsigned parts = (unsigned)std::min<size_t>(size(), std::max<size_t>(n / std::max<size_t>(grain, 1), 1));
-    if (parts <= 1) {
+    std::unique_lock<std::mutex> owner(run_mu_, std::defer_lock);
+    if (parts <= 1 || !owner.try_lock()) {
       if (n) fn(0, n);
       return;
     }
@@ -405,6 +408,7 @@ class Pool {
   }
   const int64_t spin_ns_;
   std::vector<std::thread> th_;
+  std::mutex run_mu_;  // held by the caller whose step the workers run
   std::mutex mu_;
   std::condition_variable cv_, done_;
   const std::function<void(size_t, size_t)> *fn_ = nullptr;
@@ -639,15 +643,30 @@ unsigned pool_workers(unsigned engines) {
   return std::max(1u, std::min(16u, cpus / std::max(1u, engines))) - 1;
 }
 
-// The device side of a Tunn: one GPU context with its staging sets, streams
-// and host copy threads.  A Tunn has one engine per GPU it spreads batches
-// over (wg_tunn_create_multi); each engine works on a contiguous range
+// per-call arrays of a batch (a lane's, reused by every Tunn that borrows it, or a
+// multi-GPU Tunn's own): a Tunn keeps none of its batches' packet-sized state
+struct Scratch {
+  std::vector<uint32_t> sel, slot;
+  std::vector<int32_t> code;           // pass 1: per packet, key slot if selected, else -1
+  std::vector<uint64_t> ctr_all, ctr;  // datagram counters: per packet / per selected packet
+  std::vector<uint8_t> act;            // per selected packet: what lands in dst (open_selected)
+  std::vector<uint8_t> out_dma;        // per selected packet: its dst bytes were DMA'd (no host copy)
+  std::vector<uint8_t> spec;           // per selected packet: speculated to land in dst (DMA decapsulate)
+};
+
+// The device side of a batch: one GPU context with its staging sets, streams
+// and host copy threads.  As a lane of a shared engine (wg_engine) it is borrowed
+// by one batch call at a time; a multi-GPU Tunn has one private engine per GPU it
+// spreads batches over (wg_tunn_create_multi), each working on a contiguous range
 // [k0, k1) of the batch's selected packets.
 struct Engine {
   wg_gpu_ctx *ctx = nullptr;
   int device = 0, numa = -1;
   Staging st[kSets];
   Pool *pool = nullptr;
+  bool own_pool = true;       // false: a lane of a shared engine (the engine's pool)
+  Scratch scratch;            // the per-call arrays of the calls that borrow this lane
+  wg_tunn *owner = nullptr;   // batch owner of the multi-peer calls on this lane
   Driver *driver = nullptr;   // multi-engine Tunns only (the single engine runs on the caller)
   size_t k0 = 0, k1 = 0;      // this batch's share of the selected packets
   std::vector<Chunk> chunks;
@@ -703,16 +722,31 @@ struct wg_tunn {
   // only timer state the data plane reads (set_current_session, mod.rs:530-538)
   uint64_t time_current = 0;
   uint64_t session_timers[WG_N_SESSIONS] = {};
-  std::vector<Engine *> eng;
-  wg_tunn_phases ph{};      // caller-side phases (checks, decide, totals)
-  // per-call scratch (kept to avoid reallocations)
-  std::vector<uint32_t> sel, slot;
-  std::vector<int32_t> code;    // pass 1: per packet, key slot if selected, else -1
-  std::vector<uint64_t> ctr_all, ctr;  // datagram counters: per packet / per selected packet
-  std::vector<uint8_t> act;     // per selected packet: what lands in dst (open_selected)
-  std::vector<uint8_t> out_dma; // per selected packet: its dst bytes were DMA'd (no host copy)
-  std::vector<uint8_t> spec;    // per selected packet: speculated to land in dst (DMA decapsulate)
+  // the reference's Mutex<Tunn> (device/peer.rs:29): every call on the Tunn, and a
+  // multi-peer call on each of its Tunns, holds it
+  mutable std::mutex mu;
+  wg_engine *group = nullptr;  // the shared engine (nullptr: private engines, wg_tunn_create_multi)
+  std::vector<Engine *> eng;   // the private engines, or during a call the borrowed lane
+  Scratch own;                 // per-call arrays of a Tunn with private engines
+  Scratch *sc = &own;          // ... or, during a call, the borrowed lane's
+  bool timing = false;         // wg_tunn_set_phase_timing
+  wg_tunn_phases ph{};         // caller-side phases (checks, decide, totals)
+  wg_tunn_phases ph_lanes{};   // the lanes' share of this Tunn's calls
+  std::atomic<uint64_t> mark{0};  // multi-peer calls: collecting the distinct Tunns
   wg_replay spec_window[WG_N_SESSIONS];  // the speculation's replay windows (this call)
+};
+
+// A per-GPU engine shared by Tunns (include/neptun_tunn.h): one host pool, lanes
+// made on demand and lent to one batch call at a time.
+struct wg_engine {
+  wg_gpu_ctx *ctx = nullptr;
+  int device = 0;
+  Pool *pool = nullptr;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Engine *> lanes, idle;
+  uint32_t max_lanes = 8, tunns = 0;
+  bool implicit = false;  // a context's default engine (wg_tunn_create): dies with its last Tunn
 };
 
 namespace {
@@ -887,7 +921,7 @@ void make_chunks(Engine &E, SizeFn size, size_t limit = 0, bool ramp = false) {
 // engine ranges of about equal staging bytes (size(k) per packet).
 template <class SizeFn>
 void split(wg_tunn *t, SizeFn size, size_t a = 0, size_t b = ~size_t(0)) {
-  const size_t n = std::min(b, t->sel.size()), E = t->eng.size();
+  const size_t n = std::min(b, t->sc->sel.size()), E = t->eng.size();
   if (E == 1) {
     t->eng[0]->k0 = a;
     t->eng[0]->k1 = n;
@@ -1273,6 +1307,9 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
   }
   if (!build_runs(0, nc0)) return 1;
   PipelineDrain drain_guard(E);
+  // outgrown direct-output sinks of earlier batches: their kernels have drained
+  for (void *p : E.sink_old) (void)hipHostFree(p);
+  E.sink_old.clear();
   const bool split_streams = dma_streams();
   const uint32_t scatter_cap = scatter_blocks();
   const bool split_scatter = std::getenv("WG_TUNN_SPLIT_SCATTER") != nullptr;  // (A/B only)
@@ -1441,7 +1478,7 @@ uint64_t validate(const uint8_t *pt, uint32_t P, wg_tunn_result &r) {
 //    batch size (a 16M-packet batch over 2 GPUs needs no more than 1 GPU does).
 constexpr uint8_t kFinish = 0x80;
 
-// partial: t->sel holds only the selection of the batch's first packets, and grow()
+// partial: t->sc->sel holds only the selection of the batch's first packets, and grow()
 // appends the rest (in order) -- so that a registered DMA batch can put its first chunk
 // on the device while the host is still checking the rest (pass 1); every other path
 // grows the selection first.  n_cap: the batch's packet count.
@@ -1454,18 +1491,18 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     grow();
     partial = false;
   }
-  auto size = [&](size_t k) { return round128(len[t->sel[k]]); };
+  auto size = [&](size_t k) { return round128(len[t->sc->sel[k]]); };
   if (!multi) split(t, size);
-  t->act.assign(t->sel.size(), 0);
-  t->out_dma.assign(t->sel.size(), 0);
-  t->spec.assign(t->sel.size(), 0);
+  t->sc->act.assign(t->sc->sel.size(), 0);
+  t->sc->out_dma.assign(t->sc->sel.size(), 0);
+  t->sc->spec.assign(t->sc->sel.size(), 0);
   auto grow_all = [&]() {  // the full selection, and the per-packet state sized for it
     if (!partial) return;
     grow();
     partial = false;
-    t->act.resize(t->sel.size(), 0);
-    t->out_dma.resize(t->sel.size(), 0);
-    t->spec.resize(t->sel.size(), 0);
+    t->sc->act.resize(t->sc->sel.size(), 0);
+    t->sc->out_dma.resize(t->sc->sel.size(), 0);
+    t->sc->spec.resize(t->sc->sel.size(), 0);
   };
   const bool nt = nt_copies();
   std::atomic<uint64_t> rx{0};
@@ -1476,18 +1513,18 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       uint64_t my_rx = 0;
       for (size_t kk = lo; kk < hi; ++kk) {
         const size_t k = ch.k0 + kk;
-        const uint8_t a = t->act[k];
+        const uint8_t a = t->sc->act[k];
         if (!a) continue;
-        const uint32_t i = t->sel[k];
+        const uint32_t i = t->sc->sel[k];
         const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
         // plaintext (or ring's zeros): scattered into dst already, else in the pinned staging
-        const bool in_dst = t->out_dma[k];
+        const bool in_dst = t->sc->out_dma[k];
         const uint8_t *pt = in_dst ? dst[i] : h_out + h_desc[kk].dst_off;
         if (!in_dst) {
           if ((a & 3) == 1) copy_bytes(dst[i], pt, P, nt);
           else std::memset(dst[i], 0, P);
           std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
-        } else if (t->out_dma[k] == 2) {  // direct output: the kernel wrote the plaintext only
+        } else if (t->sc->out_dma[k] == 2) {  // direct output: the kernel wrote the plaintext only
           std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
         }
         if (a & kFinish) my_rx += finish(k, in_dst ? dst[i] : pt, P);
@@ -1498,7 +1535,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
   };
   auto decide_range = [&](size_t k0, size_t k1, const int32_t *st) {
     const double a = now_us();
-    for (size_t k = k0; k < k1; ++k) t->act[k] = decide(k, st[k - k0]);
+    for (size_t k = k0; k < k1; ++k) t->sc->act[k] = decide(k, st[k - k0]);
     t->ph.decide_us += now_us() - a;
   };
   // DMA batch (registered datagrams and destinations, one engine): run_dma with the
@@ -1513,7 +1550,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
   auto registered = [&](Engine &E, size_t a, size_t b) {  // datagrams and dsts of [a, b)
     E.ddst.resize(b - E.k0);
     return all_packets(E, a, b, [&](size_t k, size_t &ha, size_t &hb) {
-      const uint32_t i = t->sel[k];
+      const uint32_t i = t->sc->sel[k];
       uint64_t unused;
       return dev_addr(E, datagram[i], len[i], unused, ha) &&
              dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0], hb);
@@ -1539,8 +1576,8 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       const size_t m = ch.k1 - ch.k0;
       uint32_t pmax = 0;
       for (size_t k = ch.k0; k < ch.k1; ++k) {  // (in packet order)
-        t->spec[k] = speculate(k);
-        if (!t->spec[k]) pmax = std::max(pmax, len[t->sel[k]] - (uint32_t)WG_DATA_OVERHEAD_SZ);
+        t->sc->spec[k] = speculate(k);
+        if (!t->sc->spec[k]) pmax = std::max(pmax, len[t->sc->sel[k]] - (uint32_t)WG_DATA_OVERHEAD_SZ);
       }
       E.ph.pack_spec_us += now_us() - a;
       // direct output: the open kernel writes the plaintext of every packet the
@@ -1550,13 +1587,13 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       // a chunk the strided text-grid open takes: every packet lands, one length and one
       // key slot, plaintext slots at a constant stride on whole 128-byte lines
       if (strided_ok && pmax == 0 && m >= 64) {
-        const uint32_t L = len[t->sel[ch.k0]], sl = t->slot[ch.k0];
+        const uint32_t L = len[t->sc->sel[ch.k0]], sl = t->sc->slot[ch.k0];
         const uint64_t d0 = E.ddst[j0], ds = m > 1 ? E.ddst[j0 + 1] - d0 : 0;
         bool uni = L >= WG_DATA_OVERHEAD_SZ && d0 % 128 == 0 && ds % 128 == 0 && ds >= L - WG_DATA_OVERHEAD_SZ &&
                    ds < (1ull << 25) && 63 * ds + L + 64 < (1ull << 31);
         for (size_t kk = 0; uni && kk < m; ++kk) {
           const size_t k = ch.k0 + kk;
-          uni = t->spec[k] && len[t->sel[k]] == L && t->slot[k] == sl && E.ddst[j0 + kk] == d0 + kk * ds;
+          uni = t->sc->spec[k] && len[t->sc->sel[k]] == L && t->sc->slot[k] == sl && E.ddst[j0 + kk] == d0 + kk * ds;
         }
         if (uni) {
           E.chunk_strided[c] = Engine::StridedOpen{L, sl, d0, ds};
@@ -1567,23 +1604,23 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       uint64_t base = 0;
       // (the sink target sits 16 bytes past a line, like the dsts auto mode takes)
       if (out_mode != 0 && (pmax + 16 <= E.sink_cap || grow_sink(E, pmax + 16))) {
-        auto addr = [&](size_t kk) { return t->spec[ch.k0 + kk] ? E.ddst[j0 + kk] : E.sink_dev + 16; };
-        auto ext = [&](size_t kk) { return (uint64_t)len[t->sel[ch.k0 + kk]] - WG_DATA_OVERHEAD_SZ; };
+        auto addr = [&](size_t kk) { return t->sc->spec[ch.k0 + kk] ? E.ddst[j0 + kk] : E.sink_dev + 16; };
+        auto ext = [&](size_t kk) { return (uint64_t)len[t->sc->sel[ch.k0 + kk]] - WG_DATA_OVERHEAD_SZ; };
         base = direct_base(m, addr, ext, out_mode == 2 ? 16 : -1);
       }
       E.chunk_direct[&ch - E.chunks.data()] = base != 0;
       E.pool->run(m, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = j0 + kk;
-          const uint32_t i = t->sel[k];
+          const uint32_t i = t->sc->sel[k];
           const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ, o = (uint32_t)E.off[j] + WG_DATA_OFFSET;
           if (base) {
-            E.b_desc[j] = wg_packet_desc{E.off[j], (t->spec[k] ? E.ddst[j] : E.sink_dev + 16) - base, 0, len[i],
-                                         t->slot[k]};
+            E.b_desc[j] = wg_packet_desc{E.off[j], (t->sc->spec[k] ? E.ddst[j] : E.sink_dev + 16) - base, 0, len[i],
+                                         t->sc->slot[k]};
           } else {
-            E.b_desc[j] = wg_packet_desc{E.off[j], o, 0, len[i], t->slot[k]};
+            E.b_desc[j] = wg_packet_desc{E.off[j], o, 0, len[i], t->sc->slot[k]};
             // plaintext then the received tag (ct||tag lands in dst, session.rs:287-289)
-            E.b_jobs[j] = t->spec[k] ? Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE} : Scatter{0, 0, 0, 0, 0};
+            E.b_jobs[j] = t->sc->spec[k] ? Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE} : Scatter{0, 0, 0, 0, 0};
           }
         }
       });
@@ -1595,10 +1632,10 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       std::vector<size_t> rep;
       const uint8_t landed = E.chunk_direct[&ch - E.chunks.data()] ? 2 : 1;  // 2: the tag still to write
       for (size_t k = ch.k0; k < ch.k1; ++k) {
-        const bool lands = (t->act[k] & 3) != 0;
-        if (lands && !t->spec[k]) rep.push_back(k);
-        t->out_dma[k] = lands && t->spec[k] ? landed : 0;
-        if (!lands && t->spec[k]) {  // (cannot happen: see above)
+        const bool lands = (t->sc->act[k] & 3) != 0;
+        if (lands && !t->sc->spec[k]) rep.push_back(k);
+        t->sc->out_dma[k] = lands && t->sc->spec[k] ? landed : 0;
+        if (!lands && t->sc->spec[k]) {  // (cannot happen: see above)
           err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: a speculated replay decision was not kept", hipSuccess);
           return;
         }
@@ -1607,16 +1644,16 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
         // open the missed packets again into pinned staging; their decisions stand
         Staging &A = E.aux;
         uint64_t bytes = 0;
-        for (size_t k : rep) bytes += round128(len[t->sel[k]]);
+        for (size_t k : rep) bytes += round128(len[t->sc->sel[k]]);
         if (const hipError_t e = reserve(A, bytes + 128, rep.size()); e != hipSuccess) {
           err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair staging", e);
           return;
         }
         uint64_t o = 0;
         for (size_t r = 0; r < rep.size(); ++r) {
-          const uint32_t i = t->sel[rep[r]];
+          const uint32_t i = t->sc->sel[rep[r]];
           std::memcpy(A.h_in + o, datagram[i], len[i]);
-          A.h_desc[r] = wg_packet_desc{o, o + WG_DATA_OFFSET, 0, len[i], t->slot[rep[r]]};
+          A.h_desc[r] = wg_packet_desc{o, o + WG_DATA_OFFSET, 0, len[i], t->sc->slot[rep[r]]};
           o += round128(len[i]);
         }
         if (const int rc = wg_gpu_open_batch(E.ctx, A.h_desc, (uint32_t)rep.size(), A.h_in, A.h_out, A.h_st,
@@ -1630,24 +1667,24 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
         }
         for (size_t r = 0; r < rep.size(); ++r) {
           const size_t k = rep[r];
-          const uint32_t i = t->sel[k];
+          const uint32_t i = t->sc->sel[k];
           const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
-          if ((t->act[k] & 3) == 1) std::memcpy(dst[i], A.h_out + A.h_desc[r].dst_off, P);
+          if ((t->sc->act[k] & 3) == 1) std::memcpy(dst[i], A.h_out + A.h_desc[r].dst_off, P);
           else std::memset(dst[i], 0, P);
           std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
-          t->out_dma[k] = 1;  // (in dst now)
+          t->sc->out_dma[k] = 1;  // (in dst now)
         }
       }
       copy_out(E, ch, nullptr, nullptr);
     };
     auto more = [&]() -> int {
       if (!partial) return 1;
-      const size_t had = t->sel.size();
+      const size_t had = t->sc->sel.size();
       grow_all();
-      if (t->sel.size() == had) return 1;
-      if (!registered(E, had, t->sel.size())) return 2;
-      append_chunks(E, size, had, t->sel.size(), chunk_bytes());
-      E.k1 = t->sel.size();
+      if (t->sc->sel.size() == had) return 1;
+      if (!registered(E, had, t->sc->sel.size())) return 2;
+      append_chunks(E, size, had, t->sc->sel.size(), chunk_bytes());
+      E.k1 = t->sc->sel.size();
       E.chunk_direct.resize(E.chunks.size(), 0);
       E.chunk_strided.resize(E.chunks.size(), Engine::StridedOpen{});
       return 0;
@@ -1661,8 +1698,8 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
                                  reinterpret_cast<uint8_t *>(so.dst), so.dst_stride, E.b_st + (ch.k0 - E.k0), q);
     };
     const int r = run_dma(
-        E, false, t_prep, n_cap, [&](size_t k) { return datagram[t->sel[k]]; },
-        [&](size_t k) { return len[t->sel[k]]; }, fill, done, more, launch);
+        E, false, t_prep, n_cap, [&](size_t k) { return datagram[t->sc->sel[k]]; },
+        [&](size_t k) { return len[t->sc->sel[k]]; }, fill, done, more, launch);
     if (r == 1 && partial) {  // (nothing was done)
       grow_all();
       split(t, size);
@@ -1673,7 +1710,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     if (const int r = dma_batch(E); r == 2) {  // the rest of the batch: staged
       grow_all();
       E.k0 = E.k1;
-      E.k1 = t->sel.size();
+      E.k1 = t->sc->sel.size();
     } else if (r != 1) {
       return r;
     }
@@ -1683,7 +1720,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     bool direct = direct_possible(E);
     E.dsrc.resize(E.k1 - E.k0);
     for (size_t k = E.k0; direct && k < E.k1; ++k) {
-      const uint32_t i = t->sel[k];
+      const uint32_t i = t->sc->sel[k];
       direct = (reinterpret_cast<uint64_t>(datagram[i]) & 15u) == 0 &&
                dev_addr(E, datagram[i], len[i], E.dsrc[k - E.k0]);
     }
@@ -1691,13 +1728,13 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = k - E.k0;
-          const uint32_t i = t->sel[k];
+          const uint32_t i = t->sc->sel[k];
           if (direct) {
             // dst is staging: the replay decision comes after the GPU (session.rs:279-300)
-            S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
+            S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->sc->slot[k]};
           } else {
             copy_bytes(S.h_in + E.off[j], datagram[i], len[i], nt);
-            S.h_desc[kk] = wg_packet_desc{E.off[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->slot[k]};
+            S.h_desc[kk] = wg_packet_desc{E.off[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->sc->slot[k]};
           }
         }
       });
@@ -1717,7 +1754,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     rc = for_engines(t, engine_job);
   } else {
     // several engines: rounds of about engines x chunk_bytes() staging bytes
-    const size_t n = t->sel.size();
+    const size_t n = t->sc->sel.size();
     const uint64_t cap = (uint64_t)chunk_bytes() * t->eng.size();
     for (size_t a = 0; a < n && !rc;) {
       size_t b = a;
@@ -1771,14 +1808,20 @@ void destroy_engine(Engine *E) {
       if (S.stream) (void)hipStreamDestroy(S.stream);
     }
   }
-  delete E->pool;
+  if (E->own_pool) delete E->pool;
+  delete E->owner;
   delete E;
 }
 
-int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out) {
+// shared: the engine's pool (a lane), else the engine makes its own
+int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out, Pool *shared = nullptr) {
   Engine *E = new (std::nothrow) Engine;
   if (!E) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: host alloc", hipSuccess);
   E->ctx = ctx;
+  if (shared) {
+    E->pool = shared;
+    E->own_pool = false;
+  }
   E->device = wg_ctx_device(ctx);
   if (multi) {
     E->numa = device_numa_node(E->device);
@@ -1804,7 +1847,7 @@ int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out) {
       destroy_engine(E);
       return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", hipGetLastError());
     }
-  E->pool = new (std::nothrow) Pool(pool_workers(engines), E->numa);
+  if (!shared) E->pool = new (std::nothrow) Pool(pool_workers(engines), E->numa);
   if (multi && E->pool) E->driver = new (std::nothrow) Driver(E->numa);
   if (!E->pool || (multi && !E->driver)) {
     destroy_engine(E);
@@ -1814,9 +1857,182 @@ int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out) {
   return WG_RC_OK;
 }
 
+// lanes of a shared engine: streams per lane (staging sets + repair + DMA streams)
+constexpr uint32_t kLaneStreams = kSets + 1 + 3;
+
+uint32_t engine_max_lanes() {  // WG_ENGINE_LANES (1..64, default 8), read when an engine is made
+  const char *e = std::getenv("WG_ENGINE_LANES");
+  return e ? (uint32_t)std::min(64, std::max(1, std::atoi(e))) : 8u;
+}
+
+// borrow a lane (made on first need, up to max_lanes; else wait for one)
+int lane_acquire(wg_engine *g, Engine **out) {
+  std::unique_lock<std::mutex> lk(g->mu);
+  for (;;) {
+    if (!g->idle.empty()) {
+      *out = g->idle.back();
+      g->idle.pop_back();
+      return WG_RC_OK;
+    }
+    if (g->lanes.size() < g->max_lanes) {
+      Engine *E = nullptr;
+      if (const int rc = make_engine(g->ctx, false, 1, &E, g->pool)) return rc;
+      g->lanes.push_back(E);
+      *out = E;
+      return WG_RC_OK;
+    }
+    g->cv.wait(lk);
+  }
+}
+
+void lane_release(wg_engine *g, Engine *E) {
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->idle.push_back(E);
+  }
+  g->cv.notify_one();
+}
+
+void add_lane_phases(wg_tunn_phases &to, const wg_tunn_phases &p) {
+  to.chunks += p.chunks;
+  to.pack_us += p.pack_us;
+  to.submit_us += p.submit_us;
+  to.wait_us += p.wait_us;
+  to.copy_out_us += p.copy_out_us;
+  to.dev_h2d_us += p.dev_h2d_us;
+  to.dev_kernel_us += p.dev_kernel_us;
+  to.dev_d2h_us += p.dev_d2h_us;
+  to.pack_spec_us += p.pack_spec_us;
+  to.prep_us += p.prep_us;
+}
+
+// A batch call's lane: a Tunn on a shared engine borrows one for the call (its
+// engine list and per-call arrays point at the lane meanwhile); the lane's phase
+// times go to the Tunn.  Private engines (multi-GPU Tunns): nothing to do.
+struct Lease {
+  wg_tunn *t;
+  Engine *E = nullptr;
+  int rc = WG_RC_OK;
+  explicit Lease(wg_tunn *tt, Engine *lane = nullptr) : t(tt) {
+    if (!t->group) return;
+    if (lane) E = lane;
+    else if ((rc = lane_acquire(t->group, &E)) != WG_RC_OK) return;
+    E->timing = t->timing;
+    E->ph = wg_tunn_phases{};
+    t->eng.assign(1, E);
+    t->sc = &E->scratch;
+  }
+  ~Lease() {
+    if (!E) return;
+    add_lane_phases(t->ph_lanes, E->ph);
+    E->ph = wg_tunn_phases{};
+    t->eng.clear();
+    t->sc = &t->own;
+    lane_release(t->group, E);
+  }
+};
+
+// every context's default engine (wg_tunn_create)
+std::mutex g_default_mu;
+std::vector<std::pair<wg_gpu_ctx *, wg_engine *>> g_default;
+
+int engine_make(wg_gpu_ctx *ctx, wg_engine **out) {
+  wg_engine *g = new (std::nothrow) wg_engine;
+  if (!g) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "engine_create: host alloc", hipSuccess);
+  g->ctx = ctx;
+  g->device = wg_ctx_device(ctx);
+  g->max_lanes = engine_max_lanes();
+  g->pool = new (std::nothrow) Pool(pool_workers(1), -1);
+  if (!g->pool) {
+    delete g;
+    return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "engine_create: threads", hipSuccess);
+  }
+  *out = g;
+  return WG_RC_OK;
+}
+
+void engine_free(wg_engine *g) {
+  for (Engine *E : g->lanes) destroy_engine(E);
+  delete g->pool;
+  delete g;
+}
+
+int tunn_attach(wg_engine *g, uint32_t first_slot, wg_tunn **out) {
+  if ((uint64_t)first_slot + 2 * WG_N_SESSIONS > wg_gpu_ctx_key_slots(g->ctx))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: needs 16 key slots", hipSuccess);
+  wg_tunn *t = new (std::nothrow) wg_tunn;
+  if (!t) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: host alloc", hipSuccess);
+  t->first_slot = first_slot;
+  t->group = g;
+  std::lock_guard<std::mutex> lk(g->mu);
+  ++g->tunns;
+  *out = t;
+  return WG_RC_OK;
+}
+
+// The distinct Tunns of a multi-peer batch, sorted by address (the lock order);
+// false if one is null or not attached to g.
+bool collect_peers(wg_engine *g, uint32_t n, wg_tunn *const *peer, std::vector<wg_tunn *> &out) {
+  static std::atomic<uint64_t> epoch{1};
+  const uint64_t ep = epoch.fetch_add(1, std::memory_order_relaxed);
+  out.clear();
+  const wg_tunn *last = nullptr;
+  for (uint32_t i = 0; i < n; ++i) {
+    wg_tunn *p = peer[i];
+    if (!p) return false;
+    if (p == last) continue;
+    last = p;
+    // (a concurrent call may re-mark a Tunn: duplicates are removed below)
+    if (p->mark.load(std::memory_order_relaxed) != ep) {
+      p->mark.store(ep, std::memory_order_relaxed);
+      out.push_back(p);
+    }
+  }
+  std::sort(out.begin(), out.end());
+  out.erase(std::unique(out.begin(), out.end()), out.end());
+  for (const wg_tunn *p : out)
+    if (p->group != g) return false;
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+int wg_engine_create(wg_gpu_ctx *ctx, wg_engine **out) {
+  if (!ctx || !out) return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "engine_create: null", hipSuccess);
+  return engine_make(ctx, out);
+}
+
+int wg_engine_destroy(wg_engine *e) {
+  if (!e) return WG_RC_OK;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->tunns || e->implicit)
+      return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "engine_destroy: Tunns are still attached", hipSuccess);
+  }
+  engine_free(e);
+  return WG_RC_OK;
+}
+
+int wg_engine_get_info(const wg_engine *e, wg_engine_info *out) {
+  if (!e || !out) return WG_RC_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(const_cast<wg_engine *>(e)->mu);
+  *out = wg_engine_info{};
+  out->tunns = e->tunns;
+  out->lanes = (uint32_t)e->lanes.size();
+  out->max_lanes = e->max_lanes;
+  out->pool_threads = e->pool->size();
+  out->streams = out->lanes * kLaneStreams;
+  return WG_RC_OK;
+}
+
+int wg_tunn_create_on(wg_engine *e, uint32_t first_slot, wg_tunn **out) {
+  if (!e || !out) return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create_on: null", hipSuccess);
+  return tunn_attach(e, first_slot, out);
+}
+
+wg_engine *wg_tunn_engine(const wg_tunn *t) { return t ? t->group : nullptr; }
 
 int wg_tunn_create_multi(wg_gpu_ctx *const *ctxs, uint32_t nctx, uint32_t first_slot,
                          wg_tunn **out) {
@@ -1827,6 +2043,7 @@ int wg_tunn_create_multi(wg_gpu_ctx *const *ctxs, uint32_t nctx, uint32_t first_
     if ((uint64_t)first_slot + 2 * WG_N_SESSIONS > wg_gpu_ctx_key_slots(ctxs[e]))
       return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: needs 16 key slots", hipSuccess);
   }
+  if (nctx == 1) return wg_tunn_create(ctxs[0], first_slot, out);  // (the context's shared engine)
   wg_tunn *t = new (std::nothrow) wg_tunn;
   if (!t) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: host alloc", hipSuccess);
   t->first_slot = first_slot;
@@ -1845,20 +2062,62 @@ int wg_tunn_create_multi(wg_gpu_ctx *const *ctxs, uint32_t nctx, uint32_t first_
 
 int wg_tunn_create(wg_gpu_ctx *ctx, uint32_t first_slot, wg_tunn **out) {
   if (!ctx || !out) return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: null", hipSuccess);
-  return wg_tunn_create_multi(&ctx, 1, first_slot, out);
+  if ((uint64_t)first_slot + 2 * WG_N_SESSIONS > wg_gpu_ctx_key_slots(ctx))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: needs 16 key slots", hipSuccess);
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  wg_engine *g = nullptr;
+  for (auto &d : g_default)
+    if (d.first == ctx) g = d.second;
+  const bool made = g == nullptr;
+  if (made) {
+    if (const int rc = engine_make(ctx, &g)) return rc;
+    g->implicit = true;
+    g_default.emplace_back(ctx, g);
+  }
+  const int rc = tunn_attach(g, first_slot, out);
+  if (rc && made) {
+    g_default.pop_back();
+    engine_free(g);
+  }
+  return rc;
 }
 
 int wg_tunn_destroy(wg_tunn *t) {
   if (!t) return WG_RC_OK;
-  for (Engine *E : t->eng) destroy_engine(E);
+  if (wg_engine *g = t->group) {
+    std::lock_guard<std::mutex> dl(g_default_mu);
+    bool last;
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      last = --g->tunns == 0 && g->implicit;
+    }
+    if (last) {  // a context's default engine goes with its last Tunn
+      for (size_t k = 0; k < g_default.size(); ++k)
+        if (g_default[k].second == g) {
+          g_default.erase(g_default.begin() + (long)k);
+          break;
+        }
+      engine_free(g);
+    }
+  } else {
+    for (Engine *E : t->eng) destroy_engine(E);
+  }
   delete t;
   return WG_RC_OK;
 }
 
-uint32_t wg_tunn_engines(const wg_tunn *t) { return t ? (uint32_t)t->eng.size() : 0u; }
+uint32_t wg_tunn_engines(const wg_tunn *t) {
+  if (!t) return 0u;
+  return t->group ? 1u : (uint32_t)t->eng.size();
+}
 
 int wg_tunn_engine_info(const wg_tunn *t, uint32_t engine, int *device, int *numa_node) {
-  if (!t || engine >= t->eng.size()) return WG_RC_INVALID_ARGUMENT;
+  if (!t || engine >= wg_tunn_engines(t)) return WG_RC_INVALID_ARGUMENT;
+  if (t->group) {
+    if (device) *device = t->group->device;
+    if (numa_node) *numa_node = -1;  // (a shared engine's pool is not bound)
+    return WG_RC_OK;
+  }
   if (device) *device = t->eng[engine]->device;
   if (numa_node) *numa_node = t->eng[engine]->numa;
   return WG_RC_OK;
@@ -1875,6 +2134,12 @@ int wg_tunn_install_session(wg_tunn *t, uint32_t local_index, uint32_t peer_inde
   std::memcpy(keys + 32, sending_key, 32);
   // receiving slot checks our index; sending slot writes the peer's (session.rs:226, :275)
   const uint32_t idx[2] = {local_index, peer_index};
+  std::lock_guard<std::mutex> lk(t->mu);
+  if (t->group) {  // (synchronous: the copy has landed when set_keys returns)
+    DevGuard g(t->group->device);
+    const int rc = wg_gpu_set_keys(t->group->ctx, t->first_slot + 2 * ring, 2, keys, idx, nullptr);
+    if (rc) return rc;
+  }
   for (Engine *E : t->eng) {  // every GPU holds the session's keys
     DevGuard g(E->device);
     const int rc = wg_gpu_set_keys(E->ctx, t->first_slot + 2 * ring, 2, keys, idx, E->st[0].stream);
@@ -1894,12 +2159,14 @@ int wg_tunn_install_session(wg_tunn *t, uint32_t local_index, uint32_t peer_inde
 
 int wg_tunn_set_time(wg_tunn *t, uint64_t now) {
   if (!t) return WG_RC_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(t->mu);
   t->time_current = now;  // update_timers: timers[TimeCurrent] = now (timers.rs:228-233)
   return WG_RC_OK;
 }
 
 int wg_tunn_stats(const wg_tunn *t, uint64_t *tx_bytes, uint64_t *rx_bytes) {
   if (!t) return WG_RC_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(t->mu);
   if (tx_bytes) *tx_bytes = t->tx_bytes;
   if (rx_bytes) *rx_bytes = t->rx_bytes;
   return WG_RC_OK;
@@ -1908,34 +2175,41 @@ int wg_tunn_stats(const wg_tunn *t, uint64_t *tx_bytes, uint64_t *rx_bytes) {
 int wg_tunn_session_counters(const wg_tunn *t, uint32_t ring_slot, uint64_t *sending_counter,
                              wg_replay *window) {
   if (!t || ring_slot >= WG_N_SESSIONS) return WG_RC_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(t->mu);
   if (sending_counter) *sending_counter = t->sessions[ring_slot].sending_counter;
   if (window) *window = t->sessions[ring_slot].window;
   return WG_RC_OK;
 }
 
-int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
-                              const uint32_t *src_len, uint8_t *const *dst,
-                              const uint32_t *dst_cap, wg_tunn_result *res) {
-  if (!t || (n && (!src || !src_len || !dst || !dst_cap || !res)))
-    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "encapsulate_batch: null", hipSuccess);
-  if (n == 0) return WG_RC_OK;
+// n x Tunn::encapsulate.  t: the batch owner (the Tunn of a single-Tunn call, whose
+// lane / engines and per-call arrays the batch runs on; a lane's owner for a
+// multi-peer call).  peer: nullptr (every packet is t's), or packet i's Tunn.
+static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_t *const *src,
+                      const uint32_t *src_len, uint8_t *const *dst, const uint32_t *dst_cap,
+                      wg_tunn_result *res) {
   PhaseCall pc(t, n);
-  Session &s = t->sessions[t->current % WG_N_SESSIONS];  // mod.rs:310
+  const bool many = peer != nullptr;
+  Session &s = t->sessions[t->current % WG_N_SESSIONS];  // mod.rs:310 (single-Tunn batches)
   const uint32_t slot = t->first_slot + 2 * (uint32_t)(t->current % WG_N_SESSIONS) + 1;
   // pass 1 (stateless checks, on the pool; the counters are reserved below) over
   // packets [lo, hi), appending to the selection
-  t->code.resize(n);
-  t->sel.clear();
+  t->sc->code.resize(n);
+  t->sc->sel.clear();
   const bool live = s.live;
+  auto live_of = [&](size_t i) {  // the packet's Tunn has a current session (mod.rs:310)
+    if (!many) return live;
+    const wg_tunn *T = peer[i];
+    return T->sessions[T->current % WG_N_SESSIONS].live;
+  };
   auto pass1 = [&](size_t lo0, size_t hi0) {
     t->eng[0]->pool->run(hi0 - lo0, [&](size_t lo, size_t hi) {
       for (size_t i = lo0 + lo; i < lo0 + hi; ++i) {
-        t->code[i] = -1;
+        t->sc->code[i] = -1;
         if ((uint64_t)src_len[i] + WG_DATA_OFFSET > dst_cap[i]) {  // encapsulate: dst[16..len+16]
           set_err(res[i], WG_STATUS_INVALID_LENGTH);
           continue;
         }
-        if (!live) {  // no session: the CPU Tunn queues the packet and starts a handshake
+        if (!live_of(i)) {  // no session: the CPU Tunn queues the packet and starts a handshake
           std::memset(&res[i], 0, sizeof res[i]);
           res[i].kind = WG_TUNN_NOT_DATA;
           res[i].status = WG_STATUS_NO_CURRENT_SESSION;
@@ -1945,18 +2219,18 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
           // until its chunk comes back a selected packet reads as failed (a batch that
           // errors part-way leaves no stale or zeroed results behind)
           set_err(res[i], WG_STATUS_CRYPTO_FAILED);
-          t->code[i] = 0;
+          t->sc->code[i] = 0;
           continue;
         }
         // mod.rs:296-299 copies src into dst[16..] before looking at the session
         std::memcpy(dst[i] + WG_DATA_OFFSET, src[i], src_len[i]);
       }
     });
-    const size_t had = t->sel.size();
-    t->sel.resize(had + (hi0 - lo0));
-    t->sel.resize(had + compact(
-        *t->eng[0]->pool, hi0 - lo0, [&](size_t j) { return t->code[lo0 + j] >= 0; },
-        [&](size_t o, size_t j) { t->sel[had + o] = (uint32_t)(lo0 + j); }));
+    const size_t had = t->sc->sel.size();
+    t->sc->sel.resize(had + (hi0 - lo0));
+    t->sc->sel.resize(had + compact(
+        *t->eng[0]->pool, hi0 - lo0, [&](size_t j) { return t->sc->code[lo0 + j] >= 0; },
+        [&](size_t o, size_t j) { t->sc->sel[had + o] = (uint32_t)(lo0 + j); }));
   };
   // one fetch_add per batch (session.rs:219), BEFORE the split: every engine's
   // packets carry counters ctr0 + k (k: the packet's rank in the selection), disjoint
@@ -1964,7 +2238,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
   // a registered DMA batch puts that part's first chunk on the device while pass 1
   // covers the rest; the reservation grows with the selection.
   const uint64_t ctr0 = s.sending_counter;
-  const size_t n0 = n >= 16384 && dma_runs() && t->eng.size() == 1 ? n / 16 : n;
+  const size_t n0 = n >= 16384 && dma_runs() && t->eng.size() == 1 && !many ? n / 16 : n;
   pass1(0, n0);
   bool partial = n0 < n;
   auto grow = [&]() {
@@ -1972,14 +2246,30 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
     partial = false;
     const double a = now_us();
     pass1(n0, n);
-    s.sending_counter = ctr0 + t->sel.size();
+    s.sending_counter = ctr0 + t->sc->sel.size();
     t->ph.checks_us += now_us() - a;
   };
-  s.sending_counter = ctr0 + t->sel.size();
-  if (t->sel.empty()) grow();
-  if (t->sel.empty()) return WG_RC_OK;
+  if (!many) s.sending_counter = ctr0 + t->sc->sel.size();
+  if (t->sc->sel.empty()) grow();
+  if (t->sc->sel.empty()) return WG_RC_OK;
+  if (many) {
+    // each Tunn's counters in the order of its packets (session.rs:219 per packet), and
+    // the key slot of its current session (mod.rs:310)
+    Scratch &q = *t->sc;
+    q.ctr.resize(q.sel.size());
+    q.slot.resize(q.sel.size());
+    for (size_t k = 0; k < q.sel.size(); ++k) {
+      wg_tunn *T = peer[q.sel[k]];
+      const uint32_t ring = (uint32_t)(T->current % WG_N_SESSIONS);
+      q.ctr[k] = T->sessions[ring].sending_counter++;
+      q.slot[k] = T->first_slot + 2 * ring + 1;
+    }
+  }
+  // the sending counter and key slot of selected packet k
+  auto ctr_of = [&](size_t k) -> uint64_t { return many ? t->sc->ctr[k] : ctr0 + k; };
+  auto slot_of = [&](size_t k) -> uint32_t { return many ? t->sc->slot[k] : slot; };
   pc.checks_done();
-  auto size = [&](size_t k) { return round128((uint64_t)src_len[t->sel[k]] + WG_DATA_OVERHEAD_SZ); };
+  auto size = [&](size_t k) { return round128((uint64_t)src_len[t->sc->sel[k]] + WG_DATA_OVERHEAD_SZ); };
   split(t, size);
   const bool nt = nt_copies();
   const int rc = for_engines(t, [&](Engine &E) -> int {
@@ -1990,7 +2280,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
     auto registered = [&](size_t a, size_t b) {  // srcs and dsts of [a, b)
       E.ddst.resize(b - E.k0);
       return all_packets(E, a, b, [&](size_t k, size_t &ha, size_t &hb) {
-        const uint32_t i = t->sel[k];
+        const uint32_t i = t->sc->sel[k];
         uint64_t unused;
         return dev_addr(E, src[i], src_len[i], unused, ha) &&
                dev_addr(E, dst[i], (uint64_t)src_len[i] + WG_DATA_OVERHEAD_SZ, E.ddst[k - E.k0], hb);
@@ -2014,18 +2304,19 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
           const uint64_t base = out_mode != 0 ? direct_base(
                                                     m, [&](size_t kk) { return E.ddst[j0 + kk]; },
                                                     [&](size_t kk) {
-                                                      return (uint64_t)src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
+                                                      return (uint64_t)src_len[t->sc->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
                                                     },
                                                     out_mode == 2 ? 0 : -1)
                                               : 0;
           E.pool->run(m, [&](size_t lo, size_t hi) {
             for (size_t kk = lo; kk < hi; ++kk) {
               const size_t k = ch.k0 + kk, j = j0 + kk;
-              const uint32_t i = t->sel[k];
+              const uint32_t i = t->sc->sel[k];
               if (base) {
-                E.b_desc[j] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.ddst[j] - base, ctr0 + k, src_len[i], slot};
+                E.b_desc[j] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.ddst[j] - base, ctr_of(k), src_len[i],
+                                             slot_of(k)};
               } else {
-                E.b_desc[j] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr0 + k, src_len[i], slot};
+                E.b_desc[j] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr_of(k), src_len[i], slot_of(k)};
                 E.b_jobs[j] = Scatter{E.ddst[j], (uint32_t)E.off[j], src_len[i] + WG_DATA_OVERHEAD_SZ, 0, 0};
               }
             }
@@ -2038,7 +2329,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
           E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
             uint64_t my_tx = 0;
             for (size_t kk = lo; kk < hi; ++kk) {
-              const uint32_t i = t->sel[ch.k0 + kk];
+              const uint32_t i = t->sc->sel[ch.k0 + kk];
               if (E.b_st[j0 + kk] != WG_STATUS_OK) {  // the GPU path has no other failure mode
                 set_err(res[i], WG_STATUS_CRYPTO_FAILED);
                 continue;
@@ -2055,17 +2346,17 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
         };
         auto more = [&]() -> int {
           if (!partial) return 1;
-          const size_t had = t->sel.size();
+          const size_t had = t->sc->sel.size();
           grow();
-          if (t->sel.size() == had) return 1;
-          if (!registered(had, t->sel.size())) return 2;
-          append_chunks(E, size, had, t->sel.size(), chunk_bytes());
-          E.k1 = t->sel.size();
+          if (t->sc->sel.size() == had) return 1;
+          if (!registered(had, t->sc->sel.size())) return 2;
+          append_chunks(E, size, had, t->sc->sel.size(), chunk_bytes());
+          E.k1 = t->sc->sel.size();
           return 0;
         };
         left = run_dma(
-            E, true, t_prep, n, [&](size_t k) { return src[t->sel[k]]; },
-            [&](size_t k) { return src_len[t->sel[k]]; }, fill, done, more,
+            E, true, t_prep, n, [&](size_t k) { return src[t->sc->sel[k]]; },
+            [&](size_t k) { return src_len[t->sc->sel[k]]; }, fill, done, more,
             [](size_t, Staging &, hipStream_t) { return -1; });
         if (left != 1 && left != 2) return left;
       }
@@ -2073,7 +2364,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
     if (left == 2) {  // the rest of the batch takes the paths below
       grow();
       E.k0 = E.k1;
-      E.k1 = t->sel.size();
+      E.k1 = t->sc->sel.size();
     } else {
       grow_all();
     }
@@ -2084,7 +2375,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
     E.dsrc.resize(E.k1 - E.k0);
     E.ddst.resize(E.k1 - E.k0);
     for (size_t k = E.k0; direct && k < E.k1; ++k) {
-      const uint32_t i = t->sel[k];
+      const uint32_t i = t->sc->sel[k];
       const size_t j = k - E.k0;
       direct = ((reinterpret_cast<uint64_t>(src[i]) | reinterpret_cast<uint64_t>(dst[i])) & 15u) == 0 &&
                dev_addr(E, src[i], src_len[i], E.dsrc[j]) &&
@@ -2095,12 +2386,12 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
       E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = k - E.k0;
-          const uint32_t i = t->sel[k];
+          const uint32_t i = t->sc->sel[k];
           if (direct) {
-            S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.ddst[j], ctr0 + k, src_len[i], slot};
+            S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.ddst[j], ctr_of(k), src_len[i], slot_of(k)};
           } else {
             copy_bytes(S.h_in + E.off[j] + WG_DATA_OFFSET, src[i], src_len[i], nt);  // NepTUN slot layout
-            S.h_desc[kk] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr0 + k, src_len[i], slot};
+            S.h_desc[kk] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr_of(k), src_len[i], slot_of(k)};
           }
         }
       });
@@ -2109,7 +2400,7 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
       const double a = now_us();
       E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
-          const uint32_t i = t->sel[ch.k0 + kk];
+          const uint32_t i = t->sc->sel[ch.k0 + kk];
           const uint32_t w = src_len[i] + WG_DATA_OVERHEAD_SZ;
           if (S.h_st[kk] != WG_STATUS_OK) {  // the GPU path has no other failure mode
             set_err(res[i], WG_STATUS_CRYPTO_FAILED);
@@ -2123,37 +2414,44 @@ int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
         }
       });
       for (size_t kk = 0; kk < ch.k1 - ch.k0; ++kk)  // mod.rs:321
-        if (S.h_st[kk] == WG_STATUS_OK) E.tx += src_len[t->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
+        if (S.h_st[kk] == WG_STATUS_OK) E.tx += src_len[t->sc->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
       E.ph.copy_out_us += now_us() - a;
     };
     return run_chunks(E, true, pack, unpack, direct, direct);
   });
   for (Engine *E : t->eng) t->tx_bytes += E->tx;
+  // a batch that failed while pass 1 still covered only its first part: the rest gets
+  // pass 1 now, so every packet's result is this call's (selected ones read as failed,
+  // their counters stay consumed like the rest of the failed batch's)
+  if (rc) grow();
+  if (many)  // tx_bytes of each packet's own Tunn (mod.rs:321)
+    for (uint32_t i = 0; i < n; ++i)
+      if (res[i].kind == WG_TUNN_WRITE_TO_NETWORK) peer[i]->tx_bytes += res[i].len;
   return rc;
 }
 
-int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
-                              const uint32_t *len, uint8_t *const *dst, const uint32_t *dst_cap,
-                              wg_tunn_result *res) {
-  if (!t || (n && (!datagram || !len || !dst || !dst_cap || !res)))
-    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decapsulate_batch: null", hipSuccess);
-  if (n == 0) return WG_RC_OK;
+// n x Tunn::decapsulate; t and peer as in encap_impl, peers: the distinct Tunns of a
+// multi-peer batch
+static int decap_impl(wg_tunn *t, wg_tunn *const *peer, const std::vector<wg_tunn *> *peers, uint32_t n,
+                      const uint8_t *const *datagram, const uint32_t *len, uint8_t *const *dst,
+                      const uint32_t *dst_cap, wg_tunn_result *res) {
   PhaseCall pc(t, n);
+  const bool many = peer != nullptr;
   // pass 1 (stateless checks, reference order; on the pool): parse, session, dst
   // size, index -- and each datagram's counter, so the in-order pass never reads
   // the datagrams again.  Over packets [lo, hi), appending to the selection.
-  t->code.resize(n);
-  t->ctr_all.resize(n);
-  t->sel.clear();
-  t->slot.clear();
-  t->ctr.clear();
+  t->sc->code.resize(n);
+  t->sc->ctr_all.resize(n);
+  t->sc->sel.clear();
+  t->sc->slot.clear();
+  t->sc->ctr.clear();
   auto pass1 = [&](size_t lo0, size_t hi0) {
     t->eng[0]->pool->run(hi0 - lo0, [&](size_t lo, size_t hi) {
       for (size_t i = lo0 + lo; i < lo0 + hi; ++i) {
         const uint8_t *d = datagram[i];
         const uint32_t L = len[i];
         std::memset(&res[i], 0, sizeof res[i]);
-        t->code[i] = -1;
+        t->sc->code[i] = -1;
         if (L == 0) {  // "repeated call": send_queued_packet is the CPU Tunn's business
           res[i].kind = WG_TUNN_NOT_DATA;
           continue;
@@ -2165,7 +2463,8 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
           continue;
         }
         const uint32_t ridx = ld32(d + 4);
-        const Session &s = t->sessions[ridx % WG_N_SESSIONS];
+        const wg_tunn *T = many ? peer[i] : t;  // (the packet's Tunn)
+        const Session &s = T->sessions[ridx % WG_N_SESSIONS];
         int32_t e = WG_STATUS_OK;
         if (!s.live) e = WG_STATUS_NO_CURRENT_SESSION;                                 // mod.rs:553-556
         else if ((uint64_t)dst_cap[i] < L - WG_DATA_OFFSET) e = WG_STATUS_DESTINATION_BUFFER_TOO_SMALL;  // session.rs:271
@@ -2173,29 +2472,29 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
         if (e) { set_err(res[i], e); continue; }
         // until its chunk returns a selected packet reads as failed
         set_err(res[i], WG_STATUS_CRYPTO_FAILED);
-        t->code[i] = (int32_t)(t->first_slot + 2 * (ridx % WG_N_SESSIONS));
-        t->ctr_all[i] = ld64(d + 8);
+        t->sc->code[i] = (int32_t)(T->first_slot + 2 * (ridx % WG_N_SESSIONS));
+        t->sc->ctr_all[i] = ld64(d + 8);
       }
     });
-    const size_t had = t->sel.size();
-    t->sel.resize(had + (hi0 - lo0));
-    t->slot.resize(t->sel.size());
-    t->ctr.resize(t->sel.size());
+    const size_t had = t->sc->sel.size();
+    t->sc->sel.resize(had + (hi0 - lo0));
+    t->sc->slot.resize(t->sc->sel.size());
+    t->sc->ctr.resize(t->sc->sel.size());
     const size_t got = compact(
-        *t->eng[0]->pool, hi0 - lo0, [&](size_t j) { return t->code[lo0 + j] >= 0; },
+        *t->eng[0]->pool, hi0 - lo0, [&](size_t j) { return t->sc->code[lo0 + j] >= 0; },
         [&](size_t o, size_t j) {
           const size_t i = lo0 + j;
-          t->sel[had + o] = (uint32_t)i;
-          t->slot[had + o] = (uint32_t)t->code[i];
-          t->ctr[had + o] = t->ctr_all[i];
+          t->sc->sel[had + o] = (uint32_t)i;
+          t->sc->slot[had + o] = (uint32_t)t->sc->code[i];
+          t->sc->ctr[had + o] = t->sc->ctr_all[i];
         });
-    t->sel.resize(had + got);
-    t->slot.resize(had + got);
-    t->ctr.resize(had + got);
+    t->sc->sel.resize(had + got);
+    t->sc->slot.resize(had + got);
+    t->sc->ctr.resize(had + got);
   };
   // a large batch checks its first sixteenth first: a registered DMA batch puts that
   // part's first chunk on the device while pass 1 covers the rest (open_selected)
-  const size_t n0 = n >= 16384 && dma_runs() && t->eng.size() == 1 ? n / 16 : n;
+  const size_t n0 = n >= 16384 && dma_runs() && t->eng.size() == 1 && !many ? n / 16 : n;
   pass1(0, n0);
   bool grown = n0 == n;
   auto grow = [&]() {
@@ -2205,40 +2504,133 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
     pass1(n0, n);
     t->ph.checks_us += now_us() - a;
   };
-  if (t->sel.empty()) grow();
+  if (t->sc->sel.empty()) grow();
   pc.checks_done();
-  if (t->sel.empty()) return WG_RC_OK;
-  for (int r = 0; r < WG_N_SESSIONS; ++r) t->spec_window[r] = t->sessions[r].window;
+  if (t->sc->sel.empty()) return WG_RC_OK;
+  if (!many)
+    for (int r = 0; r < WG_N_SESSIONS; ++r) t->spec_window[r] = t->sessions[r].window;
+  else
+    for (wg_tunn *T : *peers)
+      for (int r = 0; r < WG_N_SESSIONS; ++r) T->spec_window[r] = T->sessions[r].window;
   // pass 2 (sequential, packet order, per chunk as it returns): replay window,
   // stats; validation and the byte copies follow on the pools
-  return open_selected(
+  const int rc = open_selected(
       t, datagram, len, dst,
       [&](size_t k, int32_t g_st) -> uint8_t {
-        const uint32_t i = t->sel[k];
-        const uint64_t ctr = t->ctr[k];
-        const uint32_t ring = (t->slot[k] - t->first_slot) / 2;
-        Session &s = t->sessions[ring];
+        const uint32_t i = t->sc->sel[k];
+        wg_tunn *T = many ? peer[i] : t;
+        const uint64_t ctr = t->sc->ctr[k];
+        const uint32_t ring = (t->sc->slot[k] - T->first_slot) / 2;
+        Session &s = T->sessions[ring];
         int32_t e = wg_replay_will_accept(&s.window, ctr);  // session.rs:279
         if (e) { set_err(res[i], e); return 0; }
         if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }
         e = wg_replay_mark_did_receive(&s.window, ctr);  // session.rs:300, :192-199
         if (e) { set_err(res[i], e); return 1; }
         s.window.receive_cnt += 1;
-        set_current_session(t, s.receiving_index);  // mod.rs:562 (pass 1: ridx == receiving_index)
+        set_current_session(T, s.receiving_index);  // mod.rs:562 (pass 1: ridx == receiving_index)
         return 1 | kFinish;
       },
       [&](size_t k, const uint8_t *pt, uint32_t P) -> uint64_t {
-        wg_tunn_result &r = res[t->sel[k]];
+        wg_tunn_result &r = res[t->sc->sel[k]];
         std::memset(&r, 0, sizeof r);
         return validate(pt, P, r);
       },
       [&](size_t k) -> bool {  // the same decision with every tag assumed good
-        wg_replay &w = t->spec_window[(t->slot[k] - t->first_slot) / 2];
-        if (wg_replay_will_accept(&w, t->ctr[k])) return false;
-        (void)wg_replay_mark_did_receive(&w, t->ctr[k]);
+        wg_tunn *T = many ? peer[t->sc->sel[k]] : t;
+        wg_replay &w = T->spec_window[(t->sc->slot[k] - T->first_slot) / 2];
+        if (wg_replay_will_accept(&w, t->sc->ctr[k])) return false;
+        (void)wg_replay_mark_did_receive(&w, t->sc->ctr[k]);
         return true;
       },
       grow, !grown, n);
+  // failed while pass 1 covered only the batch's first part: the rest gets its pass-1
+  // results now (selected packets read as failed), none from an earlier call
+  if (rc) grow();
+  if (many)  // rx_bytes of each packet's own Tunn: validate()'s share (mod.rs:606-670)
+    for (uint32_t i = 0; i < n; ++i) {
+      const wg_tunn_result &r = res[i];
+      if (r.kind == WG_TUNN_DONE) peer[i]->rx_bytes += WG_DATA_OVERHEAD_SZ;
+      else if (r.kind == WG_TUNN_WRITE_TO_TUNNEL) peer[i]->rx_bytes += (uint64_t)r.len + WG_DATA_OVERHEAD_SZ;
+    }
+  return rc;
+}
+
+int wg_tunn_encapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *src,
+                              const uint32_t *src_len, uint8_t *const *dst,
+                              const uint32_t *dst_cap, wg_tunn_result *res) {
+  if (!t || (n && (!src || !src_len || !dst || !dst_cap || !res)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "encapsulate_batch: null", hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  std::lock_guard<std::mutex> lk(t->mu);
+  Lease lease(t);
+  if (lease.rc) return lease.rc;
+  return encap_impl(t, nullptr, n, src, src_len, dst, dst_cap, res);
+}
+
+int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
+                              const uint32_t *len, uint8_t *const *dst, const uint32_t *dst_cap,
+                              wg_tunn_result *res) {
+  if (!t || (n && (!datagram || !len || !dst || !dst_cap || !res)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decapsulate_batch: null", hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  std::lock_guard<std::mutex> lk(t->mu);
+  Lease lease(t);
+  if (lease.rc) return lease.rc;
+  return decap_impl(t, nullptr, nullptr, n, datagram, len, dst, dst_cap, res);
+}
+
+// A multi-peer call: the distinct Tunns locked in address order, one lane borrowed,
+// the lane's owner object as the batch owner
+struct MultiCall {
+  std::vector<wg_tunn *> peers;
+  std::vector<std::unique_lock<std::mutex>> locks;
+  Engine *lane = nullptr;
+  wg_tunn *owner = nullptr;
+  int rc = WG_RC_OK;
+  MultiCall(wg_engine *g, uint32_t n, wg_tunn *const *tunn) {
+    if (!collect_peers(g, n, tunn, peers)) {
+      rc = wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "multi batch: a Tunn is null or not on this engine", hipSuccess);
+      return;
+    }
+    locks.reserve(peers.size());
+    for (wg_tunn *p : peers) locks.emplace_back(p->mu);
+    if ((rc = lane_acquire(g, &lane)) != WG_RC_OK) return;
+    if (!lane->owner) lane->owner = new (std::nothrow) wg_tunn;
+    if (!lane->owner) {
+      lane_release(g, lane);
+      lane = nullptr;
+      rc = wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "multi batch: host alloc", hipSuccess);
+      return;
+    }
+    owner = lane->owner;
+    owner->group = g;
+  }
+  ~MultiCall() {}  // (the lease below returns the lane; the locks go last)
+};
+
+int wg_tunn_encapsulate_multi(wg_engine *e, uint32_t n, wg_tunn *const *tunn,
+                              const uint8_t *const *src, const uint32_t *src_len,
+                              uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res) {
+  if (!e || (n && (!tunn || !src || !src_len || !dst || !dst_cap || !res)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "encapsulate_multi: null", hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  MultiCall mc(e, n, tunn);
+  if (mc.rc) return mc.rc;
+  Lease lease(mc.owner, mc.lane);
+  return encap_impl(mc.owner, tunn, n, src, src_len, dst, dst_cap, res);
+}
+
+int wg_tunn_decapsulate_multi(wg_engine *e, uint32_t n, wg_tunn *const *tunn,
+                              const uint8_t *const *datagram, const uint32_t *len,
+                              uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res) {
+  if (!e || (n && (!tunn || !datagram || !len || !dst || !dst_cap || !res)))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decapsulate_multi: null", hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  MultiCall mc(e, n, tunn);
+  if (mc.rc) return mc.rc;
+  Lease lease(mc.owner, mc.lane);
+  return decap_impl(mc.owner, tunn, &mc.peers, n, datagram, len, dst, dst_cap, res);
 }
 
 int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,
@@ -2247,9 +2639,12 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
   if (!t || (n && (!datagram || !len || !dst || !dst_cap || !res)))
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decrypt_batch: null", hipSuccess);
   if (n == 0) return WG_RC_OK;
+  std::lock_guard<std::mutex> lk(t->mu);
+  Lease lease(t);
+  if (lease.rc) return lease.rc;
   PhaseCall pc(t, n);
-  t->sel.clear();
-  t->slot.clear();
+  t->sc->sel.clear();
+  t->sc->slot.clear();
   for (uint32_t i = 0; i < n; ++i) {
     const uint8_t *d = datagram[i];
     const uint32_t L = len[i];
@@ -2271,21 +2666,21 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
     // receiving key if the index is ours, else the sending key (session.rs:327-333); the
     // sending slot's key_index is the peer's index, which is what this header carries
     const bool ours = t->sessions[ring].receiving_index == ridx;
-    t->sel.push_back(i);
-    t->slot.push_back(t->first_slot + 2 * (uint32_t)ring + (ours ? 0u : 1u));
+    t->sc->sel.push_back(i);
+    t->sc->slot.push_back(t->first_slot + 2 * (uint32_t)ring + (ours ? 0u : 1u));
   }
-  if (t->sel.empty()) return WG_RC_OK;
-  for (uint32_t i : t->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);  // until its chunk returns
+  if (t->sc->sel.empty()) return WG_RC_OK;
+  for (uint32_t i : t->sc->sel) set_err(res[i], WG_STATUS_CRYPTO_FAILED);  // until its chunk returns
   pc.checks_done();
   return open_selected(
       t, datagram, len, dst,
       [&](size_t k, int32_t g_st) -> uint8_t {
-        const uint32_t i = t->sel[k];
+        const uint32_t i = t->sc->sel[k];
         if (g_st != WG_STATUS_OK) { set_err(res[i], g_st); return 2; }
         return 1 | kFinish;
       },
       [&](size_t k, const uint8_t *pt, uint32_t P) -> uint64_t {
-        wg_tunn_result &r = res[t->sel[k]];
+        wg_tunn_result &r = res[t->sc->sel[k]];
         std::memset(&r, 0, sizeof r);
         const uint64_t rx = validate(pt, P, r);
         if (r.kind == WG_TUNN_DONE) set_err(r, WG_STATUS_UNEXPECTED_PACKET);  // mod.rs:412
@@ -2297,32 +2692,26 @@ int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram
 
 int wg_tunn_get_phases(const wg_tunn *t, wg_tunn_phases *out) {
   if (!t || !out) return WG_RC_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(t->mu);
   *out = t->ph;
-  for (const Engine *E : t->eng) {
-    const wg_tunn_phases &p = E->ph;
-    out->chunks += p.chunks;
-    out->pack_us += p.pack_us;
-    out->submit_us += p.submit_us;
-    out->wait_us += p.wait_us;
-    out->copy_out_us += p.copy_out_us;
-    out->dev_h2d_us += p.dev_h2d_us;
-    out->dev_kernel_us += p.dev_kernel_us;
-    out->dev_d2h_us += p.dev_d2h_us;
-    out->pack_spec_us += p.pack_spec_us;
-    out->prep_us += p.prep_us;
-  }
+  add_lane_phases(*out, t->ph_lanes);
+  for (const Engine *E : t->eng) add_lane_phases(*out, E->ph);
   return WG_RC_OK;
 }
 
 int wg_tunn_reset_phases(wg_tunn *t) {
   if (!t) return WG_RC_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(t->mu);
   t->ph = wg_tunn_phases{};
+  t->ph_lanes = wg_tunn_phases{};
   for (Engine *E : t->eng) E->ph = wg_tunn_phases{};
   return WG_RC_OK;
 }
 
 int wg_tunn_set_phase_timing(wg_tunn *t, int on) {
   if (!t) return WG_RC_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(t->mu);
+  t->timing = on != 0;
   for (Engine *E : t->eng) E->timing = on != 0;
   return WG_RC_OK;
 }

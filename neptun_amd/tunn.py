@@ -44,6 +44,12 @@ class Phases(ctypes.Structure):
                 for f, _ in self._fields_}
 
 
+class EngineInfo(ctypes.Structure):
+    """wg_engine_info: what a shared engine holds."""
+    _fields_ = [(f, ctypes.c_uint32) for f in ("tunns", "lanes", "max_lanes", "pool_threads", "streams",
+                                               "pad")]
+
+
 def _bind(L):
     if getattr(L, "_tunn_bound", False):
         return L
@@ -68,6 +74,14 @@ def _bind(L):
     L.wg_tunn_set_phase_timing.argtypes = [vp, c.c_int]
     for fn in (L.wg_tunn_encapsulate_batch, L.wg_tunn_decapsulate_batch, L.wg_tunn_decrypt_batch):
         fn.argtypes = [vp, u32, vp, vp, vp, vp, c.POINTER(TunnResult)]
+    L.wg_engine_create.argtypes = [vp, c.POINTER(vp)]
+    L.wg_engine_destroy.argtypes = [vp]
+    L.wg_engine_get_info.argtypes = [vp, c.POINTER(EngineInfo)]
+    L.wg_tunn_create_on.argtypes = [vp, u32, c.POINTER(vp)]
+    L.wg_tunn_engine.argtypes = [vp]
+    L.wg_tunn_engine.restype = vp
+    for fn in (L.wg_tunn_encapsulate_multi, L.wg_tunn_decapsulate_multi):
+        fn.argtypes = [vp, u32, vp, vp, vp, vp, vp, c.POINTER(TunnResult)]
     L._tunn_bound = True
     return L
 
@@ -87,17 +101,95 @@ class ReplayWindow:
         return self._lib.wg_replay_mark_did_receive(ctypes.byref(self.w), counter)
 
 
+def _packet_arrays(blobs, dsts):
+    """ctypes pointer / length arrays over Python byte strings and bytearrays (kept alive)."""
+    n = len(blobs)
+    keep = [ctypes.create_string_buffer(bytes(s), max(len(s), 1)) for s in blobs]
+    src_ptr = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in keep])
+    src_len = (ctypes.c_uint32 * n)(*[len(s) for s in blobs])
+    dbufs = [(ctypes.c_uint8 * max(len(d), 1)).from_buffer(d) if len(d) else
+             (ctypes.c_uint8 * 1)() for d in dsts]
+    dst_ptr = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in dbufs])
+    dst_cap = (ctypes.c_uint32 * n)(*[len(d) for d in dsts])
+    return (keep, dbufs), src_ptr, src_len, dst_ptr, dst_cap
+
+
+def _results(res):
+    return [(r.kind, r.status, r.len, r.ip_version, bytes(r.src_ip)) for r in res]
+
+
+class Engine:
+    """wg_engine: a per-GPU engine (host pool, lanes of streams and staging) that any
+    number of Tunns share; multi-peer batches mix packets of its Tunns."""
+
+    def __init__(self, ctx):
+        self._lib = _bind(ctx._lib)
+        self._ctx = ctx
+        h = ctypes.c_void_p()
+        check(self._lib.wg_engine_create(ctx._h, ctypes.byref(h)), "wg_engine_create")
+        self._h = h
+
+    def tunn(self, first_slot: int = 0) -> "Tunn":
+        return Tunn(self._ctx, first_slot, engine=self)
+
+    def info(self) -> dict:
+        i = EngineInfo()
+        check(self._lib.wg_engine_get_info(self._h, ctypes.byref(i)), "wg_engine_get_info")
+        return {f: getattr(i, f) for f, _ in EngineInfo._fields_ if f != "pad"}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            check(self._lib.wg_engine_destroy(self._h), "wg_engine_destroy")
+            self._h = None
+
+    def _multi(self, fn, name, tunns, blobs, dsts):
+        n = len(blobs)
+        keep, sp, sl, dp, dc = _packet_arrays(blobs, dsts)
+        th = (ctypes.c_void_p * n)(*[t._h.value for t in tunns])
+        res = (TunnResult * n)()
+        check(fn(self._h, n, th, sp, sl, dp, dc, res), name)
+        return _results(res)
+
+    def encapsulate_multi(self, tunns, srcs, dsts):
+        """packet i through tunns[i] (wg_tunn_encapsulate_multi)."""
+        return self._multi(self._lib.wg_tunn_encapsulate_multi, "wg_tunn_encapsulate_multi", tunns, srcs, dsts)
+
+    def decapsulate_multi(self, tunns, datagrams, dsts):
+        return self._multi(self._lib.wg_tunn_decapsulate_multi, "wg_tunn_decapsulate_multi", tunns, datagrams,
+                           dsts)
+
+    def _multi_ptrs(self, fn, name, tunn_ptrs, src_ptrs, src_lens, dst_ptrs, dst_caps):
+        n = len(src_ptrs)
+        res = (TunnResult * n)()
+        vp = ctypes.c_void_p
+        check(fn(self._h, n, vp(tunn_ptrs.ctypes.data), vp(src_ptrs.ctypes.data), vp(src_lens.ctypes.data),
+                 vp(dst_ptrs.ctypes.data), vp(dst_caps.ctypes.data), res), name)
+        return _results(res)
+
+    def encapsulate_multi_ptrs(self, tunn_ptrs, src_ptrs, src_lens, dst_ptrs, dst_caps):
+        """over raw addresses: tunn_ptrs / src_ptrs / dst_ptrs numpy uint64, lens / caps uint32"""
+        return self._multi_ptrs(self._lib.wg_tunn_encapsulate_multi, "wg_tunn_encapsulate_multi", tunn_ptrs,
+                                src_ptrs, src_lens, dst_ptrs, dst_caps)
+
+    def decapsulate_multi_ptrs(self, tunn_ptrs, src_ptrs, src_lens, dst_ptrs, dst_caps):
+        return self._multi_ptrs(self._lib.wg_tunn_decapsulate_multi, "wg_tunn_decapsulate_multi", tunn_ptrs,
+                                src_ptrs, src_lens, dst_ptrs, dst_caps)
+
+
 class Tunn:
     """Tunn mirror bound to a GpuContext; uses 16 key slots from `first_slot`."""
 
-    def __init__(self, ctx, first_slot: int = 0):
-        """ctx: one GpuContext, or a list of them (wg_tunn_create_multi: batches are
-        split across the contexts' GPUs)."""
+    def __init__(self, ctx, first_slot: int = 0, engine: Engine | None = None):
+        """ctx: one GpuContext (the Tunn attaches to its default engine, or to `engine`),
+        or a list of them (wg_tunn_create_multi: batches are split across the contexts' GPUs)."""
         ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx]
         self._lib = _bind(ctxs[0]._lib)
         self._ctx = ctxs
+        self._engine = engine  # (kept alive while the Tunn is)
         h = ctypes.c_void_p()
-        if len(ctxs) == 1:
+        if engine is not None:
+            check(self._lib.wg_tunn_create_on(engine._h, first_slot, ctypes.byref(h)), "wg_tunn_create_on")
+        elif len(ctxs) == 1:
             check(self._lib.wg_tunn_create(ctxs[0]._h, first_slot, ctypes.byref(h)), "wg_tunn_create")
         else:
             arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value if isinstance(c._h, ctypes.c_void_p) else c._h
@@ -182,16 +274,10 @@ class Tunn:
 
     def _batch(self, fn, name, srcs, dsts):
         n = len(srcs)
-        keep = [ctypes.create_string_buffer(bytes(s), max(len(s), 1)) for s in srcs]
-        src_ptr = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in keep])
-        src_len = (ctypes.c_uint32 * n)(*[len(s) for s in srcs])
-        dbufs = [(ctypes.c_uint8 * max(len(d), 1)).from_buffer(d) if len(d) else
-                 (ctypes.c_uint8 * 1)() for d in dsts]
-        dst_ptr = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in dbufs])
-        dst_cap = (ctypes.c_uint32 * n)(*[len(d) for d in dsts])
+        keep, src_ptr, src_len, dst_ptr, dst_cap = _packet_arrays(srcs, dsts)
         res = (TunnResult * n)()
         check(fn(self._h, n, src_ptr, src_len, dst_ptr, dst_cap, res), name)
-        return [(r.kind, r.status, r.len, r.ip_version, bytes(r.src_ip)) for r in res]
+        return _results(res)
 
     def encapsulate_batch(self, srcs: list[bytes], dsts: list[bytearray]):
         return self._batch(self._lib.wg_tunn_encapsulate_batch, "wg_tunn_encapsulate_batch",

@@ -41,6 +41,27 @@ def test_tunn_entry_points_fail_loudly_on_null():
     assert b"tunn_create" in lib.wg_gpu_last_error()
 
 
+def test_engine_entry_points_fail_loudly_on_null():
+    """wg_engine_* / multi-peer batches refuse null arguments before touching a GPU."""
+    from neptun_amd.tunn import EngineInfo, TunnResult, _bind
+    lib = _bind(neptun_amd.load())
+    out = ctypes.c_void_p()
+    assert lib.wg_engine_create(None, ctypes.byref(out)) == -1
+    assert b"engine_create" in lib.wg_gpu_last_error()
+    assert lib.wg_tunn_create_on(None, 0, ctypes.byref(out)) == -1
+    assert lib.wg_engine_get_info(None, ctypes.byref(EngineInfo())) == -1
+    assert lib.wg_engine_destroy(None) == 0
+    assert lib.wg_tunn_engine(None) is None
+    res = (TunnResult * 1)()
+    for fn in (lib.wg_tunn_encapsulate_multi, lib.wg_tunn_decapsulate_multi):
+        assert fn(None, 1, None, None, None, None, None, res) == -1
+        assert b"_multi: null" in lib.wg_gpu_last_error()
+    text = open(neptun_amd.HEADER_PATH.replace("neptun_gpu.h", "neptun_tunn.h")).read()
+    body = re.search(r"typedef struct wg_engine_info \{(.*?)\}", text, re.S).group(1)
+    names = [n.strip() for decl in re.findall(r"uint32_t([^;]*);", body) for n in decl.split(",")]
+    assert names == [f for f, _ in EngineInfo._fields_] and ctypes.sizeof(EngineInfo) == 4 * len(names)
+
+
 def test_library_is_gfx950_code_object():
     data = open(neptun_amd.LIB_PATH, "rb").read()
     assert b"gfx950" in data

@@ -142,3 +142,47 @@ def test_chunked_whole_batch_check_finds_every_corruption():
         t_wire[int(starts[i]) + 4] ^= 1   # the receiver index
     r = seal_matches_oracle(t_src, t_wire, d, starts, end, keys, kidx, chunk_bytes=1 << 16)
     assert r["mismatches"] == 2 and r["bad"] == [5, last]
+
+
+def test_chunked_check_fails_when_the_oracle_writes_nothing(monkeypatch):
+    """The whole-batch check must not pass vacuously: an oracle that reports status 0
+    but writes no byte (or only part of a packet) leaves the sentinel behind, and every
+    packet it skipped is reported (the expected buffer used to start as
+    the GPU's own output)."""
+    import torch
+    import oracle_chunks
+    from tools import synth
+    rng = np.random.default_rng(9)
+    sizes = rng.choice([0, 5, 64, 1350], 400).astype(np.int64)
+    slot = (sizes + 32 + 127) // 128 * 128
+    starts = np.zeros(len(sizes), np.int64)
+    starts[1:] = np.cumsum(slot)[:-1]
+    end = int(slot.sum())
+    src = rng.integers(0, 256, end, dtype=np.uint8)
+    d = np.zeros(len(sizes), o.DESC_DTYPE)
+    d["src_off"], d["dst_off"], d["len"] = starts + 16, starts, sizes
+    keys = synth.keys(1, seed=4)
+    kidx = np.array([7], np.uint32)
+    wire = np.zeros(end, np.uint8)
+    assert (o.seal_batch(d, keys, kidx, src, wire) == 0).all()
+    t_src, t_wire = torch.from_numpy(src), torch.from_numpy(wire)
+    real = o.seal_batch
+
+    def lazy(descs, *a):  # status 0 for all, bytes for none
+        return np.zeros(len(descs), np.int32)
+
+    def partial(descs, k, ki, s, dst):  # every packet but its last byte
+        st = real(descs, k, ki, s, dst)
+        for j in range(len(descs)):
+            dst[int(descs["dst_off"][j]) + int(descs["len"][j]) + 31] ^= 0xFF
+        return st
+
+    monkeypatch.setattr(oracle_chunks.o, "seal_batch", lazy)
+    r = oracle_chunks.seal_matches_oracle(t_src, t_wire, d, starts, end, keys, kidx, chunk_bytes=1 << 15)
+    assert r["mismatches"] == len(sizes)
+    monkeypatch.setattr(oracle_chunks.o, "seal_batch", partial)
+    r = oracle_chunks.seal_matches_oracle(t_src, t_wire, d, starts, end, keys, kidx, chunk_bytes=1 << 15)
+    assert r["mismatches"] == len(sizes)
+    monkeypatch.setattr(oracle_chunks.o, "seal_batch", real)
+    r = oracle_chunks.seal_matches_oracle(t_src, t_wire, d, starts, end, keys, kidx, chunk_bytes=1 << 15)
+    assert r["mismatches"] == 0 and r["checked"] == len(sizes)
