@@ -93,6 +93,11 @@ template <bool kSeal> __global__ void aead_desc_affine_key1_kernel(DescParams pr
 #endif
 template <bool kSeal> __global__ void aead_desc_affine_kernel(DescParams prm);
 
+// Latency form (wg_xlane.hip): G lanes per packet for batches that fill a small
+// part of the chip; wg_gpu.cpp picks G from the batch size.
+constexpr uint32_t kXlaneThreads = 256;
+template <bool kSeal, uint32_t G> __global__ void aead_xlane_kernel(DescParams prm);
+
 // wg_plan.hip: counting sort of a descriptor batch by rounds (longest first)
 constexpr uint32_t kPlanBins = 256;   // rounds 0..254, 255+ share the top bin
 constexpr uint32_t kPlanTiles = 256;  // contiguous descriptor tiles, one block each

@@ -699,4 +699,87 @@ __device__ __forceinline__ void st16(uint8_t *p, uint32_t a, uint32_t b, uint32_
   *reinterpret_cast<uint4 *>(p) = make_uint4(a, b, c, d);
 }
 
+// ---------------------------------------------------------------------------
+// General multiply mod 2^130 - 5 for combining partial Poly1305 accumulators
+// (several lanes per packet, wg_xlane.hip): h = sum m_i r^(n - i + 1) splits into
+// spans, each span's Horner sum weighted by a power of r.  poly_block's radix
+// 2^32 form relies on a clamped r; powers of r are not clamped, so these use
+// radix 2^26 (poly1305-donna-32's multiply, valid for any operand whose limbs are
+// below ~2^27).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kM26 = 0x3ffffffu;
+
+struct F26 {
+  uint32_t v[5];
+};
+
+// radix 2^32 accumulator (h4 small) -> radix 2^26
+__device__ __forceinline__ F26 f26_from32(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3, uint32_t h4) {
+  F26 a;
+  a.v[0] = h0 & kM26;
+  a.v[1] = ((h0 >> 26) | (h1 << 6)) & kM26;
+  a.v[2] = ((h1 >> 20) | (h2 << 12)) & kM26;
+  a.v[3] = ((h2 >> 14) | (h3 << 18)) & kM26;
+  a.v[4] = (h3 >> 8) | (h4 << 24);
+  return a;
+}
+
+// a * b mod 2^130 - 5; result limbs < 2^26 (+ a small carry in limb 1)
+__device__ __forceinline__ F26 f26_mul(const F26 &a, const F26 &b) {
+  const uint32_t s1 = b.v[1] * 5u, s2 = b.v[2] * 5u, s3 = b.v[3] * 5u, s4 = b.v[4] * 5u;
+  const uint64_t a0 = a.v[0], a1 = a.v[1], a2 = a.v[2], a3 = a.v[3], a4 = a.v[4];
+  uint64_t d0 = a0 * b.v[0] + a1 * s4 + a2 * s3 + a3 * s2 + a4 * s1;
+  uint64_t d1 = a0 * b.v[1] + a1 * b.v[0] + a2 * s4 + a3 * s3 + a4 * s2;
+  uint64_t d2 = a0 * b.v[2] + a1 * b.v[1] + a2 * b.v[0] + a3 * s4 + a4 * s3;
+  uint64_t d3 = a0 * b.v[3] + a1 * b.v[2] + a2 * b.v[1] + a3 * b.v[0] + a4 * s4;
+  uint64_t d4 = a0 * b.v[4] + a1 * b.v[3] + a2 * b.v[2] + a3 * b.v[1] + a4 * b.v[0];
+  F26 r;
+  d1 += d0 >> 26;
+  r.v[0] = (uint32_t)d0 & kM26;
+  d2 += d1 >> 26;
+  r.v[1] = (uint32_t)d1 & kM26;
+  d3 += d2 >> 26;
+  r.v[2] = (uint32_t)d2 & kM26;
+  d4 += d3 >> 26;
+  r.v[3] = (uint32_t)d3 & kM26;
+  const uint64_t c = (d4 >> 26) * 5u + r.v[0];
+  r.v[4] = (uint32_t)d4 & kM26;
+  r.v[0] = (uint32_t)c & kM26;
+  r.v[1] += (uint32_t)(c >> 26);
+  return r;
+}
+
+__device__ __forceinline__ F26 f26_add(const F26 &a, const F26 &b) {
+  F26 r;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) r.v[q] = a.v[q] + b.v[q];
+  return r;
+}
+
+// r^e, e >= 1 (square and multiply, MSB first)
+__device__ __forceinline__ F26 f26_pow(const F26 &r, uint32_t e) {
+  F26 x = r;
+  for (int bit = 30 - __builtin_clz(e); bit >= 0; --bit) {
+    x = f26_mul(x, x);
+    if ((e >> bit) & 1u) x = f26_mul(x, r);
+  }
+  return x;
+}
+
+// radix 2^26 (limbs < 2^29) -> radix 2^32, the same value (no reduction): limb j
+// sits at bit 26 j, so each 32-bit word collects its limbs' shifted parts plus the
+// carry out of the word below; h4 < 2^5
+__device__ __forceinline__ void f26_to32(const F26 &a, uint32_t &h0, uint32_t &h1, uint32_t &h2, uint32_t &h3,
+                                         uint32_t &h4) {
+  uint64_t t = (uint64_t)a.v[0] + ((uint64_t)a.v[1] << 26);
+  h0 = (uint32_t)t;
+  t = (t >> 32) + ((uint64_t)a.v[2] << 20);
+  h1 = (uint32_t)t;
+  t = (t >> 32) + ((uint64_t)a.v[3] << 14);
+  h2 = (uint32_t)t;
+  t = (t >> 32) + ((uint64_t)a.v[4] << 8);
+  h3 = (uint32_t)t;
+  h4 = (uint32_t)(t >> 32);
+}
+
 }  // namespace wg

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -27,6 +28,7 @@ struct wg_gpu_ctx {
   uint32_t route_bits = 0;
   uint32_t cus = 0;                // compute units (persistent strided grid)
   bool pad_slots = false;          // wg_gpu_ctx_set_slot_padding
+  int64_t xlane_lanes = -1;        // wg_gpu_ctx_set_xlane_lanes (< 0: default)
   struct Range {
     uint64_t host, bytes, dev;
   };
@@ -187,6 +189,35 @@ static dim3 persistent_grid(const wg_gpu_ctx *ctx, uint32_t waves, uint32_t &spr
   return dim3(std::min((waves + per_block - 1u) / per_block, slots));
 }
 
+// Latency form (wg_xlane.hip): a batch that would fill only a small part of the
+// chip as one packet per lane runs G lanes per packet instead -- the largest G of
+// 64, 32, 16, 8 with n * G within a lane budget (wg_gpu_ctx_set_xlane_lanes, else
+// WG_XLANE_LANES, else cus * 512: two waves per SIMD).  0: the throughput forms.
+// (smallest group the selection takes: WG_XLANE_MIN_G, 2 .. 64, default 8)
+static uint32_t xlane_min_group() {
+  static const uint32_t g = [] {
+    const char *e = std::getenv("WG_XLANE_MIN_G");
+    const long v = e ? std::atol(e) : 8L;
+    uint32_t m = 2;
+    while (m < 64 && (long)m < v) m *= 2;
+    return m;
+  }();
+  return g;
+}
+
+static uint32_t xlane_group(const wg_gpu_ctx *ctx, uint32_t n) {
+  static const long long env = [] {
+    const char *e = std::getenv("WG_XLANE_LANES");
+    return e ? std::atoll(e) : -1LL;
+  }();
+  const uint64_t budget = ctx->xlane_lanes >= 0 ? (uint64_t)ctx->xlane_lanes
+                          : env >= 0            ? (uint64_t)env
+                                                : (uint64_t)ctx->cus * 512u;
+  for (uint32_t G = 64; G >= xlane_min_group(); G /= 2)
+    if ((uint64_t)n * G <= budget) return G;
+  return 0;
+}
+
 static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
                        const uint32_t *order, uint32_t n, const uint8_t *src, uint8_t *dst,
                        int32_t *status, void *stream) {
@@ -197,7 +228,20 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
   wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, order, src, dst, status, n,
                      ctx->key_slots, 0u};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (WG_DESC_SYNC && src && dst) {
+  if (const uint32_t G = xlane_group(ctx, n)) {
+    using K = void (*)(wg::DescParams);
+    static const K kernels[2][6] = {  // [seal][64, 32, 16, 8, 4, 2]
+        {wg::aead_xlane_kernel<false, 64>, wg::aead_xlane_kernel<false, 32>,
+         wg::aead_xlane_kernel<false, 16>, wg::aead_xlane_kernel<false, 8>,
+         wg::aead_xlane_kernel<false, 4>, wg::aead_xlane_kernel<false, 2>},
+        {wg::aead_xlane_kernel<true, 64>, wg::aead_xlane_kernel<true, 32>,
+         wg::aead_xlane_kernel<true, 16>, wg::aead_xlane_kernel<true, 8>,
+         wg::aead_xlane_kernel<true, 4>, wg::aead_xlane_kernel<true, 2>}};
+    const uint32_t form = 6u - (uint32_t)__builtin_ctz(G);  // 64 -> 0 ... 2 -> 5
+    const uint32_t per_block = wg::kXlaneThreads / G;
+    hipLaunchKernelGGL(kernels[seal ? 1 : 0][form], dim3((n + per_block - 1u) / per_block),
+                       dim3(wg::kXlaneThreads), 0, s, prm);
+  } else if (WG_DESC_SYNC && src && dst) {
     // phase-locked, persistent (wg_aead.hip aead_desc_sync_kernel); its compact
     // per-packet tables hold buffer-relative offsets, hence non-null bases
     const dim3 grid = persistent_grid(ctx, (n + 63u) / 64u, prm.spread);
@@ -355,6 +399,12 @@ int wg_gpu_open_strided(wg_gpu_ctx *ctx, uint32_t n, uint32_t len, uint32_t key_
 int wg_gpu_ctx_set_slot_padding(wg_gpu_ctx *ctx, int writable) {
   if (!ctx) return fail(WG_RC_INVALID_ARGUMENT, "set_slot_padding: null context");
   ctx->pad_slots = writable != 0;
+  return WG_RC_OK;
+}
+
+int wg_gpu_ctx_set_xlane_lanes(wg_gpu_ctx *ctx, int64_t lanes) {
+  if (!ctx) return fail(WG_RC_INVALID_ARGUMENT, "set_xlane_lanes: null context");
+  ctx->xlane_lanes = lanes < 0 ? -1 : lanes;
   return WG_RC_OK;
 }
 

@@ -1,0 +1,244 @@
+// wg_xlane.hip -- latency form of the descriptor batches: G lanes per packet.
+//
+// NepTUN hands the data plane batches of at most 50 packets
+// (/root/reference/neptun/src/device/packet_workers.rs:27,
+// MAX_INTERTHREAD_BATCHED_PKTS).  The throughput kernels (wg_aead.hip) run one
+// packet per lane, so such a batch is one or two waves whose lanes each walk their
+// packet's 23 ChaCha20 blocks and 85 Poly1305 blocks (1350 B) one after another
+// while the rest of the chip idles: ~70 us for 64 packets.  Here a packet is spread
+// over a group of G consecutive lanes of one wave (G = 64, 32, 16 or 8, chosen by
+// the host from the batch size, wg_gpu.cpp):
+//
+//   blocks   the packet's NB = 1 + ceil(P / 64) keystream blocks (block 0 = the
+//            Poly1305 key, RFC 8439 2.6) are dealt out in contiguous spans of
+//            C = ceil(NB / G) blocks, lane l taking [l C, l C + C); each lane loads
+//            its input pieces, XORs them with its keystream and stores the output;
+//   r        lane 0 of the group broadcasts r and s of block 0 (ds_bpermute);
+//   Horner   each lane absorbs its ciphertext pieces: h_l = sum m_i r^(k_l - i + 1)
+//            over its k_l pieces (lane 0's span starts with block 0, i.e. 4 empty
+//            slots in front, which Horner from h = 0 ignores);
+//   combine  every lane but the last holds S = 4 C slots, so with d = Lu - 2 - l
+//            (Lu lanes in use) T = sum_{l < Lu-1} h_l r^(S d) is a binary tree over
+//            the group with one power per level for all lanes (r^S, r^2S, r^4S, ...,
+//            by squaring); the last lane then forms D = T r^(c_last) + h_last, its
+//            c_last pieces following T's, then the length block and + s (the tag).
+//   open     the last lane compares the tag and broadcasts the verdict; on a
+//            mismatch every lane zeroes the plaintext it wrote (ring's open_within
+//            behaviour, as the throughput kernels do), status InvalidAeadTag.
+//
+// Per-packet checks, statuses and bytes written are those of aead_desc_kernel:
+// seal = Session::format_packet_data (session.rs:205-259), open =
+// parse_incoming_packet's DATA arm (noise/mod.rs:139-199) + receive_packet_data
+// without the replay window (session.rs:265-302).  The general multiply of the
+// combine step is radix 2^26 (wg_crypto.h f26_mul: powers of r are not clamped).
+#include <hip/hip_runtime.h>
+
+#include "wg_aead_kernels.h"
+#include "wg_crypto.h"
+
+namespace wg {
+namespace {
+
+// value of lane `src` (0 .. G-1) of this lane's group
+template <uint32_t G>
+__device__ __forceinline__ uint32_t gshfl(uint32_t x, uint32_t src) {
+  return (uint32_t)__shfl((int)x, (int)src, (int)G);
+}
+
+template <uint32_t G>
+__device__ __forceinline__ F26 gshfl26(const F26 &a, uint32_t src) {
+  F26 r;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) r.v[q] = gshfl<G>(a.v[q], src);
+  return r;
+}
+
+__device__ __forceinline__ F26 f26_zero() {
+  F26 z;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) z.v[q] = 0u;
+  return z;
+}
+
+}  // namespace
+
+template <bool kSeal, uint32_t G>
+__global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams prm) {
+  static_assert(G >= 2u && G <= 64u && (G & (G - 1u)) == 0u, "group = power of two within a wave");
+  const uint32_t gid = blockIdx.x * (kXlaneThreads / G) + threadIdx.x / G;  // packet (batch position)
+  const uint32_t l = threadIdx.x & (G - 1u);
+  if (gid >= prm.n) return;  // (the whole group)
+  const uint32_t idx = prm.order ? prm.order[gid] : gid;
+  const wg_packet_desc d = prm.descs[idx];
+  // (null bases: the offsets are absolute device addresses)
+  const uint8_t *src = reinterpret_cast<const uint8_t *>(reinterpret_cast<uint64_t>(prm.src) + d.src_off);
+  uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uint64_t>(prm.dst) + d.dst_off);
+
+  int32_t status = WG_STATUS_OK;
+  if (!kSeal && d.key_slot == WG_KEY_SLOT_INVALID_PACKET) status = WG_STATUS_INVALID_PACKET;
+  else if (!kSeal && d.key_slot == WG_KEY_SLOT_NO_SESSION) status = WG_STATUS_NO_CURRENT_SESSION;
+  else if (d.key_slot >= prm.key_slots) status = WG_STATUS_BAD_KEY_SLOT;
+  else if (((d.src_off | d.dst_off) & 15u) != 0u) status = WG_STATUS_MISALIGNED;
+  else if (!kSeal && d.len < WG_DATA_OVERHEAD_SZ) status = WG_STATUS_INVALID_PACKET;  // mod.rs:170
+
+  uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t sidx = 0, n1 = 0, n2 = 0;
+  if (status == WG_STATUS_OK) {
+    const uint4 a = ld16(prm.keys + 32u * d.key_slot), b = ld16(prm.keys + 32u * d.key_slot + 16u);
+    key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
+    key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
+    sidx = prm.key_index[d.key_slot];
+    if (kSeal) {
+      n1 = (uint32_t)d.counter;
+      n2 = (uint32_t)(d.counter >> 32);
+    } else {
+      const uint4 h = ld16(src);  // header: type, receiver_idx, counter (mod.rs:170-180)
+      if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
+      else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
+      n1 = h.z;
+      n2 = h.w;
+    }
+  }
+  if (status != WG_STATUS_OK) {  // group-uniform: nothing of the packet is written
+    if (l == 0u) prm.status[idx] = status;
+    return;
+  }
+
+  const uint32_t P = kSeal ? d.len : d.len - WG_DATA_OVERHEAD_SZ;
+  const uint8_t *in = kSeal ? src : src + WG_DATA_OFFSET;  // plaintext / ciphertext
+  uint8_t *out = kSeal ? dst + WG_DATA_OFFSET : dst;      // ciphertext / plaintext
+  const uint32_t NB = 1u + (P + 63u) / 64u;
+  const uint32_t C = (NB + G - 1u) / G;
+  const uint32_t Lu = (NB + C - 1u) / C;  // lanes in use; lane Lu - 1 holds block NB - 1
+  const uint32_t b0 = l * C, b1 = min(b0 + C, NB);
+
+  Poly ps;
+  uint32_t kpieces = 0;  // pieces this lane absorbed
+  // one data block b >= 1: XOR, store, and (once r is known) absorb its pieces
+  auto data_block = [&](uint32_t b, const uint32_t (&ks)[16], const uint4 (&x)[4]) {
+    const uint32_t off = 64u * (b - 1u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t o = off + 16u * (uint32_t)q;
+      if (o >= P) break;
+      const uint32_t valid = min(16u, P - o);
+      uint32_t w[4] = {x[q].x ^ ks[4 * q], x[q].y ^ ks[4 * q + 1], x[q].z ^ ks[4 * q + 2], x[q].w ^ ks[4 * q + 3]};
+      uint32_t c[4] = {kSeal ? w[0] : x[q].x, kSeal ? w[1] : x[q].y, kSeal ? w[2] : x[q].z, kSeal ? w[3] : x[q].w};
+      if (valid < 16u) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          w[j] &= byte_mask((int)valid, j);
+          c[j] &= byte_mask((int)valid, j);
+        }
+        store_partial(out + o, w, (int)valid);
+      } else {
+        st16(out + o, w[0], w[1], w[2], w[3]);
+      }
+      poly_block(ps, c[0], c[1], c[2], c[3]);
+      ++kpieces;
+    }
+  };
+  auto load_block = [&](uint32_t b, uint4 (&x)[4]) {
+    const uint32_t off = 64u * (b - 1u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      x[q] = (b >= 1u && off + 16u * (uint32_t)q < P) ? ld16(in + off + 16u * (uint32_t)q) : make_uint4(0, 0, 0, 0);
+  };
+
+  // first block of the span (lane 0: block 0, the one-time key)
+  uint32_t ks[16];
+  uint4 x[4];
+  const bool any = b0 < NB;
+  if (any) {
+    load_block(b0, x);
+    chacha20_block(ks, key, b0, n1, n2);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ks[j] = 0u;
+  }
+  uint32_t rk[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rk[j] = gshfl<G>(ks[j], 0u);
+  poly_init(ps, rk);
+  if (any && b0 >= 1u) data_block(b0, ks, x);
+  for (uint32_t b = b0 + 1u; b < b1; ++b) {
+    load_block(b, x);
+    chacha20_block(ks, key, b, n1, n2);
+    data_block(b, ks, x);
+  }
+
+  // combine: T = sum_{l < Lu-1} h_l r^(S (Lu - 2 - l)) in lane Lu - 2, by levels
+  const F26 r26 = f26_from32(ps.r0, ps.r1, ps.r2, ps.r3, 0u);
+  F26 v = l + 1u < Lu ? f26_from32(ps.h0, ps.h1, ps.h2, ps.h3, ps.h4) : f26_zero();
+  if (Lu > 2u) {
+    F26 R = f26_pow(r26, 4u * C);
+    const int dd = (int)Lu - 2 - (int)l;
+    for (uint32_t k = 0; (1u << k) < Lu - 1u; ++k) {
+      const uint32_t step = 1u << k;
+      const F26 pv = gshfl26<G>(v, l >= step ? l - step : 0u);  // node d + 2^k
+      if (dd >= 0 && ((uint32_t)dd & (2u * step - 1u)) == 0u && (uint32_t)dd + step <= Lu - 2u)
+        v = f26_add(v, f26_mul(pv, R));
+      if ((2u << k) < Lu - 1u) R = f26_mul(R, R);
+    }
+  }
+  const F26 T = gshfl26<G>(v, Lu >= 2u ? Lu - 2u : 0u);
+  uint32_t bad = 0u;
+  if (l == Lu - 1u) {
+    if (Lu >= 2u) {  // D = T r^(c_last) + h_last
+      const F26 D = f26_add(f26_mul(T, f26_pow(r26, kpieces)),
+                            f26_from32(ps.h0, ps.h1, ps.h2, ps.h3, ps.h4));
+      f26_to32(D, ps.h0, ps.h1, ps.h2, ps.h3, ps.h4);
+    }
+    poly_block(ps, 0u, 0u, P, 0u);  // le64(AAD len = 0) | le64(P)
+    const uint32_t s[4] = {rk[4], rk[5], rk[6], rk[7]};
+    uint32_t tag[4];
+    poly_finish(ps, s, tag);
+    if (kSeal) {
+      uint8_t *t = out + P;  // right after the ciphertext (session.rs:247-252)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t[q] = (uint8_t)(tag[q / 4] >> (8 * (q % 4)));
+    } else {
+      // received tag = bytes [P, P + 16) after the header: two aligned pieces
+      const uint32_t o = P & ~15u;
+      const uint4 ta = ld16(in + o);
+      const uint4 tb = (P & 15u) ? ld16(in + o + 16u) : make_uint4(0, 0, 0, 0);
+      const uint32_t tw[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+      const int sh = (int)(P & 15u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bad |= bytes_at(tw, sh + 4 * j) ^ tag[j];
+    }
+  }
+  if (kSeal) {
+    if (l == 0u) st16(dst, WG_MSG_DATA, sidx, n1, n2);  // header (session.rs:224-229)
+  } else {
+    bad = gshfl<G>(bad, Lu - 1u);
+    if (bad) {
+      status = WG_STATUS_INVALID_AEAD_TAG;
+      // never leave unauthenticated plaintext behind: this lane's own stores land first
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t lo = b0 >= 1u ? 64u * (b0 - 1u) : 0u;
+      const uint32_t hi = b1 >= 1u ? min(64u * (b1 - 1u), P) : 0u;
+      const uint32_t zw[4] = {0, 0, 0, 0};
+      for (uint32_t o = lo; o < hi; o += 16u) {
+        if (o + 16u <= P) st16(out + o, 0u, 0u, 0u, 0u);
+        else store_partial(out + o, zw, (int)(P - o));
+      }
+    }
+  }
+  if (l == 0u) prm.status[idx] = status;
+}
+
+template __global__ void aead_xlane_kernel<true, 64>(DescParams);
+template __global__ void aead_xlane_kernel<false, 64>(DescParams);
+template __global__ void aead_xlane_kernel<true, 32>(DescParams);
+template __global__ void aead_xlane_kernel<false, 32>(DescParams);
+template __global__ void aead_xlane_kernel<true, 16>(DescParams);
+template __global__ void aead_xlane_kernel<false, 16>(DescParams);
+template __global__ void aead_xlane_kernel<true, 8>(DescParams);
+template __global__ void aead_xlane_kernel<false, 8>(DescParams);
+template __global__ void aead_xlane_kernel<true, 4>(DescParams);
+template __global__ void aead_xlane_kernel<false, 4>(DescParams);
+template __global__ void aead_xlane_kernel<true, 2>(DescParams);
+template __global__ void aead_xlane_kernel<false, 2>(DescParams);
+
+}  // namespace wg

@@ -255,6 +255,11 @@ class GpuContext:
         check(self._lib.wg_gpu_ctx_set_slot_padding(self._h, 1 if writable else 0),
               "wg_gpu_ctx_set_slot_padding")
 
+    def set_xlane_lanes(self, lanes: int) -> None:
+        """Latency form of the descriptor batches: n * G <= lanes runs G (64..8)
+        lanes per packet; 0 = off, < 0 = default."""
+        check(self._lib.wg_gpu_ctx_set_xlane_lanes(self._h, int(lanes)), "wg_gpu_ctx_set_xlane_lanes")
+
     def seal_strided(self, n: int, length: int, key_slot: int, counter_base: int, src,
                      src_stride: int, dst, dst_stride: int, status=None, stream=None) -> None:
         check(self._lib.wg_gpu_seal_strided(self._h, n, length, key_slot, counter_base, _ptr(src),

@@ -1,0 +1,206 @@
+"""Latency form of the descriptor batches (neptun_amd/csrc/wg_xlane.hip): G lanes
+per packet for small batches -- NepTUN's inter-thread batches hold at most 50
+packets (/root/reference/neptun/src/device/packet_workers.rs:27).
+
+Each group size G = 64, 32, 16, 8 is forced through wg_gpu_ctx_set_xlane_lanes
+(n * G lanes: the largest G that fits is exactly G) and compared bit for bit with
+the oracle (oracle/neptun_oracle.c, session.rs:205-302 + RFC 8439) on seal and
+open: batch sizes 1, 50, 64 and 1000, payloads 0-9000 bytes including every
+block / piece boundary shape, many keys, nonce counters across the 32-bit carry,
+and the open failure cases (tampered ciphertext or tag, wrong index, wrong type,
+short datagrams, no session) whose plaintext must come back zeroed.
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as o
+from tools import synth
+
+from test_gpu_parity import DESC, pack, run_desc
+
+pytestmark = pytest.mark.gpu
+
+EDGE = [0, 1, 15, 16, 17, 47, 48, 63, 64, 65, 111, 112, 127, 128, 129, 191, 192, 1350, 1420,
+        4031, 4032, 4033, 8192, 9000]
+
+
+def make_batch(rng, n, n_keys):
+    sizes = rng.integers(0, 9001, n)
+    sizes[: min(len(EDGE), n)] = EDGE[: min(len(EDGE), n)]
+    rng.shuffle(sizes)
+    keys = rng.integers(0, 256, (n_keys, 32), dtype=np.uint8)
+    kidx = rng.integers(0, 2**32, n_keys, dtype=np.uint64).astype(np.uint32)
+    payloads = synth.host_payloads(sizes, seed=int(rng.integers(1 << 30)))
+    ctrs = rng.integers(0, 2**63, n, dtype=np.uint64) * 2 + rng.integers(0, 2, n, dtype=np.uint64)
+    ctrs[: min(4, n)] = [2**32 - 1, 0, 2**32, 2**64 - 1][: min(4, n)]
+    slots = rng.integers(0, n_keys, n).astype(np.uint32)
+    return sizes, keys, kidx, payloads, ctrs, slots
+
+
+def seal_descs(sizes, soffs, ctrs, slots, rng):
+    n = len(sizes)
+    perm = rng.permutation(n)
+    doffs = np.zeros(n, np.int64)
+    pos = 0
+    for i in perm:
+        doffs[i] = pos
+        pos = synth.round_up(pos + int(sizes[i]) + 32, 16)
+    d = np.zeros(n, DESC)
+    d["src_off"] = soffs
+    d["dst_off"] = doffs
+    d["counter"] = ctrs
+    d["len"] = sizes
+    d["key_slot"] = slots
+    return d, pos + 64
+
+
+@pytest.fixture
+def xl(gpu):
+    yield gpu
+    gpu.set_xlane_lanes(0)  # the session context's default for the other tests
+
+
+@pytest.mark.parametrize("G", [64, 32, 16, 8])
+@pytest.mark.parametrize("n", [1, 50, 64, 1000])
+def test_xlane_seal_open_match_oracle(torch_cuda, xl, G, n):
+    torch = torch_cuda
+    rng = np.random.default_rng(1000 * G + n)
+    sizes, keys, kidx, payloads, ctrs, slots = make_batch(rng, n, 64)
+    xl.set_keys(0, keys, kidx)
+    xl.set_xlane_lanes(n * G)
+    src, soffs = pack(payloads)
+    descs, dst_size = seal_descs(sizes, soffs, ctrs, slots, rng)
+    out, st = run_desc(torch, xl, True, descs, src, dst_size)
+    want = np.zeros(dst_size, np.uint8)
+    wst = o.seal_batch(descs, keys, kidx, src, want)
+    assert (wst == 0).all()
+    assert (st == wst).all(), st
+    assert np.array_equal(out, want), "sealed wire bytes differ from the oracle"
+    # open the oracle's datagrams back
+    d2 = np.zeros(n, DESC)
+    d2["src_off"] = descs["dst_off"]
+    d2["dst_off"] = soffs
+    d2["len"] = sizes + 32
+    d2["key_slot"] = slots
+    out2, st2 = run_desc(torch, xl, False, d2, want, len(src))
+    want2 = np.zeros(len(src), np.uint8)
+    wst2 = o.open_batch(d2, keys, kidx, want, want2)
+    assert (wst2 == 0).all() and (st2 == 0).all(), st2
+    assert np.array_equal(out2, want2)
+    assert np.array_equal(out2, src)
+
+
+@pytest.mark.parametrize("G", [64, 32, 8])
+def test_xlane_open_failures_zeroed_like_oracle(torch_cuda, xl, G):
+    """Every open failure: status as the oracle's, plaintext of a tag failure
+    zeroed, nothing written for the header / slot failures."""
+    torch = torch_cuda
+    rng = np.random.default_rng(G)
+    n = 200
+    sizes, keys, kidx, payloads, ctrs, slots = make_batch(rng, n, 16)
+    xl.set_keys(0, keys, kidx)
+    wires = [o.format_packet_data(keys[slots[i]].tobytes(), int(kidx[slots[i]]), int(ctrs[i]), payloads[i])
+             for i in range(n)]
+    wires = [bytearray(w) for w in wires]
+    slot_col = slots.copy()
+    for i in range(n):
+        case = i % 10
+        w = wires[i]
+        if case == 1 and len(w) > 32:
+            w[16 + int(rng.integers(len(w) - 32))] ^= 1 << int(rng.integers(8))  # ciphertext
+        elif case == 2:
+            w[len(w) - 1 - int(rng.integers(16))] ^= 0x80  # tag
+        elif case == 3:
+            w[4] ^= 1  # receiver index
+        elif case == 4:
+            w[0] = 1  # handshake type
+        elif case == 5:
+            wires[i] = w[: int(rng.integers(32))]  # too short for DATA
+        elif case == 6:
+            slot_col[i] = 0xFFFFFFFF  # no session
+        elif case == 7:
+            slot_col[i] = 0xFFFFFFFE  # parse failure upstream
+    wires = [bytes(w) for w in wires]
+    wsrc, woffs = pack(wires)
+    out_offs, pos = [], 0
+    for w in wires:
+        out_offs.append(pos)
+        pos = synth.round_up(pos + max(len(w) - 32, 0), 16) + 16
+    d = np.zeros(n, DESC)
+    d["src_off"] = woffs
+    d["dst_off"] = out_offs
+    d["len"] = [len(w) for w in wires]
+    d["key_slot"] = slot_col
+    xl.set_xlane_lanes(n * G)
+    d_descs = torch.from_numpy(d.view(np.uint8)).cuda()
+    d_src = torch.from_numpy(wsrc).cuda()
+    d_dst = torch.full((pos + 64,), 0xAA, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    xl.open_batch(d_descs, n, d_src, d_dst, d_st)
+    torch.cuda.synchronize()
+    st, out = d_st.cpu().numpy(), d_dst.cpu().numpy()
+    # the oracle takes the packets that reach a session; the two slot sentinels
+    # fail before anything is read (NoCurrentSession / InvalidPacket)
+    want = np.full(pos + 64, 0xAA, np.uint8)
+    real = slot_col < 0xFFFFFFFE
+    wst = np.full(n, -1, np.int32)
+    wst[~real] = np.where(slot_col[~real] == 0xFFFFFFFF, 14, 13)
+    wst[real] = o.open_batch(d[real], keys, kidx, wsrc, want)
+    assert (st == wst).all(), (st, wst)
+    assert set(np.unique(wst)) >= {0, 5, 10, 13, 14}
+    # the oracle zeroes a tag failure's plaintext and leaves the other failures' bytes
+    assert np.array_equal(out, want)
+    for i in np.nonzero(wst == 10)[0]:
+        p = len(wires[i]) - 32
+        assert not out[out_offs[i]:out_offs[i] + p].any()
+
+
+def test_xlane_in_place_and_absolute_addresses(torch_cuda, xl):
+    """In-place open (plaintext over the ciphertext) and null bases (descriptor
+    offsets = device addresses), as the throughput forms allow."""
+    torch = torch_cuda
+    rng = np.random.default_rng(7)
+    n = 64
+    sizes, keys, kidx, payloads, ctrs, slots = make_batch(rng, n, 4)
+    xl.set_keys(0, keys, kidx)
+    xl.set_xlane_lanes(n * 64)
+    wires = [o.format_packet_data(keys[slots[i]].tobytes(), int(kidx[slots[i]]), int(ctrs[i]), payloads[i])
+             for i in range(n)]
+    buf, offs = pack(wires)
+    d_buf = torch.from_numpy(buf).cuda()
+    base = d_buf.data_ptr()
+    d = np.zeros(n, DESC)
+    d["src_off"] = [base + x for x in offs]
+    d["dst_off"] = [base + x + 16 for x in offs]
+    d["len"] = [len(w) for w in wires]
+    d["key_slot"] = slots
+    d_descs = torch.from_numpy(d.view(np.uint8)).cuda()
+    d_st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    xl.open_batch(d_descs, n, None, None, d_st)
+    torch.cuda.synchronize()
+    assert (d_st.cpu().numpy() == 0).all()
+    got = d_buf.cpu().numpy()
+    for i in range(n):
+        assert got[offs[i] + 16:offs[i] + 16 + len(payloads[i])].tobytes() == payloads[i]
+
+
+def test_xlane_ordered_launch_matches_unordered(torch_cuda, xl):
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    n = 300
+    sizes, keys, kidx, payloads, ctrs, slots = make_batch(rng, n, 8)
+    xl.set_keys(0, keys, kidx)
+    src, soffs = pack(payloads)
+    descs, dst_size = seal_descs(sizes, soffs, ctrs, slots, rng)
+    want = np.zeros(dst_size, np.uint8)
+    o.seal_batch(descs, keys, kidx, src, want)
+    xl.set_xlane_lanes(n * 16)
+    d_descs = torch.from_numpy(descs.view(np.uint8)).cuda()
+    order = torch.from_numpy(rng.permutation(n).astype(np.uint32).view(np.int32)).cuda()
+    d_src = torch.from_numpy(src).cuda()
+    d_dst = torch.zeros(dst_size, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    xl.seal_batch_ordered(d_descs, order, n, d_src, d_dst, d_st)
+    torch.cuda.synchronize()
+    assert (d_st.cpu().numpy() == 0).all()
+    assert np.array_equal(d_dst.cpu().numpy(), want)
