@@ -116,6 +116,10 @@ typedef struct wg_gpu_ctx wg_gpu_ctx;
 /* ABI version (WG_GPU_ABI_VERSION). */
 int wg_gpu_abi_version(void);
 
+/* Build id: the first 16 hex digits of the SHA-256 of the sources the library was
+ * built from (neptun_amd/csrc/Makefile SRC_FILES); loaders compare it with the tree. */
+const char *wg_gpu_build_id(void);
+
 /* Last error message of the calling thread ("" if none). */
 const char *wg_gpu_last_error(void);
 

@@ -7,6 +7,7 @@ missing, calls raise ``NeptunGpuError``.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import re
 
@@ -42,6 +43,7 @@ def load() -> ctypes.CDLL:
     vp, u32, u64, i32 = c.c_void_p, c.c_uint32, c.c_uint64, c.c_int32
     L.wg_gpu_abi_version.restype = c.c_int
     L.wg_gpu_last_error.restype = c.c_char_p
+    L.wg_gpu_build_id.restype = c.c_char_p
     L.wg_gpu_ctx_create.argtypes = [c.c_int, u32, c.POINTER(vp)]
     L.wg_gpu_ctx_destroy.argtypes = [vp]
     L.wg_gpu_ctx_key_slots.argtypes = [vp]
@@ -78,8 +80,34 @@ def load() -> ctypes.CDLL:
         fn = getattr(L, name)
         if fn.restype is c.c_int and name not in ("wg_gpu_abi_version",):
             fn.restype = i32
+    want = source_build_id()
+    got = L.wg_gpu_build_id().decode()
+    if want is not None and got != want:
+        raise NeptunGpuError(
+            f"{LIB_PATH} was built from other sources (build id {got}, tree {want}): rebuild it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C neptun_amd/csrc`)")
     _lib = L
     return L
+
+
+CSRC = os.path.join(_HERE, "csrc")
+
+
+def source_build_id() -> str | None:
+    """The build id the sources in this tree give (neptun_amd/csrc/Makefile
+    SRC_FILES / SRC_HASH: the kernel and host sources, the Makefile and the public
+    headers, concatenated in that order); None when the sources are not here."""
+    if not os.path.isdir(CSRC):
+        return None
+    inc = os.path.join(os.path.dirname(_HERE), "include")
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h")))
+    files = [os.path.join(CSRC, f) for f in names] + [os.path.join(CSRC, "Makefile")]
+    files += [os.path.join(inc, f) for f in sorted(os.listdir(inc)) if f.endswith(".h")]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def check(rc: int, what: str) -> None:

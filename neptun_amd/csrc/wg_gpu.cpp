@@ -110,6 +110,11 @@ extern "C" {
 
 int wg_gpu_abi_version(void) { return WG_GPU_ABI_VERSION; }
 
+#ifndef WG_BUILD_ID
+#define WG_BUILD_ID "unknown"
+#endif
+const char *wg_gpu_build_id(void) { return WG_BUILD_ID; }
+
 const char *wg_gpu_last_error(void) { return g_last_error.c_str(); }
 
 int wg_gpu_ctx_create(int device, uint32_t key_slots, wg_gpu_ctx **out) {

@@ -25,6 +25,18 @@ def test_library_exports_header_symbols(header):
     assert lib.wg_gpu_abi_version() == 1
 
 
+def test_library_build_id_matches_the_sources(monkeypatch):
+    """The shipped .so carries the hash of the sources it was built from; the
+    loader refuses one built from other sources (a stale binary)."""
+    from neptun_amd import _native
+    lib = neptun_amd.load()
+    assert lib.wg_gpu_build_id().decode() == _native.source_build_id()
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "source_build_id", lambda: "0" * 16)
+    with pytest.raises(_native.NeptunGpuError, match="other sources"):
+        _native.load()
+
+
 def test_tunn_layouts_match_header():
     from neptun_amd.tunn import Replay, TunnResult
     text = open(neptun_amd.HEADER_PATH.replace("neptun_gpu.h", "neptun_tunn.h")).read()

@@ -13,7 +13,7 @@ AB_PAD=${AB_PAD:-1} AB_BURST=${AB_BURST:-100} AB_ROUNDS=${AB_ROUNDS:-6} \
 cat "$OUT/ab.log"
 [ $rc -eq 0 ] || exit $rc
 if [ -n "$PROBE_MEM4" ]; then
-  timeout -k 10 200 ./tools/microbench_mem4 > "$OUT/mem4.log" 2>&1; rc=$?
+  timeout -k 10 200 ./tools/probes/microbench_mem4 > "$OUT/mem4.log" 2>&1; rc=$?
   cat "$OUT/mem4.log"
   exit $rc
 fi

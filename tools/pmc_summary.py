@@ -3,7 +3,7 @@
 
 Derived numbers (per launch): HBM bytes with the gfx950 corrections of
 MI355X_MICROARCH.md "HBM": FETCH_SIZE (KiB) reads half of a wide streaming read
-on gfx950 -> x2 (calibrated for our access pattern by tools/microbench_mem*),
+on gfx950 -> x2 (calibrated for our access pattern by tools/probes/microbench_mem*),
 WRITE_SIZE (KiB) exact for 16-B/lane stores.
 """
 import csv
