@@ -205,11 +205,11 @@ int wg_gpu_ctx_set_slot_padding(wg_gpu_ctx *ctx, int writable);
  * Latency form of the descriptor batches (new, no reference counterpart; NepTUN's
  * inter-thread batches hold at most 50 packets, packet_workers.rs:27).  A batch of
  * n packets with n * G <= `lanes` runs G lanes per packet -- the largest G of 64,
- * 32, 16, 8 that fits -- instead of one packet per lane: the keystream blocks are
+ * 32, ..., 2 that fits -- instead of one packet per lane: the keystream blocks are
  * spread over the group and the Poly1305 partial sums combined with powers of r,
  * so a small batch takes about as long as one packet's share of blocks.  lanes = 0
  * turns it off; lanes < 0 restores the default (WG_XLANE_LANES from the
- * environment, else 512 per compute unit).  Results are identical either way.
+ * environment, else 256 per compute unit).  Results are identical either way.
  * Applies to later wg_gpu_seal_batch / wg_gpu_open_batch (and _ordered) calls.
  */
 int wg_gpu_ctx_set_xlane_lanes(wg_gpu_ctx *ctx, int64_t lanes);

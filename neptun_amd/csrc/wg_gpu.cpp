@@ -196,13 +196,15 @@ static dim3 persistent_grid(const wg_gpu_ctx *ctx, uint32_t waves, uint32_t &spr
 
 // Latency form (wg_xlane.hip): a batch that would fill only a small part of the
 // chip as one packet per lane runs G lanes per packet instead -- the largest G of
-// 64, 32, 16, 8 with n * G within a lane budget (wg_gpu_ctx_set_xlane_lanes, else
-// WG_XLANE_LANES, else cus * 512: two waves per SIMD).  0: the throughput forms.
-// (smallest group the selection takes: WG_XLANE_MIN_G, 2 .. 64, default 8)
+// 64 .. 2 with n * G within a lane budget (wg_gpu_ctx_set_xlane_lanes, else
+// WG_XLANE_LANES, else cus * 256: one wave per SIMD).  0: the throughput forms.
+// Measured (profiles/r05c_xlane_*.jsonl): 1350 B packets gain up to n = 32768
+// (G = 2: 37 us against 65 us), lose from 131072 on; 8192 B gain to 16384 (G = 4).
+// (smallest group the selection takes: WG_XLANE_MIN_G, 2 .. 64, default 2)
 static uint32_t xlane_min_group() {
   static const uint32_t g = [] {
     const char *e = std::getenv("WG_XLANE_MIN_G");
-    const long v = e ? std::atol(e) : 8L;
+    const long v = e ? std::atol(e) : 2L;
     uint32_t m = 2;
     while (m < 64 && (long)m < v) m *= 2;
     return m;
@@ -217,7 +219,7 @@ static uint32_t xlane_group(const wg_gpu_ctx *ctx, uint32_t n) {
   }();
   const uint64_t budget = ctx->xlane_lanes >= 0 ? (uint64_t)ctx->xlane_lanes
                           : env >= 0            ? (uint64_t)env
-                                                : (uint64_t)ctx->cus * 512u;
+                                                : (uint64_t)ctx->cus * 256u;
   for (uint32_t G = 64; G >= xlane_min_group(); G /= 2)
     if ((uint64_t)n * G <= budget) return G;
   return 0;

@@ -6,7 +6,7 @@
 // packet per lane, so such a batch is one or two waves whose lanes each walk their
 // packet's 23 ChaCha20 blocks and 85 Poly1305 blocks (1350 B) one after another
 // while the rest of the chip idles: ~70 us for 64 packets.  Here a packet is spread
-// over a group of G consecutive lanes of one wave (G = 64, 32, 16 or 8, chosen by
+// over a group of G consecutive lanes of one wave (G = 64, 32, ..., 2, chosen by
 // the host from the batch size, wg_gpu.cpp):
 //
 //   blocks   the packet's NB = 1 + ceil(P / 64) keystream blocks (block 0 = the

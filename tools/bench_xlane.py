@@ -14,6 +14,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -27,6 +28,8 @@ def main() -> None:
     ap.add_argument("--P", default="1350")
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--forms", default="default,64,32,16,8,off")
+    ap.add_argument("--warm-ms", type=float, default=300.0,
+                    help="launches before each timed form, to settle the clock (ms)")
     a = ap.parse_args()
     import torch
 
@@ -71,6 +74,11 @@ def main() -> None:
                                                     ("open", ctx.open_batch, d_open, wire, back)):
                     fn(desc, n, s_in, s_out, st)
                     torch.cuda.synchronize()
+                    t_end = time.perf_counter() + a.warm_ms / 1e3
+                    while time.perf_counter() < t_end:
+                        for _ in range(20):
+                            fn(desc, n, s_in, s_out, st)
+                        torch.cuda.synchronize()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     for _ in range(a.reps):
