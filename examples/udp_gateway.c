@@ -46,6 +46,25 @@
 #include "neptun_gpu.h"
 #include "neptun_tunn.h"
 
+/* -DGW_CPU: the same gateway with OpenSSL on the CPU in place of the GPU Tunn
+ * (gw_cpu_tunn.h) -- the same-box CPU line beside the GPU one */
+#ifdef GW_CPU
+#include "gw_cpu_tunn.h"
+typedef cpu_tunn gw_tunn;
+#define GW_BACKEND "cpu"
+#define gw_encapsulate_batch cpu_tunn_encapsulate_batch
+#define gw_decapsulate_batch cpu_tunn_decapsulate_batch
+#define gw_install_session cpu_tunn_install_session
+#define gw_destroy cpu_tunn_destroy
+#else
+typedef wg_tunn gw_tunn;
+#define GW_BACKEND "gpu"
+#define gw_encapsulate_batch wg_tunn_encapsulate_batch
+#define gw_decapsulate_batch wg_tunn_decapsulate_batch
+#define gw_install_session wg_tunn_install_session
+#define gw_destroy wg_tunn_destroy
+#endif
+
 #define MAX_DGRAM 65536
 
 typedef struct {
@@ -58,7 +77,7 @@ typedef struct {
 typedef struct {
   input_t *in;
   uint32_t i0, i1;  /* this pair's share of the input packets */
-  wg_tunn *a, *b;
+  gw_tunn *a, *b;
   int sa, sb;
   uint32_t batch, window, slot;  /* slot: bytes per preallocated packet buffer */
   /* sender output */
@@ -125,7 +144,7 @@ static void *sender(void *arg) {
     const uint32_t m = n - i0 < B ? n - i0 : B;
     for (uint32_t j = 0; j < m; ++j) cap[j] = g->slot;
     double t = now();
-    const int erc = wg_tunn_encapsulate_batch(g->a, m, (const uint8_t *const *)&g->in->pkt[i0],
+    const int erc = gw_encapsulate_batch(g->a, m, (const uint8_t *const *)&g->in->pkt[i0],
                                               &g->in->len[i0], &g->sent[i0], cap, res);
     g->t_encap += now() - t;
     if (erc) {
@@ -253,7 +272,7 @@ static void *decryptor(void *arg) {
       g->dst_cap[d + j] = L > 16 ? L - 16 : 0;
     }
     const double t = now();
-    const int drc = wg_tunn_decapsulate_batch(g->b, m, (const uint8_t *const *)&g->rx[d], &g->rx_len[d],
+    const int drc = gw_decapsulate_batch(g->b, m, (const uint8_t *const *)&g->rx[d], &g->rx_len[d],
                                               &g->dst[d], &g->dst_cap[d], &g->res[d]);
     g->t_decap += now() - t;
     if (drc) {
@@ -310,7 +329,9 @@ int main(int argc, char **argv) {
   const uint32_t pairs = argc > 4 && atoi(argv[4]) > 0 ? (uint32_t)atoi(argv[4]) : 1;
   const int reg = argc > 5 && strcmp(argv[5], "reg") == 0;
   wg_gpu_ctx *ctx = NULL;
+#ifndef GW_CPU
   CHECK(wg_gpu_ctx_create(0, 32 * pairs, &ctx));
+#endif
   const uint32_t n = in.n;
   uint8_t **sent = calloc(n, sizeof *sent), **rx = calloc(n, sizeof *rx), **dst = calloc(n, sizeof *dst);
   uint32_t *sent_len = calloc(n, 4), *rx_len = calloc(n, 4), *dst_cap = calloc(n, 4);
@@ -336,7 +357,7 @@ int main(int argc, char **argv) {
       in.pkt[i] = b;
     }
   }
-  if (reg) CHECK(wg_gpu_register_host(ctx, slabs, slab_bytes));
+  if (reg && ctx) CHECK(wg_gpu_register_host(ctx, slabs, slab_bytes));
   gw_t *gs = calloc(pairs, sizeof *gs);
   int rcvbuf = 0;
   for (uint32_t p = 0; p < pairs; ++p) {
@@ -346,11 +367,16 @@ int main(int argc, char **argv) {
     g->i1 = (uint32_t)((uint64_t)n * (p + 1) / pairs);
     g->batch = batch;
     g->slot = slot;
+#ifdef GW_CPU
+    CHECK(cpu_tunn_create(&g->a));
+    CHECK(cpu_tunn_create(&g->b));
+#else
     CHECK(wg_tunn_create(ctx, 32 * p, &g->a));
     CHECK(wg_tunn_create(ctx, 32 * p + 16, &g->b));
+#endif
     /* A sends with k1 to b_idx and receives with k2; B the mirror image */
-    CHECK(wg_tunn_install_session(g->a, in.a_idx + 256 * p, in.b_idx + 256 * p, in.k2, in.k1, 1));
-    CHECK(wg_tunn_install_session(g->b, in.b_idx + 256 * p, in.a_idx + 256 * p, in.k1, in.k2, 1));
+    CHECK(gw_install_session(g->a, in.a_idx + 256 * p, in.b_idx + 256 * p, in.k2, in.k1, 1));
+    CHECK(gw_install_session(g->b, in.b_idx + 256 * p, in.a_idx + 256 * p, in.k1, in.k2, 1));
     struct sockaddr_in aa, ab;
     g->sa = udp_socket(&aa);
     g->sb = udp_socket(&ab);
@@ -415,17 +441,17 @@ int main(int argc, char **argv) {
     }
     fclose(f);
   }
-  printf("{\"packets\": %u, \"sent\": %u, \"received\": %u, \"lost\": %u, \"batch\": %u, "
+  printf("{\"backend\": \"" GW_BACKEND "\", \"packets\": %u, \"sent\": %u, \"received\": %u, \"lost\": %u, \"batch\": %u, "
          "\"pairs\": %u, \"registered\": %d, \"window\": %u, \"rcvbuf\": %d, \"seconds\": %.6f, \"ip_bytes\": %llu, "
          "\"socket_to_socket_gbps\": %.3f, \"thread_seconds\": {\"encapsulate\": %.4f, "
          "\"sendmmsg\": %.4f, \"window_wait\": %.4f, \"recvmmsg\": %.4f, \"decapsulate\": %.4f}}\n",
          n, nsent, nrx, nsent - nrx, batch, pairs, reg, gs[0].window, rcvbuf, secs,
          (unsigned long long)bytes, bytes * 8.0 / secs / 1e9, te, ts, tw, tr, td);
   for (uint32_t p = 0; p < pairs; ++p) {
-    wg_tunn_destroy(gs[p].a);
-    wg_tunn_destroy(gs[p].b);
+    gw_destroy(gs[p].a);
+    gw_destroy(gs[p].b);
   }
-  if (reg) CHECK(wg_gpu_unregister_host(ctx, slabs));
-  wg_gpu_ctx_destroy(ctx);
+  if (reg && ctx) CHECK(wg_gpu_unregister_host(ctx, slabs));
+  if (ctx) wg_gpu_ctx_destroy(ctx);
   return 0;
 }

@@ -19,12 +19,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RES = struct.Struct("<iiIB16s3x")  # wg_tunn_result
 
 
-def build(tmp_path):
-    exe = str(tmp_path / "udp_gateway")
+def build(tmp_path, cpu=False):
+    """cpu: the OpenSSL backend (examples/gw_cpu_tunn.h) -- the same-box CPU line."""
+    exe = str(tmp_path / ("udp_gateway_cpu" if cpu else "udp_gateway"))
     lib = os.path.join(ROOT, "neptun_amd")
+    extra = ["-DGW_CPU", "-I", os.path.join(ROOT, "examples")] if cpu else []
     subprocess.run(["gcc", "-O2", "-Wall", "-Wextra", "-Werror", "-pthread", "-I",
-                    os.path.join(ROOT, "include"), os.path.join(ROOT, "examples", "udp_gateway.c"),
-                    "-L", lib, "-lneptun_gpu", f"-Wl,-rpath,{lib}", "-o", exe], check=True)
+                    os.path.join(ROOT, "include")] + extra + [os.path.join(ROOT, "examples", "udp_gateway.c"),
+                    "-L", lib, "-lneptun_gpu", f"-Wl,-rpath,{lib}"] + (["-lcrypto"] if cpu else [])
+                   + ["-o", exe], check=True)
     return exe
 
 
@@ -87,17 +90,26 @@ def test_udp_gateway_builds_and_fails_loudly_without_gpu(tmp_path):
 def test_udp_gateway_64k_packets_match_sequential_tunn(tmp_path, torch_cuda, pools):
     """64 Ki mixed-length packets through the gateway; "reg": its packet pools registered
     (the library's DMA path where a batch's packets form runs, staging elsewhere)."""
-    exe = build(tmp_path)
+    run_and_check(build(tmp_path), tmp_path, 65536, ["reg"] if pools == "reg" else [])
+
+
+def test_udp_gateway_cpu_backend_matches_sequential_tunn(tmp_path):
+    """The CPU line (OpenSSL in place of the GPU, same sockets and threads) obeys the
+    same sequential-Tunn contract, so the two gateway lines do the same work."""
+    run_and_check(build(tmp_path, cpu=True), tmp_path, 8192, [])
+
+
+def run_and_check(exe, tmp_path, n, extra):
     rng = random.Random(61)
     a_idx, b_idx = 0x00C0FE01, 0x00BEEF02
     k1, k2 = rng.randbytes(32), rng.randbytes(32)
     pkts = [ipv4(rng, rng.choice([20, 64, 576, 1350, 1400, rng.randrange(20, 1401)]))
-            for _ in range(65536)]
+            for _ in range(n)]
     for i in rng.sample(range(len(pkts)), 64):
         pkts[i] = b""  # keepalives
     inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
     write_input(inp, pkts, a_idx, b_idx, k1, k2)
-    r = subprocess.run([exe, str(inp), str(out), "1024", "1"] + (["reg"] if pools == "reg" else []),
+    r = subprocess.run([exe, str(inp), str(out), "1024", "1"] + extra,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     summary = json.loads(r.stdout.strip().splitlines()[-1])

@@ -8,7 +8,9 @@ batch sizes (the reference's default is 50, packet_workers.rs:27).
 
 GW_PAIRS="1 2 4 8" also sweeps the number of independent peers (Tunn pairs,
 socket pairs and worker threads) sharing the N packets at each batch size;
-GW_REG="0 1" also runs each with the packet pools registered (the DMA path).
+GW_REG="0 1" also runs each with the packet pools registered (the DMA path);
+GW_BACKEND="gpu cpu" also runs the CPU line (OpenSSL in place of the GPU Tunn, the
+same sockets, threads and batches: examples/gw_cpu_tunn.h).
 """
 import json
 import os
@@ -28,21 +30,28 @@ def main():
     P = int(sys.argv[2]) if len(sys.argv) > 2 else 1350
     batches = [int(b) for b in sys.argv[3:]] or [50, 256, 1024, 4096]
     with tempfile.TemporaryDirectory() as d:
-        exe = os.path.join(d, "udp_gateway")
         lib = os.path.join(ROOT, "neptun_amd")
-        subprocess.run(["gcc", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
-                        os.path.join(ROOT, "examples", "udp_gateway.c"), "-L", lib, "-lneptun_gpu",
-                        f"-Wl,-rpath,{lib}", "-o", exe], check=True)
+        exes = {}
+        for backend in os.environ.get("GW_BACKEND", "gpu").split():
+            exes[backend] = os.path.join(d, "udp_gateway_" + backend)
+            cpu = ["-DGW_CPU", "-I", os.path.join(ROOT, "examples")] if backend == "cpu" else []
+            subprocess.run(["gcc", "-O2", "-pthread", "-I", os.path.join(ROOT, "include")] + cpu
+                           + [os.path.join(ROOT, "examples", "udp_gateway.c"), "-L", lib, "-lneptun_gpu",
+                              f"-Wl,-rpath,{lib}"] + (["-lcrypto"] if cpu else []) + ["-o", exes[backend]],
+                           check=True)
         rng = random.Random(7)
         inp = os.path.join(d, "in.bin")
         write_input(inp, [ipv4(rng, P) for _ in range(n)], 11, 22, rng.randbytes(32), rng.randbytes(32))
         pairs = [int(p) for p in os.environ.get("GW_PAIRS", "1").split()]
         regs = [int(x) for x in os.environ.get("GW_REG", "0").split()]
-        for b, p, reg in ((b, p, reg) for b in batches for p in pairs for reg in regs):
+        runs = [(be, b, p, reg) for b in batches for p in pairs for be in exes
+                for reg in (regs if be == "gpu" else [0])]
+        for be, b, p, reg in runs:
+            exe = exes[be]
             r = subprocess.run([exe, inp, os.path.join(d, "out.bin"), str(b), str(p)] + (["reg"] if reg else []),
                                capture_output=True, text=True, timeout=600)
             line = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {
-                "error": r.stderr[-300:], "batch": b, "pairs": p, "registered": reg}
+                "error": r.stderr[-300:], "batch": b, "pairs": p, "registered": reg, "backend": be}
             line["packet_bytes"] = P
             print(json.dumps(line), flush=True)
 
