@@ -371,8 +371,16 @@ int main(int argc, char **argv) {
     CHECK(cpu_tunn_create(&g->a));
     CHECK(cpu_tunn_create(&g->b));
 #else
-    CHECK(wg_tunn_create(ctx, 32 * p, &g->a));
-    CHECK(wg_tunn_create(ctx, 32 * p + 16, &g->b));
+    if (getenv("GW_PRIVATE_ENGINES")) { /* (A/B: one engine per Tunn) */
+      wg_engine *ea = NULL, *eb = NULL;
+      CHECK(wg_engine_create(ctx, &ea));
+      CHECK(wg_engine_create(ctx, &eb));
+      CHECK(wg_tunn_create_on(ea, 32 * p, &g->a));
+      CHECK(wg_tunn_create_on(eb, 32 * p + 16, &g->b));
+    } else {
+      CHECK(wg_tunn_create(ctx, 32 * p, &g->a));
+      CHECK(wg_tunn_create(ctx, 32 * p + 16, &g->b));
+    }
 #endif
     /* A sends with k1 to b_idx and receives with k2; B the mirror image */
     CHECK(gw_install_session(g->a, in.a_idx + 256 * p, in.b_idx + 256 * p, in.k2, in.k1, 1));

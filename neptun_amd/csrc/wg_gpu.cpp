@@ -225,9 +225,36 @@ static uint32_t xlane_group(const wg_gpu_ctx *ctx, uint32_t n) {
   return 0;
 }
 
+// What a caller may know about a descriptor batch (the Tunn does: it wrote the
+// descriptors): its longest packet, and whether the kernel reaches src / dst in
+// host memory over PCIe.
+struct DescHint {
+  uint32_t max_len = 0;   // 0: unknown
+  bool host_mem = false;
+};
+
+// The latency form's group for a batch: the budget's G (xlane_group), narrowed to
+// the longest packet's keystream blocks when known (a 128-byte packet has 3 blocks:
+// a 64-lane group would leave 61 lanes idle and measured 2x slower than 4 lanes,
+// profiles/r05d_xlane.jsonl).  Reading host memory over PCIe, its 16-byte lane loads
+// cost more than the throughput form's whole-line loads beyond a few thousand
+// packets (Tunn staged batches of 16,384: 1.62 ms against 1.03, r05b_tunn_small).
+static uint32_t xlane_group_hinted(const wg_gpu_ctx *ctx, bool seal, uint32_t n, const DescHint &h) {
+  uint32_t G = xlane_group(ctx, n);
+  if (!G || (h.host_mem && n > 4096u)) return 0u;
+  if (h.max_len) {
+    const uint32_t P = seal ? h.max_len : (h.max_len > WG_DATA_OVERHEAD_SZ ? h.max_len - WG_DATA_OVERHEAD_SZ : 0u);
+    const uint32_t nb = 1u + (P + 63u) / 64u;
+    uint32_t g = 2;
+    while (g < nb && g < 64u) g *= 2;
+    G = std::max(std::min(G, g), xlane_min_group());
+  }
+  return G;
+}
+
 static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
                        const uint32_t *order, uint32_t n, const uint8_t *src, uint8_t *dst,
-                       int32_t *status, void *stream) {
+                       int32_t *status, void *stream, const DescHint &hint = DescHint{}) {
   // src / dst may be NULL: descriptor offsets are then absolute device addresses
   if (!ctx || (n && (!descs || !status))) return fail(WG_RC_INVALID_ARGUMENT, "batch: null argument");
   if (n == 0) return WG_RC_OK;
@@ -235,7 +262,7 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
   wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, order, src, dst, status, n,
                      ctx->key_slots, 0u};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (const uint32_t G = xlane_group(ctx, n)) {
+  if (const uint32_t G = xlane_group_hinted(ctx, seal, n, hint)) {
     using K = void (*)(wg::DescParams);
     static const K kernels[2][6] = {  // [seal][64, 32, 16, 8, 4, 2]
         {wg::aead_xlane_kernel<false, 64>, wg::aead_xlane_kernel<false, 32>,
@@ -275,6 +302,20 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
   WG_HIP(hipGetLastError(), "batch: launch");
   return WG_RC_OK;
 }
+
+}  // extern "C"
+
+// Tunn-internal launch (wg_tunn.cpp) with the batch's longest packet and memory kind
+int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, uint32_t n,
+                          const uint8_t *src, uint8_t *dst, int32_t *status, void *stream,
+                          uint32_t max_len, bool host_mem) {
+  DescHint h;
+  h.max_len = max_len;
+  h.host_mem = host_mem;
+  return launch_desc(ctx, seal, descs, nullptr, n, src, dst, status, stream, h);
+}
+
+extern "C" {
 
 int wg_gpu_seal_batch(wg_gpu_ctx *ctx, const wg_packet_desc *descs, uint32_t n,
                       const uint8_t *src, uint8_t *dst, int32_t *status, void *stream) {

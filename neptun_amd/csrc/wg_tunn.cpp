@@ -50,6 +50,9 @@
 int wg_pipe_fail(int rc, const char *what, hipError_t e);  // wg_gpu.cpp
 int wg_ctx_device(const wg_gpu_ctx *ctx);                   // wg_gpu.cpp
 bool wg_ctx_slot_padding(const wg_gpu_ctx *ctx);            // wg_gpu.cpp
+int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, uint32_t n,
+                          const uint8_t *src, uint8_t *dst, int32_t *status, void *stream,
+                          uint32_t max_len, bool host_mem);  // wg_gpu.cpp
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out);  // wg_gpu.cpp
 
 // ---------------------------------------------------------------------------
@@ -767,6 +770,13 @@ struct DevGuard {
   }
 };
 
+// longest descriptor length of a chunk (host-visible descriptors)
+inline uint32_t max_desc_len(const wg_packet_desc *d, size_t m) {
+  uint32_t x = 0;
+  for (size_t i = 0; i < m; ++i) x = std::max(x, d[i].len);
+  return x;
+}
+
 #define TUNN_HIP(call, what)                                              \
   do {                                                                    \
     hipError_t e_ = (call);                                               \
@@ -1174,10 +1184,9 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
       const uint8_t *in = abs_src ? nullptr : S.h_in;
       uint8_t *out = abs_dst ? nullptr : S.h_out;
       if (timed) TUNN_HIP(hipEventRecord(S.ev[1], S.stream), "tunn: event");
-      const int rc = seal ? wg_gpu_seal_batch(E.ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
-                                              S.stream)
-                          : wg_gpu_open_batch(E.ctx, S.h_desc, (uint32_t)m, in, out, S.h_st,
-                                              S.stream);
+      // (the kernel reads the packets over PCIe: hint the latency form's choice)
+      const int rc = wg_launch_desc_hinted(E.ctx, seal, S.h_desc, (uint32_t)m, in, out, S.h_st, S.stream,
+                                           max_desc_len(S.h_desc, m), true);
       if (rc) return rc;
       if (timed) TUNN_HIP(hipEventRecord(S.ev[2], S.stream), "tunn: event");
     } else {
@@ -1187,10 +1196,8 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
                               hipMemcpyHostToDevice, S.stream),
                "tunn: descs H2D");
       if (timed) TUNN_HIP(hipEventRecord(S.ev[1], S.stream), "tunn: event");
-      const int rc = seal ? wg_gpu_seal_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out,
-                                              S.d_st, S.stream)
-                          : wg_gpu_open_batch(E.ctx, S.d_desc, (uint32_t)m, S.d_in, S.d_out,
-                                              S.d_st, S.stream);
+      const int rc = wg_launch_desc_hinted(E.ctx, seal, S.d_desc, (uint32_t)m, S.d_in, S.d_out, S.d_st,
+                                           S.stream, max_desc_len(S.h_desc, m), false);
       if (rc) return rc;
       if (timed) TUNN_HIP(hipEventRecord(S.ev[2], S.stream), "tunn: event");
       post_kernel(ch, S);  // (may DMA the outputs straight to registered dst: S.out_dma)
@@ -1370,8 +1377,8 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
     // behind chunk c's kernel
     int rc = launch(c, S, qk);
     if (rc < 0)
-      rc = seal ? wg_gpu_seal_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk)
-                : wg_gpu_open_batch(E.ctx, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk);
+      rc = wg_launch_desc_hinted(E.ctx, seal, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk,
+                                 max_desc_len(E.b_desc + j0, m), false);
     if (rc) return rc;
     if (scatter) {
       if (split) {
