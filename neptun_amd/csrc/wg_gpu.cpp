@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -105,6 +106,49 @@ bool wg_ctx_dev_addr(wg_gpu_ctx *ctx, const void *p, uint64_t n, uint64_t *dev) 
   *dev = it->dev + (a - it->host);
   return true;
 }
+
+// Host ranges pinned by hipHostRegister, shared by every context that registers them
+// (a multi-GPU Tunn registers the caller's pools on each GPU's context): one pin per
+// range, released with its last registration.  A range must be registered with the
+// same base and size everywhere.
+namespace {
+struct Pin {
+  uint64_t bytes;
+  int refs;
+};
+std::mutex g_pin_mu;
+std::map<uint64_t, Pin> g_pins;
+
+int pin_acquire(uint64_t a, uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pins.upper_bound(a);
+  if (it != g_pins.begin()) {
+    auto p = std::prev(it);
+    if (p->first == a && p->second.bytes == bytes) {
+      ++p->second.refs;
+      return WG_RC_OK;
+    }
+    if (p->first + p->second.bytes > a)
+      return fail(WG_RC_INVALID_ARGUMENT, "register_host: overlaps a range another context registered differently");
+  }
+  if (it != g_pins.end() && it->first < a + bytes)
+    return fail(WG_RC_INVALID_ARGUMENT, "register_host: overlaps a range another context registered differently");
+  WG_HIP(hipHostRegister(reinterpret_cast<void *>(a), bytes, hipHostRegisterMapped | hipHostRegisterPortable),
+         "register_host: hipHostRegister");
+  g_pins[a] = Pin{bytes, 1};
+  return WG_RC_OK;
+}
+
+int pin_release(uint64_t a) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pins.find(a);
+  if (it == g_pins.end()) return fail(WG_RC_INVALID_ARGUMENT, "unregister_host: not pinned");
+  if (--it->second.refs > 0) return WG_RC_OK;
+  g_pins.erase(it);
+  WG_HIP(hipHostUnregister(reinterpret_cast<void *>(a)), "unregister_host: hipHostUnregister");
+  return WG_RC_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -464,11 +508,11 @@ int wg_gpu_register_host(wg_gpu_ctx *ctx, void *base, uint64_t bytes) {
     if (a < r.host + r.bytes && r.host < a + bytes)
       return fail(WG_RC_INVALID_ARGUMENT, "register_host: overlaps a registered range");
   DeviceGuard g(ctx->device);
-  WG_HIP(hipHostRegister(base, bytes, hipHostRegisterMapped), "register_host: hipHostRegister");
+  if (const int rc = pin_acquire(a, bytes)) return rc;
   void *dev = nullptr;
   const hipError_t e = hipHostGetDevicePointer(&dev, base, 0);
   if (e != hipSuccess) {
-    (void)hipHostUnregister(base);
+    (void)pin_release(a);
     return fail(WG_RC_HIP_ERROR, "register_host: device pointer", e);
   }
   const wg_gpu_ctx::Range r{a, bytes, reinterpret_cast<uint64_t>(dev)};
@@ -488,9 +532,8 @@ int wg_gpu_unregister_host(wg_gpu_ctx *ctx, void *base) {
     if (it->host == a) {
       DeviceGuard g(ctx->device);
       WG_HIP(hipDeviceSynchronize(), "unregister_host: sync");  // no batch may still use it
-      WG_HIP(hipHostUnregister(base), "unregister_host: hipHostUnregister");
       ctx->reg.erase(it);
-      return WG_RC_OK;
+      return pin_release(a);
     }
   return fail(WG_RC_INVALID_ARGUMENT, "unregister_host: not registered");
 }

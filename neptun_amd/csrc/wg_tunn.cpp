@@ -989,8 +989,9 @@ bool direct_possible(Engine &E) {
   wg_ctx_reg_snapshot(E.ctx, E.reg);
   return !E.reg.empty();
 }
-// this batch moves registered buffers by DMA runs (explicit copies; one engine)
-bool dma_possible(wg_tunn *t, Engine &E);
+// this batch moves registered buffers by DMA runs (explicit copies; one engine, or with
+// multi_ok every engine of a multi-GPU Tunn on its own share)
+bool dma_possible(wg_tunn *t, Engine &E, bool multi_ok = false);
 // DMA runs (explicit-copy mode, registered caller memory): packets whose host
 // buffers sit at a constant pitch with one length, and whose staging slots do
 // too, move as ONE 2D copy (rows = packets) on the copy engines -- the way the
@@ -1052,8 +1053,8 @@ hipError_t copy_runs(const std::vector<Run> &runs, uint8_t *dev_base, bool h2d, 
 }
 size_t max_runs(size_t m) { return std::max<size_t>(16, m / 16); }  // (16: the ramp's small chunks)
 
-bool dma_possible(wg_tunn *t, Engine &E) {
-  if (!dma_runs() || t->eng.size() != 1) return false;
+bool dma_possible(wg_tunn *t, Engine &E, bool multi_ok) {
+  if (!dma_runs() || (!multi_ok && t->eng.size() != 1)) return false;
   wg_ctx_reg_snapshot(E.ctx, E.reg);
   return !E.reg.empty();
 }
@@ -1545,6 +1546,15 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     for (size_t k = k0; k < k1; ++k) t->sc->act[k] = decide(k, st[k - k0]);
     t->ph.decide_us += now_us() - a;
   };
+  // Several engines over registered pools (multi_dma): every engine runs its share as a
+  // DMA batch of its own, concurrently; the speculation is taken for the whole selection
+  // in packet order first (pre_spec: it assumes every tag good, so it needs no result),
+  // and each chunk's decisions, repairs and copy-out wait until every engine is back
+  // (defer_done), then run in packet order.  inline_decide: the staged chunks decide as
+  // they return (one engine; or a multi-GPU engine whose share could not take the DMA
+  // batch, run on the caller in its turn).
+  bool multi_dma = false, pre_spec = false, defer_done = false, inline_decide = !multi;
+  int dma_err = WG_RC_OK;  // a chunk's results could not be taken (reported after the batch)
   // DMA batch (registered datagrams and destinations, one engine): run_dma with the
   // replay decisions speculated per chunk (every tag assumed good) so the plaintexts
   // are scattered into dst right behind the kernel.  The speculation never lands a
@@ -1563,9 +1573,62 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
              dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0], hb);
     });
   };
+  // a DMA chunk's results: in-order decisions, repairs of the packets the speculation
+  // missed, validation and copy-out
+  auto done_chunk = [&](Engine &E, const Chunk &ch, size_t j0) -> void {
+    if (dma_err) return;
+    decide_range(ch.k0, ch.k1, E.b_st + j0);
+    std::vector<size_t> rep;
+    const uint8_t landed = E.chunk_direct[&ch - E.chunks.data()] ? 2 : 1;  // 2: the tag still to write
+    for (size_t k = ch.k0; k < ch.k1; ++k) {
+      const bool lands = (t->sc->act[k] & 3) != 0;
+      if (lands && !t->sc->spec[k]) rep.push_back(k);
+      t->sc->out_dma[k] = lands && t->sc->spec[k] ? landed : 0;
+      if (!lands && t->sc->spec[k]) {  // (cannot happen: see above)
+        dma_err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: a speculated replay decision was not kept", hipSuccess);
+        return;
+      }
+    }
+    if (!rep.empty()) {
+      // open the missed packets again into pinned staging; their decisions stand
+      Staging &A = E.aux;
+      uint64_t bytes = 0;
+      for (size_t k : rep) bytes += round128(len[t->sc->sel[k]]);
+      if (const hipError_t e = reserve(A, bytes + 128, rep.size()); e != hipSuccess) {
+        dma_err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair staging", e);
+        return;
+      }
+      uint64_t o = 0;
+      for (size_t r = 0; r < rep.size(); ++r) {
+        const uint32_t i = t->sc->sel[rep[r]];
+        std::memcpy(A.h_in + o, datagram[i], len[i]);
+        A.h_desc[r] = wg_packet_desc{o, o + WG_DATA_OFFSET, 0, len[i], t->sc->slot[rep[r]]};
+        o += round128(len[i]);
+      }
+      if (const int rc = wg_gpu_open_batch(E.ctx, A.h_desc, (uint32_t)rep.size(), A.h_in, A.h_out, A.h_st,
+                                           A.stream)) {
+        dma_err = rc;
+        return;
+      }
+      if (const hipError_t e = hipStreamSynchronize(A.stream); e != hipSuccess) {
+        dma_err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair open", e);
+        return;
+      }
+      for (size_t r = 0; r < rep.size(); ++r) {
+        const size_t k = rep[r];
+        const uint32_t i = t->sc->sel[k];
+        const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
+        if ((t->sc->act[k] & 3) == 1) std::memcpy(dst[i], A.h_out + A.h_desc[r].dst_off, P);
+        else std::memset(dst[i], 0, P);
+        std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
+        t->sc->out_dma[k] = 1;  // (in dst now)
+      }
+    }
+    copy_out(E, ch, nullptr, nullptr);
+  };
   auto dma_batch = [&](Engine &E) -> int {
     const double t_prep = now_us();
-    if (multi || !dma_possible(t, E) || !registered(E, E.k0, E.k1)) {
+    if (!multi_dma && (multi || !dma_possible(t, E) || !registered(E, E.k0, E.k1))) {
       if (partial) {  // not for a DMA batch after all: the staged path takes the whole selection
         grow_all();
         split(t, size);
@@ -1573,7 +1636,6 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       return 1;
     }
     make_chunks(E, size, 0, dma_ramp());
-    int err = WG_RC_OK;  // a chunk's results could not be taken (reported after the batch)
     const int out_mode = dma_out_mode();
     const bool strided_ok = out_mode == 2 && !wg_ctx_slot_padding(E.ctx) && dma_strided();
     E.chunk_direct.assign(E.chunks.size(), 0);
@@ -1583,7 +1645,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       const size_t m = ch.k1 - ch.k0;
       uint32_t pmax = 0;
       for (size_t k = ch.k0; k < ch.k1; ++k) {  // (in packet order)
-        t->sc->spec[k] = speculate(k);
+        if (!pre_spec) t->sc->spec[k] = speculate(k);
         if (!t->sc->spec[k]) pmax = std::max(pmax, len[t->sc->sel[k]] - (uint32_t)WG_DATA_OVERHEAD_SZ);
       }
       E.ph.pack_spec_us += now_us() - a;
@@ -1634,55 +1696,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       return base ? reinterpret_cast<uint8_t *>(base) : d_out;
     };
     auto done = [&](const Chunk &ch, size_t j0) -> void {
-      if (err) return;
-      decide_range(ch.k0, ch.k1, E.b_st + j0);
-      std::vector<size_t> rep;
-      const uint8_t landed = E.chunk_direct[&ch - E.chunks.data()] ? 2 : 1;  // 2: the tag still to write
-      for (size_t k = ch.k0; k < ch.k1; ++k) {
-        const bool lands = (t->sc->act[k] & 3) != 0;
-        if (lands && !t->sc->spec[k]) rep.push_back(k);
-        t->sc->out_dma[k] = lands && t->sc->spec[k] ? landed : 0;
-        if (!lands && t->sc->spec[k]) {  // (cannot happen: see above)
-          err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: a speculated replay decision was not kept", hipSuccess);
-          return;
-        }
-      }
-      if (!rep.empty()) {
-        // open the missed packets again into pinned staging; their decisions stand
-        Staging &A = E.aux;
-        uint64_t bytes = 0;
-        for (size_t k : rep) bytes += round128(len[t->sc->sel[k]]);
-        if (const hipError_t e = reserve(A, bytes + 128, rep.size()); e != hipSuccess) {
-          err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair staging", e);
-          return;
-        }
-        uint64_t o = 0;
-        for (size_t r = 0; r < rep.size(); ++r) {
-          const uint32_t i = t->sc->sel[rep[r]];
-          std::memcpy(A.h_in + o, datagram[i], len[i]);
-          A.h_desc[r] = wg_packet_desc{o, o + WG_DATA_OFFSET, 0, len[i], t->sc->slot[rep[r]]};
-          o += round128(len[i]);
-        }
-        if (const int rc = wg_gpu_open_batch(E.ctx, A.h_desc, (uint32_t)rep.size(), A.h_in, A.h_out, A.h_st,
-                                             A.stream)) {
-          err = rc;
-          return;
-        }
-        if (const hipError_t e = hipStreamSynchronize(A.stream); e != hipSuccess) {
-          err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair open", e);
-          return;
-        }
-        for (size_t r = 0; r < rep.size(); ++r) {
-          const size_t k = rep[r];
-          const uint32_t i = t->sc->sel[k];
-          const uint32_t P = len[i] - WG_DATA_OVERHEAD_SZ;
-          if ((t->sc->act[k] & 3) == 1) std::memcpy(dst[i], A.h_out + A.h_desc[r].dst_off, P);
-          else std::memset(dst[i], 0, P);
-          std::memcpy(dst[i] + P, datagram[i] + WG_DATA_OFFSET + P, WG_AEAD_SIZE);
-          t->sc->out_dma[k] = 1;  // (in dst now)
-        }
-      }
-      copy_out(E, ch, nullptr, nullptr);
+      if (!defer_done) done_chunk(E, ch, j0);
     };
     auto more = [&]() -> int {
       if (!partial) return 1;
@@ -1711,7 +1725,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       grow_all();
       split(t, size);
     }
-    return err ? err : r;
+    return dma_err ? dma_err : r;
   };
   auto engine_job = [&](Engine &E) -> int {
     if (const int r = dma_batch(E); r == 2) {  // the rest of the batch: staged
@@ -1722,7 +1736,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       return r;
     }
     E.zc = zero_copy();
-    make_chunks(E, size, multi ? ~size_t(0) : 0);
+    make_chunks(E, size, inline_decide ? 0 : ~size_t(0));
     // direct input (zero-copy): every datagram 16-byte aligned inside registered memory
     bool direct = direct_possible(E);
     E.dsrc.resize(E.k1 - E.k0);
@@ -1748,15 +1762,54 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     };
     // statuses are back: decide in packet order (the copies follow in unpack)
     auto mid = [&](const Chunk &ch, Staging &S) -> int {
-      if (!multi) decide_range(ch.k0, ch.k1, S.h_st);  // (several engines: decided after all are back)
+      if (inline_decide) decide_range(ch.k0, ch.k1, S.h_st);  // (several engines: after all are back)
       return 0;
     };
     auto unpack = [&](const Chunk &ch, Staging &S) {
-      if (!multi) copy_out(E, ch, S.h_out, S.h_desc);
+      if (inline_decide) copy_out(E, ch, S.h_out, S.h_desc);
     };
     return run_chunks(E, false, pack, unpack, direct, false, NoHook(), mid);
   };
   int rc = WG_RC_OK;
+  if (multi) {
+    // registered pools on every engine's share: one DMA batch per engine (see multi_dma)
+    split(t, size);
+    bool all = dma_runs();
+    for (size_t e = 0; all && e < t->eng.size(); ++e) {
+      Engine &E = *t->eng[e];
+      DevGuard g(E.device);
+      all = dma_possible(t, E, true) && registered(E, E.k0, E.k1);
+    }
+    if (all) {
+      for (size_t k = 0; k < t->sc->sel.size(); ++k) t->sc->spec[k] = speculate(k);
+      multi_dma = pre_spec = defer_done = true;
+      std::vector<int> verdict(t->eng.size(), 1);
+      rc = for_engines(t, [&](Engine &E) -> int {
+        const size_t e = std::find(t->eng.begin(), t->eng.end(), &E) - t->eng.begin();
+        E.zc = zero_copy();
+        const int r = dma_batch(E);
+        verdict[e] = r;
+        return r == 1 ? WG_RC_OK : r;
+      });
+      defer_done = false;
+      // in packet order: each engine's DMA chunks, or -- a share whose input could not
+      // move as runs (verdict 1) -- the staged pipeline on the caller, deciding inline
+      for (size_t e = 0; !rc && e < t->eng.size(); ++e) {
+        Engine &E = *t->eng[e];
+        DevGuard g(E.device);
+        if (verdict[e] == 1) {
+          inline_decide = true;
+          rc = engine_job(E);
+          inline_decide = false;
+        } else {
+          for (const Chunk &ch : E.chunks) done_chunk(E, ch, ch.k0 - E.k0);
+          if (dma_err) rc = dma_err;
+        }
+      }
+      t->rx_bytes += rx.load();
+      return rc;
+    }
+  }
   if (!multi) {
     rc = for_engines(t, engine_job);
   } else {
@@ -2299,8 +2352,10 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
       split(t, size);
     };
     int left = 1;  // run_dma's verdict: 1 nothing done, 2 the packets from E.k1 on are left
-    if (!dma_possible(t, E)) grow_all();
-    if (dma_possible(t, E)) {
+    // (encapsulate has no in-order decisions: every engine of a multi-GPU Tunn runs its
+    // contiguous share as a DMA batch of its own, the counters reserved before the split)
+    if (!dma_possible(t, E, true)) grow_all();
+    if (dma_possible(t, E, true)) {
       const bool all = registered(E.k0, E.k1);
       if (all) {
         make_chunks(E, size, 0, dma_ramp());

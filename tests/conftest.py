@@ -25,8 +25,5 @@ def gpu(torch_cuda):
     """Session-wide context with a 4096-slot key table (config 4 size)."""
     from neptun_amd import GpuContext  # raises loudly if the .so is missing
     ctx = GpuContext(0, key_slots=4096)
-    # the throughput forms: descriptor tests here cover their wave shapes; the
-    # latency form has its own tests (test_xlane_gpu.py)
-    ctx.set_xlane_lanes(0)
     yield ctx
     ctx.close()

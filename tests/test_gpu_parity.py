@@ -21,6 +21,16 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 DESC = o.DESC_DTYPE
 
 
+@pytest.fixture(autouse=True)
+def throughput_forms(gpu):
+    """The descriptor tests here cover the throughput kernels' wave shapes: the latency
+    form (G lanes per packet for small batches) is off for them and has its own tests
+    (test_xlane_gpu.py); the Tunn and engine tests run with the default selection."""
+    gpu.set_xlane_lanes(0)
+    yield
+    gpu.set_xlane_lanes(-1)
+
+
 def golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)
@@ -1072,6 +1082,7 @@ def gpu1(torch_cuda):
     """A single-slot context: its descriptor launches take the SGPR-key forms."""
     from neptun_amd import GpuContext
     ctx = GpuContext(0, key_slots=1)
+    ctx.set_xlane_lanes(0)  # (the throughput forms, like the module's other tests)
     yield ctx
     ctx.close()
 

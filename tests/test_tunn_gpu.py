@@ -473,6 +473,98 @@ def test_multi_engine_split_matches_sequential_tunn(torch_cuda, monkeypatch, chu
         c.close()
 
 
+@pytest.mark.parametrize("out", ["scatter", "direct", "auto"])
+def test_multi_engine_registered_pools_match_sequential_tunn(torch_cuda, monkeypatch, out):
+    """wg_tunn_create_multi over two contexts with the caller's pools registered on both
+    (one pin shared by the contexts): each engine runs its share of a batch as a DMA
+    batch of its own -- encapsulate after the one counter reservation, decapsulate with
+    the replay speculation taken for the whole batch in packet order first and every
+    chunk's decisions, repairs and copy-out in packet order once both engines are back --
+    in each output form (WG_TUNN_DMA_OUT).  Damage as in the one-engine slot-pool test
+    (replays, old counters, forged tags ahead of the real packet, wrong indices,
+    keepalives).  Results, dst bytes, windows and stats equal the sequential model's."""
+    import numpy as np
+
+    from neptun_amd import GpuContext
+    from neptun_amd.tunn import Tunn
+    monkeypatch.setenv("WG_TUNN_DMA", "1")
+    if out != "auto":
+        monkeypatch.setenv("WG_TUNN_DMA_OUT", out)
+    monkeypatch.setenv("WG_TUNN_CHUNK_KB", "2048")
+    rng = random.Random(57)
+    ctxs = [GpuContext(0, key_slots=64), GpuContext(0, key_slots=64)]
+    tm, tg = M.Tunn(), Tunn(ctxs, 16)
+    sessions = []
+    for j, local in enumerate((5, 22)):
+        rk, sk, peer = rng.randbytes(32), rng.randbytes(32), rng.getrandbits(32)
+        for t in (tm, tg):
+            t.set_time(10 * (j + 1))
+            t.install_session(local, peer, rk, sk, True)
+        sessions.append((local, peer, rk, sk))
+    n, slot = 6000, 1536
+    srcs = [ipv4(rng, 1350 if rng.random() > 0.02 else rng.choice([64, 1349, 700])) for _ in range(n)]
+    a_src, a_dst = SlotArena(srcs, slot), SlotArena([], slot, n)
+    arenas = [a_src, a_dst]
+    for a in arenas:
+        for c in ctxs:
+            c.register_host(*a.window())
+    caps = np.full(n, slot, np.uint32)
+    dm = [bytearray(b"\xee" * slot) for _ in range(n)]
+    res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dm)]
+    tg.phases(reset=True)
+    res_g = tg.encapsulate_ptrs(a_src.ptrs, a_src.lens, a_dst.ptrs, caps)
+    check_same(res_g, res_m, [bytearray(a_dst.get(k, slot)) for k in range(n)], dm, "multi slot encap")
+    ph = tg.phases(reset=True)
+    # (prep: the DMA batches' setup -- the staged rounds have none)
+    assert ph["calls"] == 1 and ph["chunks"] >= 4 and ph["prep_us"] > 0
+    local, peer, rk, sk = sessions[1]
+    c = 0
+    dgs = []
+    for _ in range(n):
+        r = rng.random()
+        P = 1350 if rng.random() > 0.02 else rng.choice([0, 64, 1000])
+        pt = ipv4(rng, P) if P else b""
+        ctr = c if r > 0.03 else max(0, c - rng.randrange(1, 40)) if r > 0.015 else max(0, c - 3000)
+        c = max(c, ctr + 1)
+        d = bytearray(o.format_packet_data(rk, local, ctr, pt))
+        r = rng.random()
+        if r < 0.01:
+            d[rng.randrange(16, len(d))] ^= 0x04
+        elif r < 0.015:
+            d[4:8] = struct.pack("<I", local + 8)
+        dgs.append(bytes(d))
+    for at in range(100, n - 10, 997):  # a forged copy ahead of the real packet
+        forged = bytearray(dgs[at + 7])
+        forged[-1] ^= 0x80
+        dgs[at] = bytes(forged)
+    at_split = n // 2  # one forgery right at the engines' boundary
+    forged = bytearray(dgs[at_split + 3])
+    forged[-1] ^= 0x80
+    dgs[at_split - 2] = bytes(forged)
+    a_in, a_out = SlotArena(dgs, slot), SlotArena([], slot, n)
+    arenas += [a_in, a_out]
+    for a in (a_in, a_out):
+        for cx in ctxs:
+            cx.register_host(*a.window())
+    dm = [bytearray(b"\xee" * slot) for _ in range(n)]
+    res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+    res_g = tg.decapsulate_ptrs(a_in.ptrs, a_in.lens, a_out.ptrs, caps)
+    assert tg.phases(reset=True)["prep_us"] > 0
+    check_same(res_g, res_m, [bytearray(a_out.get(k, slot)) for k in range(n)], dm, "multi slot decap")
+    kinds = [r[:2] for r in res_m]
+    assert (M.ERR, M.INVALID_AEAD_TAG) in kinds and (M.ERR, M.DUPLICATE_COUNTER) in kinds
+    ctr, w = tg.session_counters(local % M.N_SESSIONS)
+    sm = tm.sessions[local % M.N_SESSIONS]
+    assert w.next == sm.window.next and list(w.bitmap) == sm.window.bitmap
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    tg.close()
+    for a in arenas:
+        for cx in ctxs:
+            cx.unregister_host(a.window()[0])
+    for cx in ctxs:
+        cx.close()
+
+
 def large_ipv4_udp_packet():
     """create_large_ipv4_udp_packet (noise/mod.rs:846-853): etherparse IPv4 (192.168.1.2 ->
     192.168.1.3, TTL 5) + UDP (5678 -> 23) around 1400 zero bytes = 1428 bytes."""

@@ -57,7 +57,7 @@ def seal_descs(sizes, soffs, ctrs, slots, rng):
 @pytest.fixture
 def xl(gpu):
     yield gpu
-    gpu.set_xlane_lanes(0)  # the session context's default for the other tests
+    gpu.set_xlane_lanes(-1)  # back to the default selection
 
 
 @pytest.mark.parametrize("G", [64, 32, 16, 8])
