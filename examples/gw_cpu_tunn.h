@@ -215,4 +215,22 @@ static int cpu_tunn_decapsulate_batch(cpu_tunn *t, uint32_t n, const uint8_t *co
   return 0;
 }
 
+/* multi-peer batches: packet i under its own Tunn's lock, one after another, as
+ * NepTUN's worker does (packet_workers.rs:207-233) */
+static int cpu_tunn_encapsulate_multi(uint32_t n, cpu_tunn *const *t, const uint8_t *const *src,
+                                      const uint32_t *src_len, uint8_t *const *dst, const uint32_t *dst_cap,
+                                      wg_tunn_result *res) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (cpu_tunn_encapsulate_batch(t[i], 1, &src[i], &src_len[i], &dst[i], &dst_cap[i], &res[i])) return -1;
+  return 0;
+}
+
+static int cpu_tunn_decapsulate_multi(uint32_t n, cpu_tunn *const *t, const uint8_t *const *dg,
+                                      const uint32_t *len, uint8_t *const *dst, const uint32_t *dst_cap,
+                                      wg_tunn_result *res) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (cpu_tunn_decapsulate_batch(t[i], 1, &dg[i], &len[i], &dst[i], &dst_cap[i], &res[i])) return -1;
+  return 0;
+}
+
 #endif /* GW_CPU_TUNN_H */

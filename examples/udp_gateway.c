@@ -19,7 +19,7 @@
  * the receive buffer overflows, so the sender keeps at most W datagrams in
  * flight (W from the socket's effective SO_RCVBUF).
  *
- *   udp_gateway IN OUT [B] [PAIRS] [reg]   -> one JSON line on stdout
+ *   udp_gateway IN OUT [B] [PAIRS] [reg] [mux]   -> one JSON line on stdout
  * PAIRS > 1 runs that many independent peers side by side (own Tunns, sockets
  * and threads, one GPU context), the way NepTUN serves peers on its n_threads
  * event loops.  "reg": the packet pools (the TUN read buffers the plaintexts land
@@ -56,6 +56,10 @@ typedef cpu_tunn gw_tunn;
 #define gw_decapsulate_batch cpu_tunn_decapsulate_batch
 #define gw_install_session cpu_tunn_install_session
 #define gw_destroy cpu_tunn_destroy
+#define gw_encapsulate_multi(e, ...) cpu_tunn_encapsulate_multi(__VA_ARGS__)
+#define gw_decapsulate_multi(e, ...) cpu_tunn_decapsulate_multi(__VA_ARGS__)
+typedef void gw_engine;
+#define gw_engine_of(t) NULL
 #else
 typedef wg_tunn gw_tunn;
 #define GW_BACKEND "gpu"
@@ -63,6 +67,10 @@ typedef wg_tunn gw_tunn;
 #define gw_decapsulate_batch wg_tunn_decapsulate_batch
 #define gw_install_session wg_tunn_install_session
 #define gw_destroy wg_tunn_destroy
+#define gw_encapsulate_multi wg_tunn_encapsulate_multi
+#define gw_decapsulate_multi wg_tunn_decapsulate_multi
+typedef wg_engine gw_engine;
+#define gw_engine_of(t) wg_tunn_engine(t)
 #endif
 
 #define MAX_DGRAM 65536
@@ -132,6 +140,55 @@ static int load_input(const char *path, input_t *in) {
   return 0;
 }
 
+/* send k prepared datagrams of pair g, keeping its window: 0, or -1 when the run stops */
+static int send_window(gw_t *g, struct mmsghdr *msgs, uint32_t k) {
+  /* flow control: at most `window` datagrams in the receiver's socket queue.
+     Lost datagrams never arrive, so a window that has not moved for 1 s is
+     written off (counted as lost) instead of waited for forever; the reader
+     ending (rx_done) or a failure stops the sender. */
+  double t;
+  uint32_t done = 0;
+  double stall_since = -1.0;
+  uint32_t stall_rx = 0;
+  while (done < k) {
+    if (atomic_load(&g->rx_done) || atomic_load(&g->failed)) return -1;
+    const uint32_t rx = atomic_load(&g->n_rx);
+    /* signed: datagrams written off as lost that arrive late after all would
+       otherwise underflow the in-flight count */
+    const int64_t inflight64 = (int64_t)atomic_load(&g->n_sent) - rx - atomic_load(&g->n_written_off);
+    const uint32_t inflight = inflight64 > 0 ? (uint32_t)inflight64 : 0u;
+    if (inflight >= g->window) {
+      t = now();
+      if (stall_since < 0 || rx != stall_rx) {
+        stall_since = t;
+        stall_rx = rx;
+      } else if (t - stall_since > 5.0 && atomic_load(&g->rx_idle)) {
+        /* only once the reader has sat idle in recvmmsg (not while it is busy
+           decrypting a slow batch) and the window has not moved for 5 s */
+        atomic_fetch_add(&g->n_written_off, inflight);
+        stall_since = -1.0;
+      }
+      sched_yield();
+      g->t_wait += now() - t;
+      continue;
+    }
+    stall_since = -1.0;
+    uint32_t can = g->window - inflight;
+    if (can > k - done) can = k - done;
+    t = now();
+    const int r = sendmmsg(g->sa, &msgs[done], can, 0);
+    g->t_send += now() - t;
+    if (r < 0) {
+      perror("sendmmsg");
+      atomic_store(&g->failed, 1);
+      return -1;
+    }
+    done += (uint32_t)r;
+    atomic_fetch_add(&g->n_sent, (uint32_t)r);
+  }
+  return 0;
+}
+
 /* encrypt worker: batch -> GPU encapsulate -> sendmmsg */
 static void *sender(void *arg) {
   gw_t *g = arg;
@@ -163,49 +220,7 @@ static void *sender(void *arg) {
       msgs[k].msg_hdr.msg_iovlen = 1;
       ++k;
     }
-    /* flow control: at most `window` datagrams in the receiver's socket queue.
-       Lost datagrams never arrive, so a window that has not moved for 1 s is
-       written off (counted as lost) instead of waited for forever; the reader
-       ending (rx_done) or a failure stops the sender. */
-    uint32_t done = 0;
-    double stall_since = -1.0;
-    uint32_t stall_rx = 0;
-    while (done < k) {
-      if (atomic_load(&g->rx_done) || atomic_load(&g->failed)) break;
-      const uint32_t rx = atomic_load(&g->n_rx);
-      /* signed: datagrams written off as lost that arrive late after all would
-         otherwise underflow the in-flight count */
-      const int64_t inflight64 = (int64_t)atomic_load(&g->n_sent) - rx - atomic_load(&g->n_written_off);
-      const uint32_t inflight = inflight64 > 0 ? (uint32_t)inflight64 : 0u;
-      if (inflight >= g->window) {
-        t = now();
-        if (stall_since < 0 || rx != stall_rx) {
-          stall_since = t;
-          stall_rx = rx;
-        } else if (t - stall_since > 5.0 && atomic_load(&g->rx_idle)) {
-          /* only once the reader has sat idle in recvmmsg (not while it is busy
-             decrypting a slow batch) and the window has not moved for 5 s */
-          atomic_fetch_add(&g->n_written_off, inflight);
-          stall_since = -1.0;
-        }
-        sched_yield();
-        g->t_wait += now() - t;
-        continue;
-      }
-      stall_since = -1.0;
-      uint32_t can = g->window - inflight;
-      if (can > k - done) can = k - done;
-      t = now();
-      const int r = sendmmsg(g->sa, &msgs[done], can, 0);
-      g->t_send += now() - t;
-      if (r < 0) {
-        perror("sendmmsg");
-        atomic_store(&g->failed, 1);
-        break;
-      }
-      done += (uint32_t)r;
-      atomic_fetch_add(&g->n_sent, (uint32_t)r);
-    }
+    if (send_window(g, msgs, k)) break;
   }
   atomic_store(&g->send_done, 1);
   free(res); free(cap); free(msgs); free(iov);
@@ -286,6 +301,150 @@ static void *decryptor(void *arg) {
   return NULL;
 }
 
+
+/* "mux": the PacketWorkers shape across peers -- ONE encrypt worker whose batches mix
+ * the pairs' packets (one at a time round robin, as NepTUN's inter-thread batches mix
+ * peers, packet_workers.rs:178-205) in one wg_tunn_encapsulate_multi call, then one
+ * sendmmsg per pair within its window; ONE decrypt worker that takes what every pair's
+ * reader has received into one wg_tunn_decapsulate_multi call.  The readers stay one
+ * per socket.  The thread count no longer grows with the pairs: 2 + pairs. */
+typedef struct {
+  gw_t *gs;
+  uint32_t pairs, batch;
+  gw_engine *e;
+  double t_encap, t_decap;
+} mux_t;
+
+static void *mux_sender(void *arg) {
+  mux_t *mx = arg;
+  const uint32_t P = mx->pairs, B = mx->batch;
+  gw_t *gs = mx->gs;
+  const input_t *in = gs[0].in;
+  gw_tunn **tun = calloc(B, sizeof *tun);
+  const uint8_t **src = calloc(B, sizeof *src);
+  uint8_t **dst = calloc(B, sizeof *dst);
+  uint32_t *len = calloc(B, 4), *cap = calloc(B, 4), *who = calloc(B, 4), *idx = calloc(B, 4);
+  uint32_t *cur = calloc(P, 4);
+  wg_tunn_result *res = calloc(B, sizeof *res);
+  struct mmsghdr *msgs = calloc(B, sizeof *msgs);
+  struct iovec *iov = calloc(B, sizeof *iov);
+  for (uint32_t p = 0; p < P; ++p) cur[p] = gs[p].i0;
+  int stop = 0;
+  while (!stop) {
+    uint32_t m = 0;
+    for (int any = 1; m < B && any;) {
+      any = 0;
+      for (uint32_t p = 0; p < P && m < B; ++p)
+        if (cur[p] < gs[p].i1) {
+          const uint32_t i = cur[p]++;
+          who[m] = p;
+          idx[m] = i;
+          tun[m] = gs[p].a;
+          src[m] = in->pkt[i];
+          len[m] = in->len[i];
+          dst[m] = gs[p].sent[i];
+          cap[m] = gs[p].slot;
+          ++m;
+          any = 1;
+        }
+    }
+    if (m == 0) break;
+    const double t = now();
+    const int erc = gw_encapsulate_multi(mx->e, m, tun, src, len, dst, cap, res);
+    mx->t_encap += now() - t;
+    if (erc) {
+      fprintf(stderr, "encapsulate_multi: %s\n", wg_gpu_last_error());
+      for (uint32_t p = 0; p < P; ++p) atomic_store(&gs[p].failed, 1);
+      break;
+    }
+    for (uint32_t p = 0; p < P && !stop; ++p) {
+      gw_t *g = &gs[p];
+      uint32_t k = 0;
+      for (uint32_t j = 0; j < m; ++j) {
+        if (who[j] != p) continue;
+        const uint32_t i = idx[j];
+        g->sent_len[i] = res[j].kind == WG_TUNN_WRITE_TO_NETWORK ? res[j].len : 0;
+        if (!g->sent_len[i]) continue;
+        iov[k].iov_base = g->sent[i];
+        iov[k].iov_len = g->sent_len[i];
+        memset(&msgs[k], 0, sizeof msgs[k]);
+        msgs[k].msg_hdr.msg_iov = &iov[k];
+        msgs[k].msg_hdr.msg_iovlen = 1;
+        ++k;
+      }
+      if (k && send_window(g, msgs, k)) stop = 1;
+    }
+  }
+  for (uint32_t p = 0; p < P; ++p) atomic_store(&gs[p].send_done, 1);
+  free(tun); free(src); free(dst); free(len); free(cap); free(who); free(idx); free(cur);
+  free(res); free(msgs); free(iov);
+  return NULL;
+}
+
+static void *mux_decryptor(void *arg) {
+  mux_t *mx = arg;
+  const uint32_t P = mx->pairs, B = mx->batch;
+  gw_t *gs = mx->gs;
+  gw_tunn **tun = calloc(B, sizeof *tun);
+  const uint8_t **dg = calloc(B, sizeof *dg);
+  uint8_t **dst = calloc(B, sizeof *dst);
+  uint32_t *len = calloc(B, 4), *cap = calloc(B, 4), *took = calloc(P, 4), *from = calloc(P, 4);
+  wg_tunn_result *res = calloc(B, sizeof *res);
+  uint32_t first = 0;  /* the pair served first (rotates: no pair starves the others) */
+  for (;;) {
+    uint32_t m = 0;
+    int all_done = 1, failed = 0;
+    for (uint32_t q = 0; q < P; ++q) {
+      const uint32_t p = (first + q) % P;
+      gw_t *g = &gs[p];
+      const int finished = atomic_load(&g->rx_done);
+      const uint32_t d = atomic_load(&g->n_dec), avail = atomic_load(&g->n_rx);
+      failed |= atomic_load(&g->failed);
+      uint32_t take = avail - d;
+      if (take > B - m) take = B - m;
+      if (!(finished && d + take == avail)) all_done = 0;
+      from[p] = d;
+      took[p] = take;
+      for (uint32_t k = 0; k < take; ++k) {
+        const uint32_t L = g->rx_len[d + k];
+        g->dst_cap[d + k] = L > 16 ? L - 16 : 0;
+        tun[m + k] = g->b;
+        dg[m + k] = g->rx[d + k];
+        len[m + k] = L;
+        dst[m + k] = g->dst[d + k];
+        cap[m + k] = g->dst_cap[d + k];
+      }
+      m += take;
+    }
+    first = (first + 1) % P;
+    if (m == 0) {
+      if (all_done || failed) break;
+      sched_yield();
+      continue;
+    }
+    const double t = now();
+    const int drc = gw_decapsulate_multi(mx->e, m, tun, dg, len, dst, cap, res);
+    mx->t_decap += now() - t;
+    if (drc) {
+      fprintf(stderr, "decapsulate_multi: %s\n", wg_gpu_last_error());
+      for (uint32_t p = 0; p < P; ++p) atomic_store(&gs[p].failed, 1);
+      break;
+    }
+    uint32_t j = 0;
+    for (uint32_t q = 0; q < P; ++q) {
+      const uint32_t p = (first + P - 1 + q) % P;  /* (the order the batch was built in) */
+      gw_t *g = &gs[p];
+      memcpy(&g->res[from[p]], &res[j], took[p] * sizeof *res);
+      j += took[p];
+      atomic_store(&g->n_dec, from[p] + took[p]);
+      if (took[p]) g->t_end = now();
+    }
+    if (all_done) break;
+  }
+  free(tun); free(dg); free(dst); free(len); free(cap); free(took); free(from); free(res);
+  return NULL;
+}
+
 static int udp_socket(struct sockaddr_in *addr) {
   const int s = socket(AF_INET, SOCK_DGRAM, 0);
   if (s < 0) return -1;
@@ -325,9 +484,14 @@ int main(int argc, char **argv) {
   const uint32_t batch = argc > 3 && atoi(argv[3]) > 0 ? (uint32_t)atoi(argv[3]) : 512;
   /* pairs > 1: that many independent peers (Tunn pairs, socket pairs and
    * threads) share the input -- NepTUN's per-peer Mutex<Tunn> + n_threads
-   * event loops; the output file is written for pairs == 1 only */
+   * event loops; the output file is written when every pair received its whole share
+   * (pair p's arrivals then sit in rx[n p / pairs, n (p + 1) / pairs)) */
   const uint32_t pairs = argc > 4 && atoi(argv[4]) > 0 ? (uint32_t)atoi(argv[4]) : 1;
-  const int reg = argc > 5 && strcmp(argv[5], "reg") == 0;
+  int reg = 0, mux = 0;
+  for (int a = 5; a < argc; ++a) {
+    reg |= strcmp(argv[a], "reg") == 0;
+    mux |= strcmp(argv[a], "mux") == 0;
+  }
   wg_gpu_ctx *ctx = NULL;
 #ifndef GW_CPU
   CHECK(wg_gpu_ctx_create(0, 32 * pairs, &ctx));
@@ -406,17 +570,25 @@ int main(int argc, char **argv) {
     g->dst_cap = dst_cap + g->i0;
     g->res = res + g->i0;
   }
+  mux_t mx = {gs, pairs, batch, gw_engine_of(gs[0].a), 0.0, 0.0};
   const double t0 = now();
   pthread_t *th = calloc(3 * pairs, sizeof *th);
+  uint32_t nth = 0;
   for (uint32_t p = 0; p < pairs; ++p) {
-    pthread_create(&th[3 * p], NULL, reader, &gs[p]);
-    pthread_create(&th[3 * p + 1], NULL, decryptor, &gs[p]);
-    pthread_create(&th[3 * p + 2], NULL, sender, &gs[p]);
+    pthread_create(&th[nth++], NULL, reader, &gs[p]);
+    if (!mux) {
+      pthread_create(&th[nth++], NULL, decryptor, &gs[p]);
+      pthread_create(&th[nth++], NULL, sender, &gs[p]);
+    }
   }
-  for (uint32_t k = 0; k < 3 * pairs; ++k) pthread_join(th[k], NULL);
+  if (mux) {
+    pthread_create(&th[nth++], NULL, mux_decryptor, &mx);
+    pthread_create(&th[nth++], NULL, mux_sender, &mx);
+  }
+  for (uint32_t k = 0; k < nth; ++k) pthread_join(th[k], NULL);
   uint32_t nrx = 0, nsent = 0;
   uint64_t bytes = 0;
-  double te = 0, ts = 0, tw = 0, tr = 0, td = 0;
+  double te = mx.t_encap, ts = 0, tw = 0, tr = 0, td = mx.t_decap;
   double t_end = t0;
   for (uint32_t p = 0; p < pairs; ++p) {
     gw_t *g = &gs[p];
@@ -430,7 +602,9 @@ int main(int argc, char **argv) {
     te += g->t_encap, ts += g->t_send, tw += g->t_wait, tr += g->t_recv, td += g->t_decap;
   }
   const double secs = t_end > t0 ? t_end - t0 : 1e-9;
-  if (pairs == 1) {
+  int whole = 1;
+  for (uint32_t p = 0; p < pairs; ++p) whole &= atomic_load(&gs[p].n_rx) == gs[p].i1 - gs[p].i0;
+  if (pairs == 1 || whole) {
     FILE *f = fopen(argv[2], "wb");
     if (!f) return 1;
     fwrite("NGWO", 1, 4, f);
@@ -450,10 +624,10 @@ int main(int argc, char **argv) {
     fclose(f);
   }
   printf("{\"backend\": \"" GW_BACKEND "\", \"packets\": %u, \"sent\": %u, \"received\": %u, \"lost\": %u, \"batch\": %u, "
-         "\"pairs\": %u, \"registered\": %d, \"window\": %u, \"rcvbuf\": %d, \"seconds\": %.6f, \"ip_bytes\": %llu, "
+         "\"pairs\": %u, \"mux\": %d, \"registered\": %d, \"window\": %u, \"rcvbuf\": %d, \"seconds\": %.6f, \"ip_bytes\": %llu, "
          "\"socket_to_socket_gbps\": %.3f, \"thread_seconds\": {\"encapsulate\": %.4f, "
          "\"sendmmsg\": %.4f, \"window_wait\": %.4f, \"recvmmsg\": %.4f, \"decapsulate\": %.4f}}\n",
-         n, nsent, nrx, nsent - nrx, batch, pairs, reg, gs[0].window, rcvbuf, secs,
+         n, nsent, nrx, nsent - nrx, batch, pairs, mux, reg, gs[0].window, rcvbuf, secs,
          (unsigned long long)bytes, bytes * 8.0 / secs / 1e9, te, ts, tw, tr, td);
   for (uint32_t p = 0; p < pairs; ++p) {
     gw_destroy(gs[p].a);

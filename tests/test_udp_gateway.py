@@ -93,13 +93,26 @@ def test_udp_gateway_64k_packets_match_sequential_tunn(tmp_path, torch_cuda, poo
     run_and_check(build(tmp_path), tmp_path, 65536, ["reg"] if pools == "reg" else [])
 
 
-def test_udp_gateway_cpu_backend_matches_sequential_tunn(tmp_path):
+@pytest.mark.parametrize("mode", [("1", []), ("3", ["mux"]), ("4", [])])
+def test_udp_gateway_cpu_backend_matches_sequential_tunn(tmp_path, mode):
     """The CPU line (OpenSSL in place of the GPU, same sockets and threads) obeys the
-    same sequential-Tunn contract, so the two gateway lines do the same work."""
-    run_and_check(build(tmp_path, cpu=True), tmp_path, 8192, [])
+    same sequential-Tunn contract, so the two gateway lines do the same work -- with
+    independent pairs, and with "mux" (one encrypt and one decrypt worker whose batches
+    mix the pairs: the multi-peer calls)."""
+    pairs, extra = mode
+    run_and_check(build(tmp_path, cpu=True), tmp_path, 8192, extra, int(pairs))
 
 
-def run_and_check(exe, tmp_path, n, extra):
+@pytest.mark.gpu
+@pytest.mark.parametrize("pools", ["plain", "reg"])
+def test_udp_gateway_mux_multi_peer_batches_match_sequential_tunns(tmp_path, torch_cuda, pools):
+    """4 peers behind one encrypt and one decrypt worker: every batch mixes the peers'
+    packets (wg_tunn_encapsulate_multi / wg_tunn_decapsulate_multi on the shared engine);
+    each peer's datagrams and decapsulated packets equal its own sequential Tunn's."""
+    run_and_check(build(tmp_path), tmp_path, 32768, ["mux"] + (["reg"] if pools == "reg" else []), 4)
+
+
+def run_and_check(exe, tmp_path, n, extra, pairs=1):
     rng = random.Random(61)
     a_idx, b_idx = 0x00C0FE01, 0x00BEEF02
     k1, k2 = rng.randbytes(32), rng.randbytes(32)
@@ -109,33 +122,36 @@ def run_and_check(exe, tmp_path, n, extra):
         pkts[i] = b""  # keepalives
     inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
     write_input(inp, pkts, a_idx, b_idx, k1, k2)
-    r = subprocess.run([exe, str(inp), str(out), "1024", "1"] + extra,
+    r = subprocess.run([exe, str(inp), str(out), "1024", str(pairs)] + extra,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     print(summary)
     sent, recv = read_output(out)
-    # A: n sequential Tunn::encapsulate calls
-    ta = M.Tunn()
-    ta.install_session(a_idx, b_idx, k2, k1, True)
-    for i, p in enumerate(pkts):
-        d = bytearray(len(p) + 32)
-        kind, st, ln = ta.encapsulate(p, d)
-        assert (kind, st) == (M.WRITE_TO_NETWORK, 0)
-        assert sent[i] == bytes(d[:ln]), i
     assert summary["lost"] == 0 and len(recv) == len(pkts)
-    # B: Tunn::decapsulate over the arrival sequence
-    tb = M.Tunn()
-    tb.install_session(b_idx, a_idx, k1, k2, True)
     kinds = set()
-    for j, (dg, res, dst) in enumerate(recv):
-        d = bytearray(len(dst))
-        m = tb.decapsulate(dg, d)
-        assert (res[0], res[1], res[2]) == m[:3], j
-        if m[0] == M.WRITE_TO_TUNNEL:
-            assert res[3] == m[3] and res[4][:4] == m[4]
-        assert dst == bytes(d), j
-        kinds.add(m[0])
+    for p in range(pairs):  # pair p: indices + 256 p, its share of the input in order
+        lo, hi = n * p // pairs, n * (p + 1) // pairs
+        # A: sequential Tunn::encapsulate calls over the pair's packets
+        ta = M.Tunn()
+        ta.install_session(a_idx + 256 * p, b_idx + 256 * p, k2, k1, True)
+        for i in range(lo, hi):
+            d = bytearray(len(pkts[i]) + 32)
+            kind, st, ln = ta.encapsulate(pkts[i], d)
+            assert (kind, st) == (M.WRITE_TO_NETWORK, 0)
+            assert sent[i] == bytes(d[:ln]), (p, i)
+        # B: Tunn::decapsulate over the pair's arrival sequence
+        tb = M.Tunn()
+        tb.install_session(b_idx + 256 * p, a_idx + 256 * p, k1, k2, True)
+        for j in range(lo, hi):
+            dg, res, dst = recv[j]
+            d = bytearray(len(dst))
+            m = tb.decapsulate(dg, d)
+            assert (res[0], res[1], res[2]) == m[:3], (p, j)
+            if m[0] == M.WRITE_TO_TUNNEL:
+                assert res[3] == m[3] and res[4][:4] == m[4]
+            assert dst == bytes(d), (p, j)
+            kinds.add(m[0])
     assert kinds == {M.WRITE_TO_TUNNEL, M.DONE}
     # loopback keeps order here, so every IP packet came back as sent
     got = [dst[:res[2]] for dg, res, dst in recv if res[0] == M.WRITE_TO_TUNNEL]

@@ -9,7 +9,8 @@ batch sizes (the reference's default is 50, packet_workers.rs:27).
 GW_PAIRS="1 2 4 8" also sweeps the number of independent peers (Tunn pairs,
 socket pairs and worker threads) sharing the N packets at each batch size;
 GW_REG="0 1" also runs each with the packet pools registered (the DMA path);
-GW_BACKEND="gpu cpu" also runs the CPU line (OpenSSL in place of the GPU Tunn, the
+GW_MUX="0 1" also runs the multi-peer worker shape ("mux": one encrypt and one decrypt
+worker whose batches mix the pairs, wg_tunn_*_multi); GW_BACKEND="gpu cpu" also runs the CPU line (OpenSSL in place of the GPU Tunn, the
 same sockets, threads and batches: examples/gw_cpu_tunn.h).
 """
 import json
@@ -44,14 +45,16 @@ def main():
         write_input(inp, [ipv4(rng, P) for _ in range(n)], 11, 22, rng.randbytes(32), rng.randbytes(32))
         pairs = [int(p) for p in os.environ.get("GW_PAIRS", "1").split()]
         regs = [int(x) for x in os.environ.get("GW_REG", "0").split()]
-        runs = [(be, b, p, reg) for b in batches for p in pairs for be in exes
+        muxes = [int(x) for x in os.environ.get("GW_MUX", "0").split()]
+        runs = [(be, b, p, reg, mx) for b in batches for p in pairs for be in exes for mx in muxes
                 for reg in (regs if be == "gpu" else [0])]
-        for be, b, p, reg in runs:
+        for be, b, p, reg, mx in runs:
             exe = exes[be]
-            r = subprocess.run([exe, inp, os.path.join(d, "out.bin"), str(b), str(p)] + (["reg"] if reg else []),
+            r = subprocess.run([exe, inp, os.path.join(d, "out.bin"), str(b), str(p)] + (["reg"] if reg else [])
+                               + (["mux"] if mx else []),
                                capture_output=True, text=True, timeout=600)
             line = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {
-                "error": r.stderr[-300:], "batch": b, "pairs": p, "registered": reg, "backend": be}
+                "error": r.stderr[-300:], "batch": b, "pairs": p, "registered": reg, "backend": be, "mux": mx}
             line["packet_bytes"] = P
             print(json.dumps(line), flush=True)
 
