@@ -315,66 +315,83 @@ void bind_thread_to_node(int node) {
   }
 }
 
-// Persistent worker pool: run(n, fn) calls fn(lo, hi) over a split of [0, n)
-// on the workers and the calling thread, and returns when all are done.
+// Persistent worker pool: run(n, fn) calls fn(lo, hi) over a split of [0, n) on the
+// workers and the calling thread, and returns when all are done.  The pool belongs to
+// an engine whose lanes run batch calls concurrently (one per peer's Tunn, from the
+// caller's threads), so several run()s may be active at once: each is a job of parts
+// that its caller and any idle worker claim one at a time (under the pool's lock; parts
+// are a batch's sixteenths, so the lock is taken a few times per step), the workers
+// taking turns over the active jobs.  A caller always works on its own job, so no
+// step waits behind another lane's.
 class Pool {
  public:
   Pool(unsigned workers, int node) : spin_ns_(spin_ns()) {
     for (unsigned i = 0; i < workers; ++i)
-      th_.emplace_back([this, i, node] {
+      th_.emplace_back([this, node] {
         bind_thread_to_node(node);
-        loop(i + 1);
+        loop();
       });
   }
   ~Pool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
-      agen_.store(~0ull, std::memory_order_release);
+      agen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     for (auto &t : th_) t.join();
   }
   unsigned size() const { return (unsigned)th_.size() + 1; }
-  // (grain: the fewest items worth a part of their own).  The pool belongs to an
-  // engine whose lanes run batches concurrently: a caller that finds it busy with
-  // another lane's step runs its own step on its own thread instead of waiting.
+  // (grain: the fewest items worth a part of their own)
   void run(size_t n, const std::function<void(size_t, size_t)> &fn, size_t grain = 64) {
     const unsigned parts = (unsigned)std::min<size_t>(size(), std::max<size_t>(n / std::max<size_t>(grain, 1), 1));
-    std::unique_lock<std::mutex> owner(run_mu_, std::defer_lock);
-    if (parts <= 1 || !owner.try_lock()) {
+    if (parts <= 1) {
       if (n) fn(0, n);
       return;
     }
+    Job j;
+    j.fn = &fn;
+    j.n = n;
+    j.parts = parts;
+    j.left.store(parts, std::memory_order_relaxed);
     bool wake;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      fn_ = &fn;
-      n_ = n;
-      parts_ = parts;
-      pending_.store(parts - 1, std::memory_order_relaxed);
-      ++gen_;
-      agen_.store(gen_, std::memory_order_release);
+      active_.push_back(&j);
+      agen_.fetch_add(1, std::memory_order_release);
       wake = sleepers_ > 0;
     }
     if (wake) cv_.notify_all();
-    fn(0, n / parts);  // part 0 on the caller
-    // the other parts: spin briefly (the workers are usually still spinning too), then block
+    // the caller's own parts first
+    for (;;) {
+      unsigned p;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (j.next >= j.parts) break;
+        p = claim(&j);
+      }
+      part(j, p);
+    }
+    // the parts workers took: spin briefly (they are usually still running), then block
     const auto t0 = std::chrono::steady_clock::now();
-    while (pending_.load(std::memory_order_acquire) != 0) {
+    while (j.left.load(std::memory_order_acquire) != 0) {
       if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() >
           spin_ns_) {
         std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [this] { return pending_.load(std::memory_order_acquire) == 0; });
+        done_.wait(lk, [&] { return j.left.load(std::memory_order_acquire) == 0; });
         break;
       }
       _mm_pause();
     }
-    std::lock_guard<std::mutex> lk(mu_);
-    fn_ = nullptr;
   }
 
  private:
+  struct Job {
+    const std::function<void(size_t, size_t)> *fn = nullptr;
+    size_t n = 0;
+    unsigned parts = 0, next = 0;  // (next: under the pool's lock)
+    std::atomic<unsigned> left{0};
+  };
   // Workers spin this long for the next job before they block on the condition variable
   // (WG_TUNN_SPIN_US, default 20): a batch call runs several pool steps back to back,
   // and a blocked worker's wake-up costs tens of microseconds on a loaded host.
@@ -382,43 +399,61 @@ class Pool {
     const char *e = std::getenv("WG_TUNN_SPIN_US");
     return (e ? std::max(0, std::atoi(e)) : 20) * 1000ll;
   }
-  void loop(unsigned id) {
-    uint64_t seen = 0;
+  // (under mu_) the next part of j; a job whose parts are all claimed leaves the list
+  unsigned claim(Job *j) {
+    const unsigned p = j->next++;
+    if (j->next >= j->parts) active_.erase(std::find(active_.begin(), active_.end(), j));
+    return p;
+  }
+  // run part p of j; the last part to finish wakes the job's caller (j may be gone
+  // as soon as `left` reaches 0: only the pool's own members are touched after it)
+  void part(Job &j, unsigned p) {
+    (*j.fn)(j.n * p / j.parts, j.n * (p + 1) / j.parts);
+    if (j.left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+      std::lock_guard<std::mutex> lk(mu_);  // (the caller may be about to block on done_)
+      done_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = agen_.load(std::memory_order_acquire);
+    size_t rr = 0;
     for (;;) {
+      Job *j = nullptr;
+      unsigned p = 0;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        if (!active_.empty()) {
+          j = active_[rr++ % active_.size()];
+          p = claim(j);
+        } else if (stop_) {
+          return;
+        }
+      }
+      if (j) {
+        part(*j, p);
+        continue;
+      }
+      // nothing to do: spin on the job generation, then block
       const auto t0 = std::chrono::steady_clock::now();
       while (agen_.load(std::memory_order_acquire) == seen &&
              std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() <
                  spin_ns_)
         _mm_pause();
       std::unique_lock<std::mutex> lk(mu_);
-      if (!stop_ && gen_ == seen) {
+      if (!stop_ && active_.empty() && agen_.load(std::memory_order_acquire) == seen) {
         ++sleepers_;
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        cv_.wait(lk, [&] { return stop_ || !active_.empty(); });
         --sleepers_;
       }
-      if (stop_) return;
-      seen = gen_;
-      if (id >= parts_) continue;
-      const auto *fn = fn_;
-      const size_t lo = n_ * id / parts_, hi = n_ * (id + 1) / parts_;
-      lk.unlock();
-      (*fn)(lo, hi);
-      if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
-        lk.lock();  // (the caller may be about to block on done_)
-        done_.notify_one();
-      }
+      seen = agen_.load(std::memory_order_acquire);
     }
   }
   const int64_t spin_ns_;
   std::vector<std::thread> th_;
-  std::mutex run_mu_;  // held by the caller whose step the workers run
   std::mutex mu_;
   std::condition_variable cv_, done_;
-  const std::function<void(size_t, size_t)> *fn_ = nullptr;
-  size_t n_ = 0;
-  unsigned parts_ = 0, sleepers_ = 0;
-  std::atomic<unsigned> pending_{0};
-  uint64_t gen_ = 0;
+  std::vector<Job *> active_;  // jobs with parts not yet claimed
+  unsigned sleepers_ = 0;
   std::atomic<uint64_t> agen_{0};
   bool stop_ = false;
 };
