@@ -626,9 +626,28 @@ int main(int argc, char **argv) {
   printf("{\"backend\": \"" GW_BACKEND "\", \"packets\": %u, \"sent\": %u, \"received\": %u, \"lost\": %u, \"batch\": %u, "
          "\"pairs\": %u, \"mux\": %d, \"registered\": %d, \"window\": %u, \"rcvbuf\": %d, \"seconds\": %.6f, \"ip_bytes\": %llu, "
          "\"socket_to_socket_gbps\": %.3f, \"thread_seconds\": {\"encapsulate\": %.4f, "
-         "\"sendmmsg\": %.4f, \"window_wait\": %.4f, \"recvmmsg\": %.4f, \"decapsulate\": %.4f}}\n",
+         "\"sendmmsg\": %.4f, \"window_wait\": %.4f, \"recvmmsg\": %.4f, \"decapsulate\": %.4f}",
          n, nsent, nrx, nsent - nrx, batch, pairs, mux, reg, gs[0].window, rcvbuf, secs,
          (unsigned long long)bytes, bytes * 8.0 / secs / 1e9, te, ts, tw, tr, td);
+#ifndef GW_CPU
+  /* where the library's time went, summed over the pairs' Tunns (wg_tunn_get_phases) */
+  for (int side = 0; side < 2; ++side) {
+    wg_tunn_phases s = {0}, q;
+    for (uint32_t p = 0; p < pairs; ++p) {
+      if (wg_tunn_get_phases(side ? gs[p].b : gs[p].a, &q)) continue;
+      s.calls += q.calls, s.packets += q.packets, s.total_us += q.total_us, s.checks_us += q.checks_us;
+      s.pack_us += q.pack_us, s.submit_us += q.submit_us, s.wait_us += q.wait_us, s.decide_us += q.decide_us;
+      s.copy_out_us += q.copy_out_us, s.prep_us += q.prep_us;
+    }
+    printf(", \"%s_phases_s\": {\"calls\": %llu, \"packets\": %llu, \"total\": %.4f, \"checks\": %.4f, "
+           "\"pack\": %.4f, \"submit\": %.4f, \"wait\": %.4f, \"decide\": %.4f, \"copy_out\": %.4f, "
+           "\"prep\": %.4f}",
+           side ? "decapsulate" : "encapsulate", (unsigned long long)s.calls, (unsigned long long)s.packets,
+           s.total_us * 1e-6, s.checks_us * 1e-6, s.pack_us * 1e-6, s.submit_us * 1e-6, s.wait_us * 1e-6,
+           s.decide_us * 1e-6, s.copy_out_us * 1e-6, s.prep_us * 1e-6);
+  }
+#endif
+  printf("}\n");
   for (uint32_t p = 0; p < pairs; ++p) {
     gw_destroy(gs[p].a);
     gw_destroy(gs[p].b);
