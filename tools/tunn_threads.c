@@ -98,16 +98,21 @@ int main(int argc, char **argv) {
       return 1;
     }
   }
-  /* warm-up call per thread (staging allocations) */
+  /* warm-up: two calls per thread, all threads at once (the engines' lanes and staging
+   * are made on first use, one lane per concurrent call) */
+  pthread_t *th = calloc(T, sizeof *th);
   for (uint32_t t = 0; t < T; ++t) {
-    job_t w = jobs[t];
-    w.calls = 1;
-    run(&w);
-    if (w.rc) return 1;
+    jobs[t].calls = 2;
+    pthread_create(&th[t], NULL, run, &jobs[t]);
+  }
+  for (uint32_t t = 0; t < T; ++t) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].rc) return 1;
+    jobs[t].calls = calls;
+    jobs[t].t_enc = jobs[t].t_dec = 0;
     wg_tunn_reset_phases(jobs[t].a);
     wg_tunn_reset_phases(jobs[t].b);
   }
-  pthread_t *th = calloc(T, sizeof *th);
   const double t0 = now();
   for (uint32_t t = 0; t < T; ++t) pthread_create(&th[t], NULL, run, &jobs[t]);
   for (uint32_t t = 0; t < T; ++t) pthread_join(th[t], NULL);
