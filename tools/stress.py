@@ -8,8 +8,12 @@ buffers, canaries included, to be byte-identical; open both back and require
 the plaintext, statuses and untouched canaries; every few iterations also a
 mixed-length descriptor batch through the plan (ordered launch) against its
 unordered twin, and every third a batch with a random key slot per packet (a
-4096-slot table: the affine descriptor kernel against the plan-ordered one).  A one-in-a-million corruption in any form shows up as a
-mismatch between forms that share no kernel.  Prints one JSON summary line.
+4096-slot table: the affine descriptor kernel against the plan-ordered one).  The
+unordered descriptor launch draws its form at random (round 5): the throughput kernels,
+the default selection, or the latency form with a forced group of 2 .. 64 lanes per
+packet (wg_xlane.hip) -- and so does the descriptor open.  A one-in-a-million
+corruption in any form shows up as a mismatch between forms that share no kernel.
+Prints one JSON summary line.
 
     python tools/stress.py [SECONDS] [OUT.json]
 """
@@ -41,6 +45,8 @@ def main():
     ctxk = neptun_amd.GpuContext(0, key_slots=4096)
     ctxk.set_keys(0, synth.keys(4096, seed=seed + 1),
                   np.full(4096, synth.RECEIVER_IDX, np.uint32) + np.arange(4096, dtype=np.uint32))
+    ctx1.set_xlane_lanes(0)
+    ctxk.set_xlane_lanes(0)
     stats = {"seed": seed, "iterations": 0, "packets": 0, "bytes": 0, "mismatches": [], "forms": {}}
     t_end = time.time() + seconds
     last_print = time.time()
@@ -72,6 +78,18 @@ def main():
         d_descs = torch.from_numpy(descs.view(np.uint8)).to(dev)
         outs, sts = [], []
         forms = ["desc-ordered", "desc"] if (mixed or keyed) else ["strided", "desc"]
+
+        def pick_xlane():  # the unordered descriptor launch's form
+            c = int(rng.integers(0, 4))
+            if c == 0:
+                ctx.set_xlane_lanes(0)
+                return "tput"
+            if c == 1:
+                ctx.set_xlane_lanes(-1)
+                return "default"
+            G = int(rng.choice([2, 4, 8, 16, 32, 64]))
+            ctx.set_xlane_lanes(n * G)
+            return f"xlane{G}"
         for form in forms:
             w = torch.full((n * S + 64,), 0xA5, dtype=torch.uint8, device=dev)
             st = torch.full((n,), -1, dtype=torch.int32, device=dev)
@@ -83,7 +101,9 @@ def main():
                 ctx.plan_batch(True, d_descs, n, order, scratch)
                 ctx.seal_batch_ordered(d_descs, order, n, pt, w, st)
             else:
+                form = form + "-" + pick_xlane()
                 ctx.seal_batch(d_descs, n, pt, w, st)
+                ctx.set_xlane_lanes(0)  # (the ordered launches: the throughput kernels)
             outs.append(w)
             sts.append(st)
             tag = form + ("-keyed" if keyed else "")
@@ -100,8 +120,11 @@ def main():
         d2["len"] = sizes + 32
         back = torch.full((n * S + 64,), 0x5A, dtype=torch.uint8, device=dev)
         st2 = torch.full((n,), -1, dtype=torch.int32, device=dev)
-        if mixed or keyed:
+        if mixed or keyed or it % 2 == 0:
+            tag = "open-" + pick_xlane()
+            stats["forms"][tag] = stats["forms"].get(tag, 0) + 1
             ctx.open_batch(torch.from_numpy(d2.view(np.uint8)).to(dev), n, outs[0], back, st2)
+            ctx.set_xlane_lanes(0)
         else:
             ctx.open_strided(n, int(sizes[0]) + 32, 0, outs[0], S, back, S, st2)
         torch.cuda.synchronize()
