@@ -19,7 +19,7 @@
  * the receive buffer overflows, so the sender keeps at most W datagrams in
  * flight (W from the socket's effective SO_RCVBUF).
  *
- *   udp_gateway IN OUT [B] [PAIRS] [reg] [mux]   -> one JSON line on stdout
+ *   udp_gateway IN OUT [B] [PAIRS] [reg] [mux[=W]]   -> one JSON line on stdout
  * PAIRS > 1 runs that many independent peers side by side (own Tunns, sockets
  * and threads, one GPU context), the way NepTUN serves peers on its n_threads
  * event loops.  "reg": the packet pools (the TUN read buffers the plaintexts land
@@ -302,14 +302,15 @@ static void *decryptor(void *arg) {
 }
 
 
-/* "mux": the PacketWorkers shape across peers -- ONE encrypt worker whose batches mix
- * the pairs' packets (one at a time round robin, as NepTUN's inter-thread batches mix
- * peers, packet_workers.rs:178-205) in one wg_tunn_encapsulate_multi call, then one
- * sendmmsg per pair within its window; ONE decrypt worker that takes what every pair's
- * reader has received into one wg_tunn_decapsulate_multi call.  The readers stay one
- * per socket.  The thread count no longer grows with the pairs: 2 + pairs. */
+/* "mux[=W]": the PacketWorkers shape across peers -- W worker groups (default 1), each
+ * serving the pairs p with p % W == its index: ONE encrypt worker whose batches mix its
+ * pairs' packets (one at a time round robin, as NepTUN's inter-thread batches mix peers,
+ * packet_workers.rs:178-205) in one wg_tunn_encapsulate_multi call, then one sendmmsg
+ * per pair within its window; ONE decrypt worker that takes what each of its pairs'
+ * readers has received into one wg_tunn_decapsulate_multi call.  The readers stay one
+ * per socket.  Threads: 2 W + pairs, whatever the number of peers per worker. */
 typedef struct {
-  gw_t *gs;
+  gw_t **gp;   /* this group's pairs */
   uint32_t pairs, batch;
   gw_engine *e;
   double t_encap, t_decap;
@@ -318,8 +319,8 @@ typedef struct {
 static void *mux_sender(void *arg) {
   mux_t *mx = arg;
   const uint32_t P = mx->pairs, B = mx->batch;
-  gw_t *gs = mx->gs;
-  const input_t *in = gs[0].in;
+  gw_t **gp = mx->gp;
+  const input_t *in = gp[0]->in;
   gw_tunn **tun = calloc(B, sizeof *tun);
   const uint8_t **src = calloc(B, sizeof *src);
   uint8_t **dst = calloc(B, sizeof *dst);
@@ -328,22 +329,22 @@ static void *mux_sender(void *arg) {
   wg_tunn_result *res = calloc(B, sizeof *res);
   struct mmsghdr *msgs = calloc(B, sizeof *msgs);
   struct iovec *iov = calloc(B, sizeof *iov);
-  for (uint32_t p = 0; p < P; ++p) cur[p] = gs[p].i0;
+  for (uint32_t p = 0; p < P; ++p) cur[p] = gp[p]->i0;
   int stop = 0;
   while (!stop) {
     uint32_t m = 0;
     for (int any = 1; m < B && any;) {
       any = 0;
       for (uint32_t p = 0; p < P && m < B; ++p)
-        if (cur[p] < gs[p].i1) {
+        if (cur[p] < gp[p]->i1) {
           const uint32_t i = cur[p]++;
           who[m] = p;
           idx[m] = i;
-          tun[m] = gs[p].a;
+          tun[m] = gp[p]->a;
           src[m] = in->pkt[i];
           len[m] = in->len[i];
-          dst[m] = gs[p].sent[i];
-          cap[m] = gs[p].slot;
+          dst[m] = gp[p]->sent[i];
+          cap[m] = gp[p]->slot;
           ++m;
           any = 1;
         }
@@ -354,11 +355,11 @@ static void *mux_sender(void *arg) {
     mx->t_encap += now() - t;
     if (erc) {
       fprintf(stderr, "encapsulate_multi: %s\n", wg_gpu_last_error());
-      for (uint32_t p = 0; p < P; ++p) atomic_store(&gs[p].failed, 1);
+      for (uint32_t p = 0; p < P; ++p) atomic_store(&gp[p]->failed, 1);
       break;
     }
     for (uint32_t p = 0; p < P && !stop; ++p) {
-      gw_t *g = &gs[p];
+      gw_t *g = gp[p];
       uint32_t k = 0;
       for (uint32_t j = 0; j < m; ++j) {
         if (who[j] != p) continue;
@@ -375,7 +376,7 @@ static void *mux_sender(void *arg) {
       if (k && send_window(g, msgs, k)) stop = 1;
     }
   }
-  for (uint32_t p = 0; p < P; ++p) atomic_store(&gs[p].send_done, 1);
+  for (uint32_t p = 0; p < P; ++p) atomic_store(&gp[p]->send_done, 1);
   free(tun); free(src); free(dst); free(len); free(cap); free(who); free(idx); free(cur);
   free(res); free(msgs); free(iov);
   return NULL;
@@ -384,7 +385,7 @@ static void *mux_sender(void *arg) {
 static void *mux_decryptor(void *arg) {
   mux_t *mx = arg;
   const uint32_t P = mx->pairs, B = mx->batch;
-  gw_t *gs = mx->gs;
+  gw_t **gp = mx->gp;
   gw_tunn **tun = calloc(B, sizeof *tun);
   const uint8_t **dg = calloc(B, sizeof *dg);
   uint8_t **dst = calloc(B, sizeof *dst);
@@ -396,7 +397,7 @@ static void *mux_decryptor(void *arg) {
     int all_done = 1, failed = 0;
     for (uint32_t q = 0; q < P; ++q) {
       const uint32_t p = (first + q) % P;
-      gw_t *g = &gs[p];
+      gw_t *g = gp[p];
       const int finished = atomic_load(&g->rx_done);
       const uint32_t d = atomic_load(&g->n_dec), avail = atomic_load(&g->n_rx);
       failed |= atomic_load(&g->failed);
@@ -427,13 +428,13 @@ static void *mux_decryptor(void *arg) {
     mx->t_decap += now() - t;
     if (drc) {
       fprintf(stderr, "decapsulate_multi: %s\n", wg_gpu_last_error());
-      for (uint32_t p = 0; p < P; ++p) atomic_store(&gs[p].failed, 1);
+      for (uint32_t p = 0; p < P; ++p) atomic_store(&gp[p]->failed, 1);
       break;
     }
     uint32_t j = 0;
     for (uint32_t q = 0; q < P; ++q) {
       const uint32_t p = (first + P - 1 + q) % P;  /* (the order the batch was built in) */
-      gw_t *g = &gs[p];
+      gw_t *g = gp[p];
       memcpy(&g->res[from[p]], &res[j], took[p] * sizeof *res);
       j += took[p];
       atomic_store(&g->n_dec, from[p] + took[p]);
@@ -516,10 +517,10 @@ int main(int argc, char **argv) {
    * event loops; the output file is written when every pair received its whole share
    * (pair p's arrivals then sit in rx[n p / pairs, n (p + 1) / pairs)) */
   const uint32_t pairs = argc > 4 && atoi(argv[4]) > 0 ? (uint32_t)atoi(argv[4]) : 1;
-  int reg = 0, mux = 0;
+  int reg = 0, mux = 0;  /* mux: worker groups (0: one sender + decryptor per pair) */
   for (int a = 5; a < argc; ++a) {
     reg |= strcmp(argv[a], "reg") == 0;
-    mux |= strcmp(argv[a], "mux") == 0;
+    if (strncmp(argv[a], "mux", 3) == 0) mux = argv[a][3] == '=' ? atoi(argv[a] + 4) : 1;
   }
   wg_gpu_ctx *ctx = NULL;
 #ifndef GW_CPU
@@ -635,9 +636,18 @@ int main(int argc, char **argv) {
     free(wt);
     memset(slabs, 0, (size_t)3 * n * slot);  /* (the sent / received / decrypted regions) */
   }
-  mux_t mx = {gs, pairs, batch, gw_engine_of(gs[0].a), 0.0, 0.0};
+  if (mux > (int)pairs) mux = (int)pairs;
+  mux_t *mxs = calloc(mux > 0 ? mux : 1, sizeof *mxs);
+  gw_t **gps = calloc(pairs, sizeof *gps);
+  for (int w = 0, k = 0; w < mux; ++w) {  /* group w: pairs w, w + W, ... */
+    mxs[w].gp = gps + k;
+    for (uint32_t p = (uint32_t)w; p < pairs; p += (uint32_t)mux) gps[k++] = &gs[p];
+    mxs[w].pairs = (uint32_t)(gps + k - mxs[w].gp);
+    mxs[w].batch = batch;
+    mxs[w].e = gw_engine_of(gs[0].a);
+  }
   const double t0 = now();
-  pthread_t *th = calloc(3 * pairs, sizeof *th);
+  pthread_t *th = calloc(3 * pairs + 2 * (mux > 0 ? mux : 0), sizeof *th);
   uint32_t nth = 0;
   for (uint32_t p = 0; p < pairs; ++p) {
     pthread_create(&th[nth++], NULL, reader, &gs[p]);
@@ -646,14 +656,15 @@ int main(int argc, char **argv) {
       pthread_create(&th[nth++], NULL, sender, &gs[p]);
     }
   }
-  if (mux) {
-    pthread_create(&th[nth++], NULL, mux_decryptor, &mx);
-    pthread_create(&th[nth++], NULL, mux_sender, &mx);
+  for (int w = 0; w < mux; ++w) {
+    pthread_create(&th[nth++], NULL, mux_decryptor, &mxs[w]);
+    pthread_create(&th[nth++], NULL, mux_sender, &mxs[w]);
   }
   for (uint32_t k = 0; k < nth; ++k) pthread_join(th[k], NULL);
   uint32_t nrx = 0, nsent = 0;
   uint64_t bytes = 0;
-  double te = mx.t_encap, ts = 0, tw = 0, tr = 0, td = mx.t_decap;
+  double te = 0, ts = 0, tw = 0, tr = 0, td = 0;
+  for (int w = 0; w < mux; ++w) te += mxs[w].t_encap, td += mxs[w].t_decap;
   double t_end = t0;
   for (uint32_t p = 0; p < pairs; ++p) {
     gw_t *g = &gs[p];

@@ -93,7 +93,7 @@ def test_udp_gateway_64k_packets_match_sequential_tunn(tmp_path, torch_cuda, poo
     run_and_check(build(tmp_path), tmp_path, 65536, ["reg"] if pools == "reg" else [])
 
 
-@pytest.mark.parametrize("mode", [("1", []), ("3", ["mux"]), ("4", [])])
+@pytest.mark.parametrize("mode", [("1", []), ("3", ["mux"]), ("4", []), ("5", ["mux=2"])])
 def test_udp_gateway_cpu_backend_matches_sequential_tunn(tmp_path, mode):
     """The CPU line (OpenSSL in place of the GPU, same sockets and threads) obeys the
     same sequential-Tunn contract, so the two gateway lines do the same work -- with

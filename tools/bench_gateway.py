@@ -9,8 +9,8 @@ batch sizes (the reference's default is 50, packet_workers.rs:27).
 GW_PAIRS="1 2 4 8" also sweeps the number of independent peers (Tunn pairs,
 socket pairs and worker threads) sharing the N packets at each batch size;
 GW_REG="0 1" also runs each with the packet pools registered (the DMA path);
-GW_MUX="0 1" also runs the multi-peer worker shape ("mux": one encrypt and one decrypt
-worker whose batches mix the pairs, wg_tunn_*_multi); GW_BACKEND="gpu cpu" also runs the CPU line (OpenSSL in place of the GPU Tunn, the
+GW_MUX="0 1 4" also runs the multi-peer worker shape with that many worker groups ("mux=W":
+each group one encrypt and one decrypt worker whose batches mix its pairs, wg_tunn_*_multi); GW_BACKEND="gpu cpu" also runs the CPU line (OpenSSL in place of the GPU Tunn, the
 same sockets, threads and batches: examples/gw_cpu_tunn.h).
 """
 import json
@@ -51,7 +51,7 @@ def main():
         for be, b, p, reg, mx in runs:
             exe = exes[be]
             r = subprocess.run([exe, inp, os.path.join(d, "out.bin"), str(b), str(p)] + (["reg"] if reg else [])
-                               + (["mux"] if mx else []),
+                               + ([f"mux={mx}"] if mx else []),
                                capture_output=True, text=True, timeout=600)
             line = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {
                 "error": r.stderr[-300:], "batch": b, "pairs": p, "registered": reg, "backend": be, "mux": mx}
