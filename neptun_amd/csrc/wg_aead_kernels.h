@@ -97,6 +97,7 @@ template <bool kSeal> __global__ void aead_desc_affine_kernel(DescParams prm);
 // part of the chip; wg_gpu.cpp picks G from the batch size.
 constexpr uint32_t kXlaneThreads = 256;
 template <bool kSeal, uint32_t G> __global__ void aead_xlane_kernel(DescParams prm);
+template <bool kSeal, uint32_t G> __global__ void aead_xlane_strided_kernel(StridedParams prm);
 
 // wg_plan.hip: counting sort of a descriptor batch by rounds (longest first)
 constexpr uint32_t kPlanBins = 256;   // rounds 0..254, 255+ share the top bin

@@ -447,6 +447,27 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     prm.full_in = in_origin % 128u == 0 && src_stride % 128u == 0;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // small batches: the latency form (G lanes per packet, wg_xlane.hip), its group
+  // narrowed to the packets' blocks; not with slot padding (its kernels write no padding)
+  if (!prm.pad_tail) {
+    DescHint h;
+    h.max_len = len;
+    if (const uint32_t G = xlane_group_hinted(ctx, seal, n, h)) {
+      using K = void (*)(wg::StridedParams);
+      static const K kernels[2][6] = {  // [seal][64, 32, 16, 8, 4, 2]
+          {wg::aead_xlane_strided_kernel<false, 64>, wg::aead_xlane_strided_kernel<false, 32>,
+           wg::aead_xlane_strided_kernel<false, 16>, wg::aead_xlane_strided_kernel<false, 8>,
+           wg::aead_xlane_strided_kernel<false, 4>, wg::aead_xlane_strided_kernel<false, 2>},
+          {wg::aead_xlane_strided_kernel<true, 64>, wg::aead_xlane_strided_kernel<true, 32>,
+           wg::aead_xlane_strided_kernel<true, 16>, wg::aead_xlane_strided_kernel<true, 8>,
+           wg::aead_xlane_strided_kernel<true, 4>, wg::aead_xlane_strided_kernel<true, 2>}};
+      const uint32_t per_block = wg::kXlaneThreads / G;
+      hipLaunchKernelGGL(kernels[seal ? 1 : 0][6u - (uint32_t)__builtin_ctz(G)],
+                         dim3((n + per_block - 1u) / per_block), dim3(wg::kXlaneThreads), 0, s, prm);
+      WG_HIP(hipGetLastError(), "strided: launch");
+      return WG_RC_OK;
+    }
+  }
   const uint32_t full_waves = n / 64u;
   if (full_waves) {
     // persistent: kStridedBlocksPerCU resident workgroups per CU walk the

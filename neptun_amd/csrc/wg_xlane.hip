@@ -62,35 +62,30 @@ __device__ __forceinline__ F26 f26_zero() {
 
 }  // namespace
 
+// One packet on the G lanes of its group (l = the lane's index in the group): the
+// checks, the spread keystream / Poly1305 spans, the combine, the tag.  align: the
+// packet's offsets OR-ed (misaligned -> WG_STATUS_MISALIGNED); st: its status (or null).
 template <bool kSeal, uint32_t G>
-__global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams prm) {
-  static_assert(G >= 2u && G <= 64u && (G & (G - 1u)) == 0u, "group = power of two within a wave");
-  const uint32_t gid = blockIdx.x * (kXlaneThreads / G) + threadIdx.x / G;  // packet (batch position)
-  const uint32_t l = threadIdx.x & (G - 1u);
-  if (gid >= prm.n) return;  // (the whole group)
-  const uint32_t idx = prm.order ? prm.order[gid] : gid;
-  const wg_packet_desc d = prm.descs[idx];
-  // (null bases: the offsets are absolute device addresses)
-  const uint8_t *src = reinterpret_cast<const uint8_t *>(reinterpret_cast<uint64_t>(prm.src) + d.src_off);
-  uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uint64_t>(prm.dst) + d.dst_off);
-
+__device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uint8_t *dst, uint32_t len,
+                                             uint32_t slot, uint64_t counter, uint64_t align, int32_t *st,
+                                             const uint8_t *keys, const uint32_t *key_index, uint32_t key_slots) {
   int32_t status = WG_STATUS_OK;
-  if (!kSeal && d.key_slot == WG_KEY_SLOT_INVALID_PACKET) status = WG_STATUS_INVALID_PACKET;
-  else if (!kSeal && d.key_slot == WG_KEY_SLOT_NO_SESSION) status = WG_STATUS_NO_CURRENT_SESSION;
-  else if (d.key_slot >= prm.key_slots) status = WG_STATUS_BAD_KEY_SLOT;
-  else if (((d.src_off | d.dst_off) & 15u) != 0u) status = WG_STATUS_MISALIGNED;
-  else if (!kSeal && d.len < WG_DATA_OVERHEAD_SZ) status = WG_STATUS_INVALID_PACKET;  // mod.rs:170
+  if (!kSeal && slot == WG_KEY_SLOT_INVALID_PACKET) status = WG_STATUS_INVALID_PACKET;
+  else if (!kSeal && slot == WG_KEY_SLOT_NO_SESSION) status = WG_STATUS_NO_CURRENT_SESSION;
+  else if (slot >= key_slots) status = WG_STATUS_BAD_KEY_SLOT;
+  else if ((align & 15u) != 0u) status = WG_STATUS_MISALIGNED;
+  else if (!kSeal && len < WG_DATA_OVERHEAD_SZ) status = WG_STATUS_INVALID_PACKET;  // mod.rs:170
 
   uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t sidx = 0, n1 = 0, n2 = 0;
   if (status == WG_STATUS_OK) {
-    const uint4 a = ld16(prm.keys + 32u * d.key_slot), b = ld16(prm.keys + 32u * d.key_slot + 16u);
+    const uint4 a = ld16(keys + 32u * slot), b = ld16(keys + 32u * slot + 16u);
     key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
     key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
-    sidx = prm.key_index[d.key_slot];
+    sidx = key_index[slot];
     if (kSeal) {
-      n1 = (uint32_t)d.counter;
-      n2 = (uint32_t)(d.counter >> 32);
+      n1 = (uint32_t)counter;
+      n2 = (uint32_t)(counter >> 32);
     } else {
       const uint4 h = ld16(src);  // header: type, receiver_idx, counter (mod.rs:170-180)
       if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
@@ -100,11 +95,11 @@ __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams pr
     }
   }
   if (status != WG_STATUS_OK) {  // group-uniform: nothing of the packet is written
-    if (l == 0u) prm.status[idx] = status;
+    if (l == 0u && st) *st = status;
     return;
   }
 
-  const uint32_t P = kSeal ? d.len : d.len - WG_DATA_OVERHEAD_SZ;
+  const uint32_t P = kSeal ? len : len - WG_DATA_OVERHEAD_SZ;
   const uint8_t *in = kSeal ? src : src + WG_DATA_OFFSET;  // plaintext / ciphertext
   uint8_t *out = kSeal ? dst + WG_DATA_OFFSET : dst;      // ciphertext / plaintext
   const uint32_t NB = 1u + (P + 63u) / 64u;
@@ -225,7 +220,35 @@ __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams pr
       }
     }
   }
-  if (l == 0u) prm.status[idx] = status;
+  if (l == 0u && st) *st = status;
+}
+
+template <bool kSeal, uint32_t G>
+__global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams prm) {
+  static_assert(G >= 2u && G <= 64u && (G & (G - 1u)) == 0u, "group = power of two within a wave");
+  const uint32_t gid = blockIdx.x * (kXlaneThreads / G) + threadIdx.x / G;  // packet (batch position)
+  const uint32_t l = threadIdx.x & (G - 1u);
+  if (gid >= prm.n) return;  // (the whole group)
+  const uint32_t idx = prm.order ? prm.order[gid] : gid;
+  const wg_packet_desc d = prm.descs[idx];
+  // (null bases: the offsets are absolute device addresses)
+  const uint8_t *src = reinterpret_cast<const uint8_t *>(reinterpret_cast<uint64_t>(prm.src) + d.src_off);
+  uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uint64_t>(prm.dst) + d.dst_off);
+  xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, prm.status + idx,
+                         prm.keys, prm.key_index, prm.key_slots);
+}
+
+// Strided batches (wg_gpu_seal_strided / wg_gpu_open_strided without slot padding):
+// packet i at src + i src_stride / dst + i dst_stride, one length and key slot, seal
+// counter counter_base + i; the host has checked alignment and the slot
+template <bool kSeal, uint32_t G>
+__global__ __launch_bounds__(kXlaneThreads) void aead_xlane_strided_kernel(StridedParams prm) {
+  const uint32_t i = blockIdx.x * (kXlaneThreads / G) + threadIdx.x / G;
+  const uint32_t l = threadIdx.x & (G - 1u);
+  if (i >= prm.n) return;
+  xlane_packet<kSeal, G>(l, prm.src + (uint64_t)i * prm.src_stride, prm.dst + (uint64_t)i * prm.dst_stride, prm.len,
+                         prm.key_slot, prm.counter_base + i, 0u, prm.status ? prm.status + i : nullptr, prm.keys,
+                         prm.key_index, 0xffffffffu);
 }
 
 template __global__ void aead_xlane_kernel<true, 64>(DescParams);
@@ -240,5 +263,18 @@ template __global__ void aead_xlane_kernel<true, 4>(DescParams);
 template __global__ void aead_xlane_kernel<false, 4>(DescParams);
 template __global__ void aead_xlane_kernel<true, 2>(DescParams);
 template __global__ void aead_xlane_kernel<false, 2>(DescParams);
+
+template __global__ void aead_xlane_strided_kernel<true, 64>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<false, 64>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<true, 32>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<false, 32>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<true, 16>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<false, 16>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<true, 8>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<false, 8>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<true, 4>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<false, 4>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<true, 2>(StridedParams);
+template __global__ void aead_xlane_strided_kernel<false, 2>(StridedParams);
 
 }  // namespace wg

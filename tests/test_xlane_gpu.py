@@ -204,3 +204,43 @@ def test_xlane_ordered_launch_matches_unordered(torch_cuda, xl):
     torch.cuda.synchronize()
     assert (d_st.cpu().numpy() == 0).all()
     assert np.array_equal(d_dst.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("G", [64, 16, 2])
+@pytest.mark.parametrize("n,P", [(1, 0), (63, 1350), (64, 17), (200, 8192), (1000, 127)])
+def test_xlane_strided_matches_throughput_form_and_oracle(torch_cuda, xl, G, n, P):
+    """Strided batches take the latency form too (wg_xlane.hip aead_xlane_strided_kernel):
+    every byte of the destination buffer -- packets and the canary bytes around them --
+    equals the throughput kernels' output, the sampled datagrams equal the oracle's, and
+    the open restores every plaintext (status array optional, as the ABI allows)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(G * 7 + n + P)
+    keys = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+    kidx = np.array([0x1234567], np.uint32)
+    xl.set_keys(0, keys, kidx)
+    S = synth.round_up(P + 32 + 16 * int(rng.integers(0, 3)), 16)
+    src = torch.from_numpy(rng.integers(0, 256, n * S + 64, dtype=np.uint8)).cuda()
+    ctr0 = 2**32 - 5
+    outs = []
+    for lanes in (0, n * G):
+        xl.set_xlane_lanes(lanes)
+        w = torch.full((n * S + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        xl.seal_strided(n, P, 0, ctr0, src, S, w, S, st)
+        torch.cuda.synchronize()
+        assert (st.cpu().numpy() == 0).all()
+        outs.append(w)
+    assert torch.equal(outs[0], outs[1]), "latency-form seal differs from the throughput form"
+    got = outs[1].cpu().numpy()
+    s_np = src.cpu().numpy()
+    for i in sorted({0, n // 2, n - 1}):
+        want = o.format_packet_data(keys[0].tobytes(), int(kidx[0]), ctr0 + i, s_np[i * S:i * S + P].tobytes())
+        assert got[i * S:i * S + P + 32].tobytes() == want, i
+    back = torch.full((n * S + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+    xl.set_xlane_lanes(n * G)
+    xl.open_strided(n, P + 32, 0, outs[1], S, back, S, None)
+    torch.cuda.synchronize()
+    b = back.cpu().numpy()
+    for i in range(n):
+        assert b[i * S:i * S + P].tobytes() == s_np[i * S:i * S + P].tobytes(), i
+        assert (b[i * S + P:(i + 1) * S] == 0x5A).all(), i
