@@ -354,14 +354,14 @@ class Pool {
     j.n = n;
     j.parts = parts;
     j.left.store(parts, std::memory_order_relaxed);
-    bool wake;
+    unsigned wake;
     {
       std::lock_guard<std::mutex> lk(mu_);
       active_.push_back(&j);
       agen_.fetch_add(1, std::memory_order_release);
-      wake = sleepers_ > 0;
+      wake = std::min(sleepers_, parts - 1);  // (the spinning workers see agen_ change)
     }
-    if (wake) cv_.notify_all();
+    for (unsigned w = 0; w < wake; ++w) cv_.notify_one();
     // the caller's own parts first
     for (;;) {
       unsigned p;
@@ -1035,6 +1035,15 @@ bool dma_possible(wg_tunn *t, Engine &E, bool multi_ok = false);
 bool dma_runs() {  // (read per batch, like the other WG_TUNN_* knobs)
   const char *e = std::getenv("WG_TUNN_DMA");
   return !e || std::atoi(e) != 0;
+}
+// Registered encapsulate batches below this many packets take the zero-copy kernels on
+// the caller's memory instead of a DMA batch: the copy engine's per-batch setup and
+// completion cost more than the kernel's PCIe reads of a few MB (WG_TUNN_DMA_MIN,
+// default 8192; measured 25 vs 37 us at 64 packets, 358 vs 400 at 4096,
+// profiles/r05q_small_reg.jsonl).  Decapsulate measured no consistent gain.
+size_t dma_min_encap() {
+  const char *e = std::getenv("WG_TUNN_DMA_MIN");
+  return e ? (size_t)std::max(0L, std::atol(e)) : 8192u;
 }
 
 // Cut packets [a, b) with use(k) into runs: host(k) pointer, width(k) bytes,
@@ -2389,8 +2398,9 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
     int left = 1;  // run_dma's verdict: 1 nothing done, 2 the packets from E.k1 on are left
     // (encapsulate has no in-order decisions: every engine of a multi-GPU Tunn runs its
     // contiguous share as a DMA batch of its own, the counters reserved before the split)
-    if (!dma_possible(t, E, true)) grow_all();
-    if (dma_possible(t, E, true)) {
+    const bool dma_ok = dma_possible(t, E, true) && n >= dma_min_encap();
+    if (!dma_ok) grow_all();
+    if (dma_ok) {
       const bool all = registered(E.k0, E.k1);
       if (all) {
         make_chunks(E, size, 0, dma_ramp());

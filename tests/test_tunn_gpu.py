@@ -488,6 +488,7 @@ def test_multi_engine_registered_pools_match_sequential_tunn(torch_cuda, monkeyp
     from neptun_amd import GpuContext
     from neptun_amd.tunn import Tunn
     monkeypatch.setenv("WG_TUNN_DMA", "1")
+    monkeypatch.setenv("WG_TUNN_DMA_MIN", "0")  # (DMA batches for encapsulate at this size too)
     if out != "auto":
         monkeypatch.setenv("WG_TUNN_DMA_OUT", out)
     monkeypatch.setenv("WG_TUNN_CHUNK_KB", "2048")
@@ -662,6 +663,7 @@ def test_registered_slot_pools_match_sequential_tunn(gpu, monkeypatch, dma):
 
     import numpy as np
     monkeypatch.setenv("WG_TUNN_DMA", dma[0])
+    monkeypatch.setenv("WG_TUNN_DMA_MIN", "0")  # (DMA batches for encapsulate at this size too)
     if dma in ("1-scatter", "1-direct"):
         monkeypatch.setenv("WG_TUNN_DMA_OUT", dma[2:])
     if dma == "1-nested":
