@@ -10,17 +10,24 @@ the raw samples and a summary.  Read-only on the GPU (no settings changed).
 """
 import json
 import os
+import shutil
 import subprocess
+import sys
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+AMD_SMI = shutil.which("amd-smi") or "/opt/rocm/bin/amd-smi"
+
+
 def sample(gpu: int = 0):
     """One `amd-smi metric` reading of GPU `gpu` (amd-smi's index), read-only."""
     try:
-        out = subprocess.run(["amd-smi", "metric", "-g", str(gpu), "--json"], capture_output=True,
+        # (the interpreter runs the amd-smi script itself: its `#!/usr/bin/env` line is an
+        # exec, which a process the profiler's preload initialised for the GPU may not do)
+        out = subprocess.run([sys.executable, AMD_SMI, "metric", "-g", str(gpu), "--json"], capture_output=True,
                              text=True, timeout=20)
         return json.loads(out.stdout) if out.returncode == 0 else {"err": out.stderr[-300:]}
     except Exception as e:  # noqa: BLE001
