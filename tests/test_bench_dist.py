@@ -137,7 +137,8 @@ def _bench_cli(args, extra_env=None, timeout=120):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
-    env.update(BENCH_FAKE_DEVICE="tests.bench_fake", **(extra_env or {}))
+    env["BENCH_FAKE_DEVICE"] = "tests.bench_fake"
+    env.update(extra_env or {})
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], cwd=root, env=env,
                          capture_output=True, text=True, timeout=timeout)
     return out.returncode, [x for x in out.stdout.splitlines() if x.startswith("{")]
@@ -188,3 +189,19 @@ def test_gpus_flag_a_dead_rank_ends_the_run():
     rc, lines = _bench_cli(["--gpus", "2", *COMMON], extra_env={"FAKE_CRASH_RANK": "1"})
     assert rc != 0
     assert time.time() - t0 < 100
+
+
+@pytest.mark.gpu
+def test_gpus_flag_two_ranks_on_the_gpu(torch_cuda):
+    """The N-rank path with the real workload and HIP kernels: `bench.py --gpus 2` starts
+    two rank processes that both run on cuda:0 here (tests/bench_shared_gpu.py: a 1-GPU
+    box has one device), each sealing and opening its own shard with disjoint counters,
+    gloo carrying the barrier, max-over-ranks time and byte sums.  One line: n_gpus 2,
+    both ranks' telemetry, both shards verified, the packets summed."""
+    rc, lines = _bench_cli(["--gpus", "2", "--packets", "65536", *COMMON], timeout=300,
+                           extra_env={"BENCH_FAKE_DEVICE": "tests.bench_shared_gpu", "BENCH_FAKE_GPUS": "2"})
+    assert rc == 0 and len(lines) == 1, lines
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and len(line["per_rank"]) == 2
+    assert line["packets_per_step"] == 2 * 65536
+    assert "error" not in line and line.get("verified")
