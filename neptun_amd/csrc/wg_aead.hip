@@ -1640,11 +1640,22 @@ __device__ __forceinline__ void strided_body(const StridedParams &prm) {
     }
 #define WALK_STEP g_step
 #define WALK_END g_end
+    // spread: which of the workgroup's waves carry its share -- waves w and w + 4 share a
+    // SIMD, so a share of 5 or 6 waves doubles up on one or two SIMDs; rotating the live
+    // set by 2 on every other workgroup lets the two workgroups of a CU double up on
+    // different SIMDs (WG_SPREAD_ROT, wg_gpu.cpp: which workgroups are "every other")
+    uint32_t vwave = wave;
+    if (prm.spread >> 8) {
+      const uint32_t mode = prm.spread >> 8;
+      const uint32_t b = blockIdx.x;
+      const uint32_t odd = mode == 1u ? (b & 1u) : mode == 2u ? ((b >> 8) & 1u) : ((b >> 3) & 1u);
+      vwave = (wave + kWaves - 2u * odd) % kWaves;
+    }
     for (uint32_t grp = g_first; grp < g_end; grp += g_step) {
-      const uint32_t pkt0 = prm.spread ? (s_lo + wave) * 64u : (grp * kWaves + wave) * 64u;
+      const uint32_t pkt0 = prm.spread ? (s_lo + vwave) * 64u : (grp * kWaves + wave) * 64u;
       // only the last group can be partial, and it is this workgroup's last
       // iteration: a wave without packets ends (ended waves leave the barrier)
-      if (prm.spread ? s_lo + wave >= s_hi : pkt0 + 64u > prm.n) return;
+      if (prm.spread ? s_lo + vwave >= s_hi : pkt0 + 64u > prm.n) return;
 #if WG_OPEN_HDR_PREFETCH
       // open: this lane's datagram in the wave's next group (0: none), whose header
       // run_wave may prefetch into the tag park

@@ -228,6 +228,15 @@ int wg_gpu_set_keys(wg_gpu_ctx *ctx, uint32_t first_slot, uint32_t n, const uint
 // kernels): kStridedBlocksPerCU workgroups per CU walking workgroup-sized groups, or,
 // when the waves do not fill those slots, one workgroup per slot (at most one per
 // wave) with an even share each (`spread`, wg_aead_kernels.h WG_SPREAD)
+// WG_SPREAD_ROT: 0 none, 1 odd blockIdx, 2 blockIdx bit 8, 3 blockIdx bit 3 (A/B)
+static uint32_t spread_rot() {
+  static const uint32_t m = [] {
+    const char *e = std::getenv("WG_SPREAD_ROT");
+    return e ? (uint32_t)std::min(3, std::max(0, std::atoi(e))) : 0u;
+  }();
+  return m;
+}
+
 static dim3 persistent_grid(const wg_gpu_ctx *ctx, uint32_t waves, uint32_t &spread) {
   const uint32_t slots = ctx->cus * wg::kStridedBlocksPerCU, per_block = wg::kStridedThreads / 64u;
   if (WG_SPREAD && waves <= per_block * slots) {
@@ -473,6 +482,8 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     // persistent: kStridedBlocksPerCU resident workgroups per CU walk the
     // workgroup-sized packet groups (wg_aead.hip aead_strided_kernel)
     const dim3 grid = persistent_grid(ctx, full_waves, prm.spread);
+    // (strided kernels: the spread's live-wave rotation, wg_aead.hip strided_body)
+    if (prm.spread) prm.spread |= spread_rot() << 8;
     if (seal)
       hipLaunchKernelGGL((wg::aead_strided_kernel<true, false>), grid, dim3(wg::kStridedThreads),
                          0, s, prm);
