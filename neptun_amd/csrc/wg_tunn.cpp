@@ -144,9 +144,14 @@ inline uint64_t round128(uint64_t x) { return (x + 127) / 128 * 128; }
 // stores: the bytes are read next by the copy engines or the caller, not by this
 // core, and a streaming store skips the read-for-ownership of the destination
 // line (a third of a cached memcpy's DRAM traffic).  WG_TUNN_NT=0: memcpy.
-bool nt_copies() {
+// Streaming (non-temporal) stores for the host copies into and out of pinned staging:
+// they pay for batches far larger than the last-level cache and cost at smaller ones
+// (1350-B packets, staged: memcpy 40 vs 66-84 us at 64 packets, 1.7-2.0 vs 2.3 ms at
+// 16,384; streaming stores 150-158 vs 146-147 Gbit/s at 262,144; r05y / r05z).
+// WG_TUNN_NT=1 / 0 forces either; default: streaming from 32,768 packets on.
+bool nt_copies(size_t packets) {
   const char *e = std::getenv("WG_TUNN_NT");
-  return !e || std::atoi(e) != 0;
+  return e ? std::atoi(e) != 0 : packets >= 32768;
 }
 void copy_bytes(uint8_t *dst, const uint8_t *src, size_t n, bool nt) {
   if (!nt || n < 256) {
@@ -1556,7 +1561,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     t->sc->out_dma.resize(t->sc->sel.size(), 0);
     t->sc->spec.resize(t->sc->sel.size(), 0);
   };
-  const bool nt = nt_copies();
+  const bool nt = nt_copies(n_cap);
   std::atomic<uint64_t> rx{0};
   // what lands in dst from pinned staging (pt: the plaintext there), then finish
   auto copy_out = [&](Engine &E, const Chunk &ch, const uint8_t *h_out, const wg_packet_desc *h_desc) {
@@ -2375,7 +2380,7 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
   pc.checks_done();
   auto size = [&](size_t k) { return round128((uint64_t)src_len[t->sc->sel[k]] + WG_DATA_OVERHEAD_SZ); };
   split(t, size);
-  const bool nt = nt_copies();
+  const bool nt = nt_copies(n);
   const int rc = for_engines(t, [&](Engine &E) -> int {
     E.zc = zero_copy();
     // registered src and dst (one engine): the DMA batch -- plaintexts in as runs, the
