@@ -1041,12 +1041,12 @@ bool dma_runs() {  // (read per batch, like the other WG_TUNN_* knobs)
   const char *e = std::getenv("WG_TUNN_DMA");
   return !e || std::atoi(e) != 0;
 }
-// Registered encapsulate batches below this many packets take the zero-copy kernels on
-// the caller's memory instead of a DMA batch: the copy engine's per-batch setup and
-// completion cost more than the kernel's PCIe reads of a few MB (WG_TUNN_DMA_MIN,
-// default 8192; measured 25 vs 37 us at 64 packets, 358 vs 400 at 4096,
-// profiles/r05q_small_reg.jsonl).  Decapsulate measured no consistent gain.
-size_t dma_min_encap() {
+// Registered batches below this many packets take the zero-copy kernels on the caller's
+// memory instead of a DMA batch: the copy engine's per-batch setup and completion cost
+// more than the kernel's PCIe reads of a few MB (WG_TUNN_DMA_MIN, default 8192; 64 packets
+// encapsulate 25 vs 37 us, decapsulate 34 vs 43; 4096: 346-385 vs 346-384 and 384-446 vs
+// 445-476; equal at 16,384; profiles/r05q_small_reg.jsonl, r05ab_tunn_small_reg.jsonl).
+size_t dma_min() {
   const char *e = std::getenv("WG_TUNN_DMA_MIN");
   return e ? (size_t)std::max(0L, std::atol(e)) : 8192u;
 }
@@ -1677,7 +1677,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
   };
   auto dma_batch = [&](Engine &E) -> int {
     const double t_prep = now_us();
-    if (!multi_dma && (multi || !dma_possible(t, E) || !registered(E, E.k0, E.k1))) {
+    if (!multi_dma && (multi || n_cap < dma_min() || !dma_possible(t, E) || !registered(E, E.k0, E.k1))) {
       if (partial) {  // not for a DMA batch after all: the staged path takes the whole selection
         grow_all();
         split(t, size);
@@ -1823,7 +1823,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
   if (multi) {
     // registered pools on every engine's share: one DMA batch per engine (see multi_dma)
     split(t, size);
-    bool all = dma_runs();
+    bool all = dma_runs() && n_cap >= dma_min();
     for (size_t e = 0; all && e < t->eng.size(); ++e) {
       Engine &E = *t->eng[e];
       DevGuard g(E.device);
@@ -2403,7 +2403,7 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
     int left = 1;  // run_dma's verdict: 1 nothing done, 2 the packets from E.k1 on are left
     // (encapsulate has no in-order decisions: every engine of a multi-GPU Tunn runs its
     // contiguous share as a DMA batch of its own, the counters reserved before the split)
-    const bool dma_ok = dma_possible(t, E, true) && n >= dma_min_encap();
+    const bool dma_ok = dma_possible(t, E, true) && n >= dma_min();
     if (!dma_ok) grow_all();
     if (dma_ok) {
       const bool all = registered(E.k0, E.k1);
