@@ -153,6 +153,26 @@ bool nt_copies(size_t packets) {
   const char *e = std::getenv("WG_TUNN_NT");
   return e ? std::atoi(e) != 0 : packets >= 32768;
 }
+// The fewest packets worth a pool part of their own.  A blocked worker wakes tens of
+// microseconds late on a loaded host (workers block 20 us after their last part, and a
+// small call's GPU wait is longer than that), and a part it takes then holds up its
+// caller: steps that only read headers or write descriptors (a few ns per packet) split
+// from 2 x WG_TUNN_GRAIN_LIGHT (default 1024) packets; steps that copy payloads split
+// into parts of WG_TUNN_GRAIN_COPY (64) packets once a batch has WG_TUNN_COPY_SPLIT
+// (512) packets, and run on the caller below that (profiles/r05ai_*: 2-part copies were
+// the slowest form, 256 packets copy faster alone, 512+ faster on every worker).
+size_t env_count(const char *name, size_t dflt) {
+  const char *e = std::getenv(name);
+  return e ? (size_t)std::max(1L, std::atol(e)) : dflt;
+}
+size_t grain_light() {
+  static const size_t g = env_count("WG_TUNN_GRAIN_LIGHT", 1024);
+  return g;
+}
+size_t grain_copy(size_t n) {
+  static const size_t g = env_count("WG_TUNN_GRAIN_COPY", 64), split = env_count("WG_TUNN_COPY_SPLIT", 512);
+  return n < split ? std::max<size_t>(n, 1) : g;
+}
 void copy_bytes(uint8_t *dst, const uint8_t *src, size_t n, bool nt) {
   if (!nt || n < 256) {
     std::memcpy(dst, src, n);
@@ -348,7 +368,7 @@ class Pool {
   }
   unsigned size() const { return (unsigned)th_.size() + 1; }
   // (grain: the fewest items worth a part of their own)
-  void run(size_t n, const std::function<void(size_t, size_t)> &fn, size_t grain = 64) {
+  void run(size_t n, const std::function<void(size_t, size_t)> &fn, size_t grain) {
     const unsigned parts = (unsigned)std::min<size_t>(size(), std::max<size_t>(n / std::max<size_t>(grain, 1), 1));
     if (parts <= 1) {
       if (n) fn(0, n);
@@ -894,7 +914,7 @@ bool all_packets(Engine &E, size_t a, size_t b, Ok ok) {
     size_t ha = ~size_t(0), hb = ~size_t(0);
     for (size_t j = lo; j < hi && all.load(std::memory_order_relaxed); ++j)
       if (!ok(a + j, ha, hb)) all.store(false, std::memory_order_relaxed);
-  });
+  }, grain_light());
   return all.load();
 }
 template <class Ok>
@@ -1587,7 +1607,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
         if (a & kFinish) my_rx += finish(k, in_dst ? dst[i] : pt, P);
       }
       rx.fetch_add(my_rx, std::memory_order_relaxed);
-    });
+    }, grain_copy(ch.k1 - ch.k0));
     E.ph.copy_out_us += now_us() - a;
   };
   auto decide_range = [&](size_t k0, size_t k1, const int32_t *st) {
@@ -1741,7 +1761,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
             E.b_jobs[j] = t->sc->spec[k] ? Scatter{E.ddst[j], o, P, o + P, WG_AEAD_SIZE} : Scatter{0, 0, 0, 0, 0};
           }
         }
-      });
+      }, grain_light());
       return base ? reinterpret_cast<uint8_t *>(base) : d_out;
     };
     auto done = [&](const Chunk &ch, size_t j0) -> void {
@@ -1807,7 +1827,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
             S.h_desc[kk] = wg_packet_desc{E.off[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->sc->slot[k]};
           }
         }
-      });
+      }, direct ? grain_light() : grain_copy(ch.k1 - ch.k0));
     };
     // statuses are back: decide in packet order (the copies follow in unpack)
     auto mid = [&](const Chunk &ch, Staging &S) -> int {
@@ -2334,7 +2354,7 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
         // mod.rs:296-299 copies src into dst[16..] before looking at the session
         std::memcpy(dst[i] + WG_DATA_OFFSET, src[i], src_len[i]);
       }
-    });
+    }, grain_light());  // (payload copies only for packets not sent: rare)
     const size_t had = t->sc->sel.size();
     t->sc->sel.resize(had + (hi0 - lo0));
     t->sc->sel.resize(had + compact(
@@ -2432,7 +2452,7 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
                 E.b_jobs[j] = Scatter{E.ddst[j], (uint32_t)E.off[j], src_len[i] + WG_DATA_OVERHEAD_SZ, 0, 0};
               }
             }
-          });
+          }, grain_light());
           return base ? reinterpret_cast<uint8_t *>(base) : d_out;
         };
         auto done = [&](const Chunk &ch, size_t j0) {
@@ -2452,7 +2472,7 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
               my_tx += res[i].len;  // mod.rs:321
             }
             tx.fetch_add(my_tx, std::memory_order_relaxed);
-          });
+          }, grain_light());
           E.tx += tx.load();
           E.ph.copy_out_us += now_us() - a;
         };
@@ -2506,7 +2526,7 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
             S.h_desc[kk] = wg_packet_desc{E.off[j] + WG_DATA_OFFSET, E.off[j], ctr_of(k), src_len[i], slot_of(k)};
           }
         }
-      });
+      }, direct ? grain_light() : grain_copy(ch.k1 - ch.k0));
     };
     auto unpack = [&](const Chunk &ch, Staging &S) {
       const double a = now_us();
@@ -2524,7 +2544,7 @@ static int encap_impl(wg_tunn *t, wg_tunn *const *peer, uint32_t n, const uint8_
           res[i].kind = WG_TUNN_WRITE_TO_NETWORK;
           res[i].len = w;
         }
-      });
+      }, direct ? grain_light() : grain_copy(ch.k1 - ch.k0));
       for (size_t kk = 0; kk < ch.k1 - ch.k0; ++kk)  // mod.rs:321
         if (S.h_st[kk] == WG_STATUS_OK) E.tx += src_len[t->sc->sel[ch.k0 + kk]] + WG_DATA_OVERHEAD_SZ;
       E.ph.copy_out_us += now_us() - a;
@@ -2587,7 +2607,7 @@ static int decap_impl(wg_tunn *t, wg_tunn *const *peer, const std::vector<wg_tun
         t->sc->code[i] = (int32_t)(T->first_slot + 2 * (ridx % WG_N_SESSIONS));
         t->sc->ctr_all[i] = ld64(d + 8);
       }
-    });
+    }, grain_light());
     const size_t had = t->sc->sel.size();
     t->sc->sel.resize(had + (hi0 - lo0));
     t->sc->slot.resize(t->sc->sel.size());
