@@ -73,6 +73,14 @@ struct DescParams {
   int32_t *status;
   uint32_t n, key_slots;
   uint32_t spread;  // as StridedParams::spread (persistent descriptor kernels)
+  // latency form only (aead_xlane_kernel): when done_flag is set, the grid's last
+  // workgroup stores done_seq there (pinned host memory, system scope) once every
+  // workgroup's outputs and statuses are out; done_count is its arrival counter
+  // (device memory, 0 between launches).  The host spins on the word instead of an
+  // event (wg_tunn.cpp small zero-copy calls).
+  uint32_t *done_count = nullptr;
+  uint32_t *done_flag = nullptr;
+  uint32_t done_seq = 0;
 };
 
 template <bool kSeal, bool kTail> __global__ void aead_strided_kernel(StridedParams prm);

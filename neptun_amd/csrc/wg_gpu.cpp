@@ -284,6 +284,11 @@ static uint32_t xlane_group(const wg_gpu_ctx *ctx, uint32_t n) {
 struct DescHint {
   uint32_t max_len = 0;   // 0: unknown
   bool host_mem = false;
+  // a completion word the latency form stores when done (DescParams::done_flag); the
+  // launch sets *flagged when the chosen form does so (other forms leave it false)
+  uint32_t *done_count = nullptr, *done_flag = nullptr;
+  uint32_t done_seq = 0;
+  bool *flagged = nullptr;
 };
 
 // The latency form's group for a batch: the budget's G (xlane_group), narrowed to
@@ -315,7 +320,14 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
   wg::DescParams prm{ctx->d_keys, ctx->d_key_index, descs, order, src, dst, status, n,
                      ctx->key_slots, 0u};
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (hint.flagged) *hint.flagged = false;
   if (const uint32_t G = xlane_group_hinted(ctx, seal, n, hint)) {
+    if (hint.done_flag && hint.done_count) {
+      prm.done_count = hint.done_count;
+      prm.done_flag = hint.done_flag;
+      prm.done_seq = hint.done_seq;
+      if (hint.flagged) *hint.flagged = true;
+    }
     using K = void (*)(wg::DescParams);
     static const K kernels[2][6] = {  // [seal][64, 32, 16, 8, 4, 2]
         {wg::aead_xlane_kernel<false, 64>, wg::aead_xlane_kernel<false, 32>,
@@ -361,10 +373,15 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
 // Tunn-internal launch (wg_tunn.cpp) with the batch's longest packet and memory kind
 int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, uint32_t n,
                           const uint8_t *src, uint8_t *dst, int32_t *status, void *stream,
-                          uint32_t max_len, bool host_mem) {
+                          uint32_t max_len, bool host_mem, uint32_t *done_count, uint32_t *done_flag,
+                          uint32_t done_seq, bool *flagged) {
   DescHint h;
   h.max_len = max_len;
   h.host_mem = host_mem;
+  h.done_count = done_count;
+  h.done_flag = done_flag;
+  h.done_seq = done_seq;
+  h.flagged = flagged;
   return launch_desc(ctx, seal, descs, nullptr, n, src, dst, status, stream, h);
 }
 

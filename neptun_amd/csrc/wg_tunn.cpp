@@ -52,7 +52,9 @@ int wg_ctx_device(const wg_gpu_ctx *ctx);                   // wg_gpu.cpp
 bool wg_ctx_slot_padding(const wg_gpu_ctx *ctx);            // wg_gpu.cpp
 int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, uint32_t n,
                           const uint8_t *src, uint8_t *dst, int32_t *status, void *stream,
-                          uint32_t max_len, bool host_mem);  // wg_gpu.cpp
+                          uint32_t max_len, bool host_mem, uint32_t *done_count = nullptr,
+                          uint32_t *done_flag = nullptr, uint32_t done_seq = 0,
+                          bool *flagged = nullptr);  // wg_gpu.cpp
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out);  // wg_gpu.cpp
 
 // ---------------------------------------------------------------------------
@@ -604,6 +606,11 @@ struct Staging {
   uint32_t nsc = 0;            // ... that many scatter jobs (h_sc)
   uint8_t stage = 0;           // run_chunks: kIdle / kSubmitted / kOutputs / kReady
   unsigned host_flags = hipHostMallocDefault;  // + hipHostMallocNumaUser on NUMA-bound engines
+  // zero-copy chunks in the latency form: the kernel's completion word (pinned) and its
+  // workgroup counter (HBM); `flagged`: the chunk in flight stores done_seq there
+  uint32_t *h_flag = nullptr, *d_count = nullptr;
+  uint32_t done_seq = 0;
+  bool flagged = false;
 };
 
 void free_buffers(Staging &s) {
@@ -616,6 +623,9 @@ void free_buffers(Staging &s) {
   (void)hipFree(s.d_out);
   (void)hipFree(s.d_desc);
   (void)hipFree(s.d_st);
+  (void)hipHostFree(s.h_flag);
+  (void)hipFree(s.d_count);
+  s.h_flag = s.d_count = nullptr;
   s.h_in = s.h_out = s.d_in = s.d_out = nullptr;
   s.h_desc = s.d_desc = nullptr;
   s.h_sc = nullptr;
@@ -1141,6 +1151,37 @@ int injected_failure(size_t c) {
 // sets idle: work still queued on a set is waited for (its kernel may still be
 // writing the pinned staging a later reserve() would free) and `busy` cleared,
 // so the next batch starts from a clean pipeline.
+// Small zero-copy calls learn that their kernel is done from the kernel's own
+// completion word (a host spin: 6 us from launch for an empty kernel against 12 us
+// through hipEventSynchronize, profiles/r05am_launch_latency.json) -- chunks of at
+// most WG_TUNN_FLAG packets (default 128; 0: never).  Larger grids lose by it: every
+// workgroup's system-scope release writes back its L2 (4096 packets staged 518 against
+// 389 us, profiles/r05ao).  The event stays recorded behind the kernel: a word that has
+// not come after 200 us (a slow or failed launch) hands over to the event, so errors
+// surface.
+bool flag_completion(size_t packets) {
+  const char *e = std::getenv("WG_TUNN_FLAG");
+  return packets <= (e ? (size_t)std::max(0L, std::atol(e)) : 128u);
+}
+hipError_t wait_chunk(Staging &S) {
+  if (S.flagged) {
+    S.flagged = false;
+    const volatile uint32_t *f = S.h_flag;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+      if (*f == S.done_seq) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return hipSuccess;
+      }
+      if ((i & 255u) == 0u &&
+          std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() > 200)
+        break;
+      _mm_pause();
+    }
+  }
+  return hipEventSynchronize(S.done);
+}
+
 struct PipelineDrain {
   Engine &E;
   explicit PipelineDrain(Engine &e) : E(e) { drain(); }
@@ -1189,7 +1230,7 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
   auto stage_mid = [&](size_t c) -> int {
     Staging &S = E.st[c % sets];
     const double a = now_us();
-    TUNN_HIP(hipEventSynchronize(S.done), "tunn: chunk wait");
+    TUNN_HIP(wait_chunk(S), "tunn: chunk wait");
     E.ph.wait_us += now_us() - a;
     const int mr = (int)mid(E.chunks[c], S);
     if (mr == -2)
@@ -1254,9 +1295,20 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
       const uint8_t *in = abs_src ? nullptr : S.h_in;
       uint8_t *out = abs_dst ? nullptr : S.h_out;
       if (timed) TUNN_HIP(hipEventRecord(S.ev[1], S.stream), "tunn: event");
+      // (the latency form's completion word: the set's own, made on first use)
+      const bool word = !timed && flag_completion(m);
+      if (word && !S.h_flag) {
+        TUNN_HIP(hipHostMalloc((void **)&S.h_flag, 64, hipHostMallocCoherent), "tunn: completion word");
+        TUNN_HIP(hipMalloc((void **)&S.d_count, 64), "tunn: completion counter");
+        TUNN_HIP(hipMemsetAsync(S.d_count, 0, 64, S.stream), "tunn: completion counter");
+        *S.h_flag = 0;
+        S.done_seq = 0;
+      }
+      if (word) ++S.done_seq;
       // (the kernel reads the packets over PCIe: hint the latency form's choice)
       const int rc = wg_launch_desc_hinted(E.ctx, seal, S.h_desc, (uint32_t)m, in, out, S.h_st, S.stream,
-                                           max_desc_len(S.h_desc, m), true);
+                                           max_desc_len(S.h_desc, m), true, word ? S.d_count : nullptr,
+                                           word ? S.h_flag : nullptr, S.done_seq, &S.flagged);
       if (rc) return rc;
       if (timed) TUNN_HIP(hipEventRecord(S.ev[2], S.stream), "tunn: event");
     } else {

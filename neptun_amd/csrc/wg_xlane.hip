@@ -223,19 +223,40 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   if (l == 0u && st) *st = status;
 }
 
+// The grid's completion word (DescParams::done_flag): each wave waits for its own
+// stores (outputs and status) to be acknowledged, the workgroup meets at a barrier, and
+// its thread 0 arrives on done_count with a system-scope release (one L2 write-back per
+// workgroup; no acquire: nothing is read after it, and an acquire's L2 invalidate per
+// wave cost 1024-packet calls 50 us, profiles/r05an); the last to arrive resets the
+// counter for the stream's next launch and publishes seq.  (Thread-indexed addresses:
+// the counter and the word take vector memory operations.)
+__device__ __forceinline__ void grid_done(uint32_t *count, uint32_t *flag, uint32_t seq) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    const uint32_t prev = __hip_atomic_fetch_add(count + threadIdx.x, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (prev == gridDim.x - 1u) {
+      __hip_atomic_store(count + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flag + threadIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 template <bool kSeal, uint32_t G>
 __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams prm) {
   static_assert(G >= 2u && G <= 64u && (G & (G - 1u)) == 0u, "group = power of two within a wave");
   const uint32_t gid = blockIdx.x * (kXlaneThreads / G) + threadIdx.x / G;  // packet (batch position)
   const uint32_t l = threadIdx.x & (G - 1u);
-  if (gid >= prm.n) return;  // (the whole group)
-  const uint32_t idx = prm.order ? prm.order[gid] : gid;
-  const wg_packet_desc d = prm.descs[idx];
-  // (null bases: the offsets are absolute device addresses)
-  const uint8_t *src = reinterpret_cast<const uint8_t *>(reinterpret_cast<uint64_t>(prm.src) + d.src_off);
-  uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uint64_t>(prm.dst) + d.dst_off);
-  xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, prm.status + idx,
-                         prm.keys, prm.key_index, prm.key_slots);
+  if (gid < prm.n) {  // (the whole group)
+    const uint32_t idx = prm.order ? prm.order[gid] : gid;
+    const wg_packet_desc d = prm.descs[idx];
+    // (null bases: the offsets are absolute device addresses)
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(reinterpret_cast<uint64_t>(prm.src) + d.src_off);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uint64_t>(prm.dst) + d.dst_off);
+    xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, prm.status + idx,
+                           prm.keys, prm.key_index, prm.key_slots);
+  }
+  if (prm.done_flag) grid_done(prm.done_count, prm.done_flag, prm.done_seq);  // (kernel-uniform)
 }
 
 // Strided batches (wg_gpu_seal_strided / wg_gpu_open_strided without slot padding):

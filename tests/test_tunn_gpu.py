@@ -416,6 +416,60 @@ def test_registered_direct_batches_match_sequential_tunn(gpu, seed):
     tg.close()
 
 
+@pytest.mark.parametrize("word", ["1", "0"])
+def test_small_calls_back_to_back_match_sequential_tunn(gpu, monkeypatch, word):
+    """Many back-to-back calls of 1-64 packets (NepTUN's batch size): the latency form
+    on the caller's memory, whose completion the host takes from the kernel's own
+    completion word (WG_TUNN_FLAG=64: chunks of up to 64 packets) or from the event
+    (0).  Staged and registered calls alternate, so consecutive calls share the staging
+    sets' words and sequence numbers; every call equals the sequential model."""
+    import numpy as np
+    monkeypatch.setenv("WG_TUNN_FLAG", "64" if word == "1" else "0")
+    rng = random.Random(31 if word == "1" else 32)
+    tm, tg, sessions = make_pair(gpu, rng)
+    ctr_state = {}
+    regs = []
+    for call in range(120):
+        n = rng.choice([1, 2, 7, 16, 50, 64])
+        registered = call % 3 == 2
+        if call % 2 == 0:
+            srcs = [ipv4(rng, rng.choice([20, 64, 1350, rng.randrange(20, 1500)])) for _ in range(n)]
+            caps = [len(s) + 32 for s in srcs]
+            dm = [bytearray(b"\xee" * c) for c in caps]
+            res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dm)]
+            if registered:
+                a_src, a_dst = Arena(srcs, [0] * n), Arena([b""] * n, caps)
+                for a in (a_src, a_dst):
+                    gpu.register_host(*a.window())
+                    regs.append(a)
+                res_g = tg.encapsulate_ptrs(a_src.ptrs, a_src.lens, a_dst.ptrs, np.array(caps, np.uint32))
+                dg = [bytearray(a_dst.get(k, caps[k])) for k in range(n)]
+            else:
+                dg = [bytearray(b"\xee" * c) for c in caps]
+                res_g = tg.encapsulate_batch(srcs, dg)
+            check_same(res_g, res_m, dg, dm, f"encap call {call}")
+        else:
+            dgs = datagrams(rng, sessions, n, ctr_state)
+            caps = [max(len(d) - 16, 1) for d in dgs]
+            dm = [bytearray(b"\xee" * c) for c in caps]
+            res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+            if registered:
+                a_in, a_out = Arena(dgs, [0] * n), Arena([b""] * n, caps)
+                for a in (a_in, a_out):
+                    gpu.register_host(*a.window())
+                    regs.append(a)
+                res_g = tg.decapsulate_ptrs(a_in.ptrs, a_in.lens, a_out.ptrs, np.array(caps, np.uint32))
+                dg = [bytearray(a_out.get(k, caps[k])) for k in range(n)]
+            else:
+                dg = [bytearray(b"\xee" * c) for c in caps]
+                res_g = tg.decapsulate_batch(dgs, dg)
+            check_same(res_g, res_m, dg, dm, f"decap call {call}")
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    for a in regs:
+        gpu.unregister_host(a.window()[0])
+    tg.close()
+
+
 @pytest.mark.parametrize("chunk_kb", [None, "64"])
 def test_multi_engine_split_matches_sequential_tunn(torch_cuda, monkeypatch, chunk_kb):
     """wg_tunn_create_multi over two contexts on device 0 (the 1-GPU stand-in for

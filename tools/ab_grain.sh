@@ -4,7 +4,7 @@
 set -e
 TAG=${1:?}; shift
 mkdir -p gpurun_out/$TAG
-B="python tools/bench_tunn.py --sizes ${AB_SIZES:-16,64,128,256,512,1024,4096} --reps 30 --phase-timing"
+B="python tools/bench_tunn.py --sizes ${AB_SIZES:-16,64,128,256,512,1024,4096} --reps 30 ${AB_FLAGS---phase-timing}"
 for r in $(seq 1 ${AB_REPS:-2}); do
   for v in "$@"; do
     name=${v%%:*}; envs=${v#*:}
