@@ -289,6 +289,7 @@ struct DescHint {
   uint32_t *done_count = nullptr, *done_flag = nullptr;
   uint32_t done_seq = 0;
   bool *flagged = nullptr;
+  bool xlane_ok = true;  // false: the throughput forms only
 };
 
 // The latency form's group for a batch: the budget's G (xlane_group), narrowed to
@@ -298,7 +299,7 @@ struct DescHint {
 // cost more than the throughput form's whole-line loads beyond a few thousand
 // packets (Tunn staged batches of 16,384: 1.62 ms against 1.03, r05b_tunn_small).
 static uint32_t xlane_group_hinted(const wg_gpu_ctx *ctx, bool seal, uint32_t n, const DescHint &h) {
-  uint32_t G = xlane_group(ctx, n);
+  uint32_t G = h.xlane_ok ? xlane_group(ctx, n) : 0u;
   if (!G || (h.host_mem && n > 4096u)) return 0u;
   if (h.max_len) {
     const uint32_t P = seal ? h.max_len : (h.max_len > WG_DATA_OVERHEAD_SZ ? h.max_len - WG_DATA_OVERHEAD_SZ : 0u);
@@ -374,7 +375,7 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
 int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, uint32_t n,
                           const uint8_t *src, uint8_t *dst, int32_t *status, void *stream,
                           uint32_t max_len, bool host_mem, uint32_t *done_count, uint32_t *done_flag,
-                          uint32_t done_seq, bool *flagged) {
+                          uint32_t done_seq, bool *flagged, bool xlane_ok) {
   DescHint h;
   h.max_len = max_len;
   h.host_mem = host_mem;
@@ -382,6 +383,7 @@ int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *desc
   h.done_flag = done_flag;
   h.done_seq = done_seq;
   h.flagged = flagged;
+  h.xlane_ok = xlane_ok;
   return launch_desc(ctx, seal, descs, nullptr, n, src, dst, status, stream, h);
 }
 

@@ -54,7 +54,7 @@ int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *desc
                           const uint8_t *src, uint8_t *dst, int32_t *status, void *stream,
                           uint32_t max_len, bool host_mem, uint32_t *done_count = nullptr,
                           uint32_t *done_flag = nullptr, uint32_t done_seq = 0,
-                          bool *flagged = nullptr);  // wg_gpu.cpp
+                          bool *flagged = nullptr, bool xlane_ok = true);  // wg_gpu.cpp
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out);  // wg_gpu.cpp
 
 // ---------------------------------------------------------------------------
@@ -1499,8 +1499,11 @@ int run_dma(Engine &E, bool seal, double t_prep, size_t n_cap, InHost in_host, I
     // behind chunk c's kernel
     int rc = launch(c, S, qk);
     if (rc < 0)
+      // (decapsulate chunks keep the throughput open: the latency form's open cost
+      // 262,144-packet registered batches 280 -> 233 Gbit/s, where the seal gains 279 ->
+      // 296; profiles/r05ba)
       rc = wg_launch_desc_hinted(E.ctx, seal, E.b_desc + j0, (uint32_t)m, S.d_in, out_base, E.b_st + j0, qk,
-                                 max_desc_len(E.b_desc + j0, m), false);
+                                 max_desc_len(E.b_desc + j0, m), false, nullptr, nullptr, 0, nullptr, seal);
     if (rc) return rc;
     if (scatter) {
       if (split) {
@@ -1994,8 +1997,22 @@ void destroy_engine(Engine *E) {
   delete E;
 }
 
-// shared: the engine's pool (a lane), else the engine makes its own
-int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out, Pool *shared = nullptr) {
+// The HIP runtime spreads a process's streams over GPU_MAX_HW_QUEUES hardware queues
+// (default 4) in creation order, and kernels of one hardware queue run one after
+// another.  Every lane makes the same number of streams (a multiple of 4), so without
+// care st[0] -- the stream of every single-chunk call -- of all lanes shares one or two
+// queues: 8 concurrent 50-packet calls then ran on 2 queues, one after another
+// (profiles/r05av trace).  A lane therefore makes its streams in an order rotated by
+// its index, st[0] of lanes 0, 1, 2, 3 ... landing on consecutive queues.
+unsigned hw_queues() {
+  const char *e = std::getenv("GPU_MAX_HW_QUEUES");
+  return e && std::atoi(e) > 0 ? (unsigned)std::atoi(e) : 4u;
+}
+
+// shared: the engine's pool (a lane), else the engine makes its own; rot: the lane's
+// index (stream order, above)
+int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out, Pool *shared = nullptr,
+                unsigned rot = 0) {
   Engine *E = new (std::nothrow) Engine;
   if (!E) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: host alloc", hipSuccess);
   E->ctx = ctx;
@@ -2009,25 +2026,25 @@ int make_engine(wg_gpu_ctx *ctx, bool multi, unsigned engines, Engine **out, Poo
     for (auto &S : E->st) S.host_flags = E->numa >= 0 ? hipHostMallocNumaUser : hipHostMallocDefault;
   }
   DevGuard g(E->device);
-  for (auto &S : E->st) {
-    hipError_t e = hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&S.done2, hipEventDisableTiming);
-    if (e != hipSuccess) {
+  std::vector<hipStream_t *> streams;  // (st[0] first, then the rest, rotated below)
+  for (auto &S : E->st) streams.push_back(&S.stream);
+  streams.push_back(&E->aux.stream);
+  for (hipStream_t &q : E->dq) streams.push_back(&q);
+  const size_t ns = streams.size(), r = rot % hw_queues() % ns;
+  for (size_t j = 0; j < ns; ++j)  // st[0] is made r-th
+    if (const hipError_t e = hipStreamCreateWithFlags(streams[(j + ns - r) % ns], hipStreamNonBlocking);
+        e != hipSuccess) {
       destroy_engine(E);
       return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", e);
     }
-  }
-  if (hipStreamCreateWithFlags(&E->aux.stream, hipStreamNonBlocking) != hipSuccess) {
-    destroy_engine(E);
-    return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", hipGetLastError());
-  }
-  for (hipStream_t &q : E->dq)
-    if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) {
-      q = nullptr;
+  for (auto &S : E->st) {
+    hipError_t e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&S.done2, hipEventDisableTiming);
+    if (e != hipSuccess) {
       destroy_engine(E);
-      return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: stream", hipGetLastError());
+      return wg_pipe_fail(WG_RC_HIP_ERROR, "tunn_create: event", e);
     }
+  }
   if (!shared) E->pool = new (std::nothrow) Pool(pool_workers(engines), E->numa);
   if (multi && E->pool) E->driver = new (std::nothrow) Driver(E->numa);
   if (!E->pool || (multi && !E->driver)) {
@@ -2057,7 +2074,7 @@ int lane_acquire(wg_engine *g, Engine **out) {
     }
     if (g->lanes.size() < g->max_lanes) {
       Engine *E = nullptr;
-      if (const int rc = make_engine(g->ctx, false, 1, &E, g->pool)) return rc;
+      if (const int rc = make_engine(g->ctx, false, 1, &E, g->pool, (unsigned)g->lanes.size())) return rc;
       g->lanes.push_back(E);
       *out = E;
       return WG_RC_OK;

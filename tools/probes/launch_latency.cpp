@@ -7,10 +7,14 @@
 //   flag_wv    hipStreamWriteValue32 to pinned host memory after the kernel; host spins
 //   graph      a one-node hipGraph, hipGraphLaunch + hipStreamSynchronize
 // Each: 2000 calls after 200 warm-up, median and p90 in microseconds, one JSON line.
+// Then the aggregate rate of T threads (1 .. 16), each on its own stream: "mt_flag" =
+// launch + spin on the thread's own word per call; "mt_async" = launches only, one
+// stream synchronize at the end (the dispatch rate).
 //   hipcc --offload-arch=gfx950 -O2 launch_latency.cpp -o launch_latency
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <thread>
 #include <chrono>
 #include <cstdio>
 #include <vector>
@@ -102,6 +106,41 @@ int main() {
     if (hipGraphLaunch(ge, s) != hipSuccess) return 1;
     return hipStreamSynchronize(s) != hipSuccess ? 1 : 0;
   }, true);
+  // T threads, each with its own stream and word
+  for (int mode = 0; mode < 2; ++mode) {
+    printf(", \"%s\": {", mode ? "mt_async" : "mt_flag");
+    for (int T : {1, 2, 4, 8, 16}) {
+      std::vector<std::thread> th;
+      std::vector<int> bad(T, 0);
+      const int calls = 4000;
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+          hipStream_t q;
+          if (hipStreamCreateWithFlags(&q, hipStreamNonBlocking) != hipSuccess) { bad[t] = 1; return; }
+          uint32_t *word = dflag + 16 * (t + 1);  // (own 64-byte line)
+          volatile uint32_t *hw = flag + 16 * (t + 1);
+          *hw = 0;
+          for (int i = 1; i <= calls && !bad[t]; ++i) {
+            if (mode == 0) {
+              hipLaunchKernelGGL(flag_kernel, dim3(1), dim3(64), 0, q, word, (uint32_t)i);
+              const auto w0 = std::chrono::steady_clock::now();
+              while (*hw != (uint32_t)i)
+                if (us_since(w0) > 1e6) { bad[t] = 1; break; }
+            } else {
+              hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, q, nullptr);
+            }
+          }
+          if (hipStreamSynchronize(q) != hipSuccess) bad[t] = 1;
+          (void)hipStreamDestroy(q);
+        });
+      for (auto &x : th) x.join();
+      const double us = us_since(t0);
+      for (int b : bad) rc |= b;
+      printf("\"%d\": %.0f%s", T, T * calls / us * 1e3, T == 16 ? "" : ", ");  // kcalls/s
+    }
+    printf("}");
+  }
   printf("}\n");
   CHECK(hipStreamSynchronize(s));
   CHECK(hipGraphExecDestroy(ge));
