@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Gateway sweep table: best-of-runs socket_to_socket_gbps per (registered, batch, pairs) and variant.
-    python tools/gw_table.py DIR variant1,variant2   (files DIR/VARIANT_R.jsonl)"""
+"""Gateway sweep table: socket_to_socket_gbps per (backend, registered, batch, pairs) and
+variant, the best of the runs (or their median with --median).
+    python tools/gw_table.py DIR variant1,variant2 [--median]   (files DIR/VARIANT_R.jsonl)"""
 import collections
 import glob
 import json
+import statistics
 import sys
 
 d = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -19,5 +21,6 @@ print("backend reg batch  " + "  ".join(f"{n:>{6 * len(pairs)}}" for n in names)
 for k in sorted(d):
     cells = []
     for n in names:
-        cells.append("".join("%6.1f" % max(d[k][(n, p)]) if d[k][(n, p)] else "     -" for p in pairs))
+        agg = statistics.median if "--median" in sys.argv else max
+        cells.append("".join("%6.1f" % agg(d[k][(n, p)]) if d[k][(n, p)] else "     -" for p in pairs))
     print("%-7s %3d %5d  " % k + "  ".join(cells))
