@@ -3,8 +3,8 @@
 sequential Tunn model -- TEST INFRASTRUCTURE (imports oracle/, like tests/).
 
 Each round draws a batch size (1 .. 40,000, skewed small; the early start takes >= 16,384),
-a slot size, an output mode (WG_TUNN_DMA_OUT direct / scatter / default), chunk size and
-stream form, encapsulates a batch of mostly-1350-byte packets from registered slots and
+a slot size, an output mode (WG_TUNN_DMA_OUT direct / scatter / default), chunk size,
+stream form and completion-word policy (WG_TUNN_FLAG), encapsulates a batch of mostly-1350-byte packets from registered slots and
 decapsulates the peer's traffic with replays, too-old counters, tampered tags, forged-
 then-real counters, wrong indices and keepalives -- with destination slots on 128-byte
 lines, 16 bytes past one, or 8 bytes off 16-byte alignment (each output mode's case) or one dst
@@ -49,7 +49,10 @@ def main():
         env = {"WG_TUNN_DMA_OUT": rng.choice(["direct", "scatter", ""]),
                "WG_TUNN_CHUNK_KB": rng.choice(["", "2048", "8192", "65536"]),
                "WG_TUNN_DMA_STREAMS": rng.choice(["", "0"]),
-               "WG_TUNN_SETS": rng.choice(["", "3"])}
+               "WG_TUNN_SETS": rng.choice(["", "3"]),
+               # the kernel's completion word: default (chunks <= 128 packets), never,
+               # or every zero-copy latency-form chunk (grids of up to 4096 packets)
+               "WG_TUNN_FLAG": rng.choice(["", "0", "4096"])}
         for k, v in env.items():
             if v:
                 os.environ[k] = v
