@@ -611,6 +611,7 @@ struct Staging {
   uint32_t *h_flag = nullptr, *d_count = nullptr;
   uint32_t done_seq = 0;
   bool flagged = false;
+  bool evented = true;  // `done` was recorded behind the chunk in flight
 };
 
 void free_buffers(Staging &s) {
@@ -1163,6 +1164,11 @@ bool flag_completion(size_t packets) {
   const char *e = std::getenv("WG_TUNN_FLAG");
   return packets <= (e ? (size_t)std::max(0L, std::atol(e)) : 128u);
 }
+// (WG_TUNN_WORD_EVENT=1: record the chunk's event behind a word-completed kernel too)
+bool word_event() {
+  const char *e = std::getenv("WG_TUNN_WORD_EVENT");
+  return e && std::atoi(e) != 0;
+}
 hipError_t wait_chunk(Staging &S) {
   if (S.flagged) {
     S.flagged = false;
@@ -1179,7 +1185,7 @@ hipError_t wait_chunk(Staging &S) {
       _mm_pause();
     }
   }
-  return hipEventSynchronize(S.done);
+  return S.evented ? hipEventSynchronize(S.done) : hipStreamSynchronize(S.stream);
 }
 
 struct PipelineDrain {
@@ -1283,7 +1289,7 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
     const size_t m = ch.k1 - ch.k0;
     const double pa = now_us();
     TUNN_HIP(reserve(S, (abs_src && abs_dst) ? 128 : ch.bytes + 128, m), "tunn: staging");
-    S.in_dma = S.out_dma = S.defer_out = false;
+    S.in_dma = S.out_dma = S.defer_out = S.flagged = false;
     const bool timed = E.timing;
     if (timed && !S.ev[0])
       for (auto &e : S.ev) TUNN_HIP(hipEventCreate(&e), "tunn: timing event");
@@ -1330,7 +1336,9 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
                "tunn: status D2H");
       if (timed) TUNN_HIP(hipEventRecord(S.ev[3], S.stream), "tunn: event");
     }
-    TUNN_HIP(hipEventRecord(S.done, S.stream), "tunn: event");
+    // (a chunk on the completion word needs no event: its fallback syncs the stream)
+    if (!S.flagged || word_event()) TUNN_HIP(hipEventRecord(S.done, S.stream), "tunn: event");
+    S.evented = !S.flagged || word_event();
     S.busy = true;
     S.stage = kSubmitted;
     S.timed = timed;

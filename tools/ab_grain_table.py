@@ -1,7 +1,9 @@
 import json,sys,glob,collections,statistics as st
 d=collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(sys.argv[1]+'/*.jsonl'):
-    name,mode,r=f.split('/')[-1][:-6].rsplit('_',2)
+    parts=f.split('/')[-1][:-6].rsplit('_',2)
+    if len(parts)!=3 or parts[1] not in ('reg','staged'): continue
+    name,mode,r=parts
     for l in open(f):
         if l.startswith('{'):
             x=json.loads(l); assert x['verified']
