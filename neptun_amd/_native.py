@@ -13,6 +13,9 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libneptun_gpu.so")
+# the same library with the latency form's accesses bounds-checked (Makefile CHECKED):
+# test infrastructure for that form's audit, never the product path
+CHECKED_LIB_PATH = os.path.join(_HERE, "libneptun_gpu_checked.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "neptun_gpu.h")
 
 
@@ -20,7 +23,7 @@ class NeptunGpuError(RuntimeError):
     pass
 
 
-_lib: ctypes.CDLL | None = None
+_libs: dict[str, ctypes.CDLL] = {}
 
 
 def header_functions(path: str = HEADER_PATH) -> list[str]:
@@ -30,15 +33,16 @@ def header_functions(path: str = HEADER_PATH) -> list[str]:
     return sorted(set(re.findall(r"\b(wg_[a-z0-9_]+)\s*\(", text)))
 
 
-def load() -> ctypes.CDLL:
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """The library at `path` (default: the product), bound and checked against the
+    tree's sources; loaded once per path."""
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
         raise NeptunGpuError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (or `make -C neptun_amd/csrc`)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     c = ctypes
     vp, u32, u64, i32 = c.c_void_p, c.c_uint32, c.c_uint64, c.c_int32
     L.wg_gpu_abi_version.restype = c.c_int
@@ -76,6 +80,8 @@ def load() -> ctypes.CDLL:
     L.wg_gpu_pipe_open_strided.argtypes = [vp, u32, u32, u32, vp, u64, vp, u64, vp]
     L.wg_gpu_seal_strided.argtypes = [vp, u32, u32, u32, u64, vp, u64, vp, u64, vp, vp]
     L.wg_gpu_open_strided.argtypes = [vp, u32, u32, u32, vp, u64, vp, u64, vp, vp]
+    L.wg_gpu_debug_xlane_check.argtypes = [c.POINTER(c.c_ulonglong), c.c_int]
+    L.wg_gpu_debug_xlane_check.restype = c.c_int
     for name in header_functions():
         fn = getattr(L, name)
         if fn.restype is c.c_int and name not in ("wg_gpu_abi_version",):
@@ -84,9 +90,9 @@ def load() -> ctypes.CDLL:
     got = L.wg_gpu_build_id().decode()
     if want is not None and got != want:
         raise NeptunGpuError(
-            f"{LIB_PATH} was built from other sources (build id {got}, tree {want}): rebuild it with "
+            f"{path} was built from other sources (build id {got}, tree {want}): rebuild it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C neptun_amd/csrc`)")
-    _lib = L
+    _libs[path] = L
     return L
 
 
@@ -100,6 +106,8 @@ def source_build_id() -> str | None:
     if not os.path.isdir(CSRC):
         return None
     inc = os.path.join(os.path.dirname(_HERE), "include")
+    if not os.path.isdir(inc):
+        return None
     names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h")))
     files = [os.path.join(CSRC, f) for f in names] + [os.path.join(CSRC, "Makefile")]
     files += [os.path.join(inc, f) for f in sorted(os.listdir(inc)) if f.endswith(".h")]
@@ -110,7 +118,7 @@ def source_build_id() -> str | None:
     return h.hexdigest()[:16]
 
 
-def check(rc: int, what: str) -> None:
+def check(rc: int, what: str, lib: ctypes.CDLL | None = None) -> None:
     if rc != 0:
-        msg = load().wg_gpu_last_error().decode(errors="replace")
+        msg = (lib or load()).wg_gpu_last_error().decode(errors="replace")
         raise NeptunGpuError(f"{what} failed (rc={rc}): {msg}")

@@ -34,6 +34,9 @@ struct wg_gpu_ctx {
     uint64_t host, bytes, dev;
   };
   std::vector<Range> reg;          // registered host memory, sorted by host address
+  // key-slot ranges [first, first + count) held by Tunns (wg_tunn.cpp): a Tunn's
+  // install_session writes its slots, so two Tunns may never share one
+  std::vector<std::pair<uint32_t, uint32_t>> claims;
   std::mutex mu;                   // serialises key-table and route-table updates
 };
 
@@ -84,6 +87,26 @@ struct DeviceGuard {
 int wg_pipe_fail(int rc, const char *what, hipError_t e) { return fail(rc, what, e); }
 int wg_ctx_device(const wg_gpu_ctx *ctx) { return ctx->device; }
 bool wg_ctx_slot_padding(const wg_gpu_ctx *ctx) { return ctx->pad_slots; }
+// a Tunn's key slots: claimed at create (an overlap with a live Tunn's range on this
+// context is refused), released at destroy
+int wg_ctx_claim_slots(wg_gpu_ctx *ctx, uint32_t first, uint32_t count) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if ((uint64_t)first + count > ctx->key_slots)
+    return fail(WG_RC_INVALID_ARGUMENT, "tunn_create: needs 16 key slots");
+  for (const auto &c : ctx->claims)
+    if (first < c.first + c.second && c.first < first + count)
+      return fail(WG_RC_INVALID_ARGUMENT, "tunn_create: key slots overlap another Tunn's on this context");
+  ctx->claims.emplace_back(first, count);
+  return WG_RC_OK;
+}
+void wg_ctx_release_slots(wg_gpu_ctx *ctx, uint32_t first) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  for (size_t k = 0; k < ctx->claims.size(); ++k)
+    if (ctx->claims[k].first == first) {
+      ctx->claims.erase(ctx->claims.begin() + (long)k);
+      return;
+    }
+}
 // snapshot of the registered ranges as (host, bytes, dev) triples, sorted by host
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out) {
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -197,7 +220,8 @@ int wg_gpu_ctx_destroy(wg_gpu_ctx *ctx) {
   (void)hipFree(ctx->d_keys);
   (void)hipFree(ctx->d_key_index);
   (void)hipFree(ctx->d_route);
-  for (const auto &r : ctx->reg) (void)hipHostUnregister(reinterpret_cast<void *>(r.host));
+  // (through the shared pins: another context may still hold the same range)
+  for (const auto &r : ctx->reg) (void)pin_release(r.host);
   delete ctx;
   return WG_RC_OK;
 }

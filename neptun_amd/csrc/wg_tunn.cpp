@@ -56,6 +56,8 @@ int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *desc
                           uint32_t *done_flag = nullptr, uint32_t done_seq = 0,
                           bool *flagged = nullptr, bool xlane_ok = true);  // wg_gpu.cpp
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out);  // wg_gpu.cpp
+int wg_ctx_claim_slots(wg_gpu_ctx *ctx, uint32_t first, uint32_t count);  // wg_gpu.cpp
+void wg_ctx_release_slots(wg_gpu_ctx *ctx, uint32_t first);              // wg_gpu.cpp
 
 // ---------------------------------------------------------------------------
 // replay window: ReceivingKeyCounterValidator, session.rs:40-157
@@ -1923,7 +1925,9 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
         verdict[e] = r;
         return r == 1 ? WG_RC_OK : r;
       });
-      defer_done = false;
+      // (a verdict-1 share re-runs as the staged pipeline: dma_batch must then decline
+      // it at once rather than build its chunks and runs again)
+      defer_done = multi_dma = false;
       // in packet order: each engine's DMA chunks, or -- a share whose input could not
       // move as runs (verdict 1) -- the staged pipeline on the caller, deciding inline
       for (size_t e = 0; !rc && e < t->eng.size(); ++e) {
@@ -2168,6 +2172,10 @@ int tunn_attach(wg_engine *g, uint32_t first_slot, wg_tunn **out) {
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "tunn_create: needs 16 key slots", hipSuccess);
   wg_tunn *t = new (std::nothrow) wg_tunn;
   if (!t) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn_create: host alloc", hipSuccess);
+  if (const int rc = wg_ctx_claim_slots(g->ctx, first_slot, 2 * WG_N_SESSIONS)) {
+    delete t;
+    return rc;
+  }
   t->first_slot = first_slot;
   t->group = g;
   std::lock_guard<std::mutex> lk(g->mu);
@@ -2255,7 +2263,11 @@ int wg_tunn_create_multi(wg_gpu_ctx *const *ctxs, uint32_t nctx, uint32_t first_
   t->first_slot = first_slot;
   for (uint32_t e = 0; e < nctx; ++e) {
     Engine *E = nullptr;
-    const int rc = make_engine(ctxs[e], nctx > 1, nctx, &E);
+    int rc = make_engine(ctxs[e], nctx > 1, nctx, &E);
+    if (!rc) {
+      rc = wg_ctx_claim_slots(ctxs[e], first_slot, 2 * WG_N_SESSIONS);
+      if (rc) destroy_engine(E);
+    }
     if (rc) {
       wg_tunn_destroy(t);
       return rc;
@@ -2291,6 +2303,7 @@ int wg_tunn_create(wg_gpu_ctx *ctx, uint32_t first_slot, wg_tunn **out) {
 int wg_tunn_destroy(wg_tunn *t) {
   if (!t) return WG_RC_OK;
   if (wg_engine *g = t->group) {
+    wg_ctx_release_slots(g->ctx, t->first_slot);
     std::lock_guard<std::mutex> dl(g_default_mu);
     bool last;
     {
@@ -2306,7 +2319,10 @@ int wg_tunn_destroy(wg_tunn *t) {
       engine_free(g);
     }
   } else {
-    for (Engine *E : t->eng) destroy_engine(E);
+    for (Engine *E : t->eng) {
+      wg_ctx_release_slots(E->ctx, t->first_slot);
+      destroy_engine(E);
+    }
   }
   delete t;
   return WG_RC_OK;

@@ -36,8 +36,50 @@
 #include "wg_aead_kernels.h"
 #include "wg_crypto.h"
 
+// Checked build (WG_XLANE_CHECK=1 -> neptun_amd/libneptun_gpu_checked.so, the
+// tests' bounds audit of this form): every global access of a packet is checked
+// against that packet's own extents -- input [src, src + round_up(in bytes, 16)),
+// output [dst, dst + out bytes) -- and a stray one is counted (first address,
+// packet and lane kept) and not made.  wg_gpu_debug_xlane_check reads the record.
+#ifndef WG_XLANE_CHECK
+#define WG_XLANE_CHECK 0
+#endif
+
 namespace wg {
+#if WG_XLANE_CHECK
+__device__ unsigned long long g_xlane_check[4];  // violations, first address, its packet, its lane
+#endif
 namespace {
+
+// a packet's extents (checked build) and who it is
+struct XBounds {
+  uint64_t in_lo, in_hi, out_lo, out_hi;
+  uint32_t pkt, lane;
+};
+
+__device__ __forceinline__ bool xok(uint64_t a, uint32_t bytes, uint64_t lo, uint64_t hi, const XBounds &B) {
+#if WG_XLANE_CHECK
+  if (a >= lo && a + bytes <= hi) return true;
+  if (atomicAdd(&g_xlane_check[0], 1ull) == 0ull) {
+    atomicExch(&g_xlane_check[1], (unsigned long long)a);
+    atomicExch(&g_xlane_check[2], (unsigned long long)B.pkt);
+    atomicExch(&g_xlane_check[3], (unsigned long long)B.lane);
+  }
+  return false;
+#else
+  (void)a; (void)bytes; (void)lo; (void)hi; (void)B;
+  return true;
+#endif
+}
+__device__ __forceinline__ uint4 xld16(const uint8_t *p, const XBounds &B) {
+  return xok((uint64_t)p, 16u, B.in_lo, B.in_hi, B) ? ld16(p) : make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void xst16(uint8_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d, const XBounds &B) {
+  if (xok((uint64_t)p, 16u, B.out_lo, B.out_hi, B)) st16(p, a, b, c, d);
+}
+__device__ __forceinline__ void xstore_partial(uint8_t *p, const uint32_t w[4], int k, const XBounds &B) {
+  if (xok((uint64_t)p, (uint32_t)k, B.out_lo, B.out_hi, B)) store_partial(p, w, k);
+}
 
 // value of lane `src` (0 .. G-1) of this lane's group
 template <uint32_t G>
@@ -68,7 +110,8 @@ __device__ __forceinline__ F26 f26_zero() {
 template <bool kSeal, uint32_t G>
 __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uint8_t *dst, uint32_t len,
                                              uint32_t slot, uint64_t counter, uint64_t align, int32_t *st,
-                                             const uint8_t *keys, const uint32_t *key_index, uint32_t key_slots) {
+                                             const uint8_t *keys, const uint32_t *key_index, uint32_t key_slots,
+                                             uint32_t pkt) {
   int32_t status = WG_STATUS_OK;
   if (!kSeal && slot == WG_KEY_SLOT_INVALID_PACKET) status = WG_STATUS_INVALID_PACKET;
   else if (!kSeal && slot == WG_KEY_SLOT_NO_SESSION) status = WG_STATUS_NO_CURRENT_SESSION;
@@ -76,6 +119,10 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   else if ((align & 15u) != 0u) status = WG_STATUS_MISALIGNED;
   else if (!kSeal && len < WG_DATA_OVERHEAD_SZ) status = WG_STATUS_INVALID_PACKET;  // mod.rs:170
 
+  // (seal: plaintext in, datagram out; open: datagram in, plaintext out)
+  const uint32_t in_bytes = (len + 15u) & ~15u;
+  const uint32_t out_bytes = kSeal ? len + WG_DATA_OVERHEAD_SZ : (len >= WG_DATA_OVERHEAD_SZ ? len - WG_DATA_OVERHEAD_SZ : 0u);
+  const XBounds B{(uint64_t)src, (uint64_t)src + in_bytes, (uint64_t)dst, (uint64_t)dst + out_bytes, pkt, l};
   uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t sidx = 0, n1 = 0, n2 = 0;
   if (status == WG_STATUS_OK) {
@@ -87,7 +134,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       n1 = (uint32_t)counter;
       n2 = (uint32_t)(counter >> 32);
     } else {
-      const uint4 h = ld16(src);  // header: type, receiver_idx, counter (mod.rs:170-180)
+      const uint4 h = xld16(src, B);  // header: type, receiver_idx, counter (mod.rs:170-180)
       if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
       else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
       n1 = h.z;
@@ -125,9 +172,9 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
           w[j] &= byte_mask((int)valid, j);
           c[j] &= byte_mask((int)valid, j);
         }
-        store_partial(out + o, w, (int)valid);
+        xstore_partial(out + o, w, (int)valid, B);
       } else {
-        st16(out + o, w[0], w[1], w[2], w[3]);
+        xst16(out + o, w[0], w[1], w[2], w[3], B);
       }
       poly_block(ps, c[0], c[1], c[2], c[3]);
       ++kpieces;
@@ -137,7 +184,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     const uint32_t off = 64u * (b - 1u);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      x[q] = (b >= 1u && off + 16u * (uint32_t)q < P) ? ld16(in + off + 16u * (uint32_t)q) : make_uint4(0, 0, 0, 0);
+      x[q] = (b >= 1u && off + 16u * (uint32_t)q < P) ? xld16(in + off + 16u * (uint32_t)q, B) : make_uint4(0, 0, 0, 0);
   };
 
   // first block of the span (lane 0: block 0, the one-time key)
@@ -190,13 +237,15 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     poly_finish(ps, s, tag);
     if (kSeal) {
       uint8_t *t = out + P;  // right after the ciphertext (session.rs:247-252)
+      if (xok((uint64_t)t, 16u, B.out_lo, B.out_hi, B)) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) t[q] = (uint8_t)(tag[q / 4] >> (8 * (q % 4)));
+        for (int q = 0; q < 16; ++q) t[q] = (uint8_t)(tag[q / 4] >> (8 * (q % 4)));
+      }
     } else {
       // received tag = bytes [P, P + 16) after the header: two aligned pieces
       const uint32_t o = P & ~15u;
-      const uint4 ta = ld16(in + o);
-      const uint4 tb = (P & 15u) ? ld16(in + o + 16u) : make_uint4(0, 0, 0, 0);
+      const uint4 ta = xld16(in + o, B);
+      const uint4 tb = (P & 15u) ? xld16(in + o + 16u, B) : make_uint4(0, 0, 0, 0);
       const uint32_t tw[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
       const int sh = (int)(P & 15u);
 #pragma unroll
@@ -204,7 +253,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     }
   }
   if (kSeal) {
-    if (l == 0u) st16(dst, WG_MSG_DATA, sidx, n1, n2);  // header (session.rs:224-229)
+    if (l == 0u) xst16(dst, WG_MSG_DATA, sidx, n1, n2, B);  // header (session.rs:224-229)
   } else {
     bad = gshfl<G>(bad, Lu - 1u);
     if (bad) {
@@ -215,8 +264,8 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       const uint32_t hi = b1 >= 1u ? min(64u * (b1 - 1u), P) : 0u;
       const uint32_t zw[4] = {0, 0, 0, 0};
       for (uint32_t o = lo; o < hi; o += 16u) {
-        if (o + 16u <= P) st16(out + o, 0u, 0u, 0u, 0u);
-        else store_partial(out + o, zw, (int)(P - o));
+        if (o + 16u <= P) xst16(out + o, 0u, 0u, 0u, 0u, B);
+        else xstore_partial(out + o, zw, (int)(P - o), B);
       }
     }
   }
@@ -227,8 +276,9 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
 // stores (outputs and status) to be acknowledged, the workgroup meets at a barrier, and
 // its thread 0 arrives on done_count with a system-scope release (one L2 write-back per
 // workgroup; no acquire: nothing is read after it, and an acquire's L2 invalidate per
-// wave cost 1024-packet calls 50 us, profiles/r05an); the last to arrive resets the
-// counter for the stream's next launch and publishes seq.  (Thread-indexed addresses:
+// wave cost 1024-packet calls 50 us, profiles/r05an); the last to arrive takes one
+// system-scope acquire, resets the counter for the stream's next launch and
+// publishes seq.  (Thread-indexed addresses:
 // the counter and the word take vector memory operations.)
 __device__ __forceinline__ void grid_done(uint32_t *count, uint32_t *flag, uint32_t seq) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -236,6 +286,9 @@ __device__ __forceinline__ void grid_done(uint32_t *count, uint32_t *flag, uint3
   if (threadIdx.x == 0u) {
     const uint32_t prev = __hip_atomic_fetch_add(count + threadIdx.x, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (prev == gridDim.x - 1u) {
+      // the one last arrival acquires every other workgroup's release, so the word
+      // it publishes orders their outputs and statuses too (one invalidate per grid)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       __hip_atomic_store(count + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(flag + threadIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -254,7 +307,7 @@ __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams pr
     const uint8_t *src = reinterpret_cast<const uint8_t *>(reinterpret_cast<uint64_t>(prm.src) + d.src_off);
     uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uint64_t>(prm.dst) + d.dst_off);
     xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, prm.status + idx,
-                           prm.keys, prm.key_index, prm.key_slots);
+                           prm.keys, prm.key_index, prm.key_slots, idx);
   }
   if (prm.done_flag) grid_done(prm.done_count, prm.done_flag, prm.done_seq);  // (kernel-uniform)
 }
@@ -269,7 +322,7 @@ __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_strided_kernel(Strid
   if (i >= prm.n) return;
   xlane_packet<kSeal, G>(l, prm.src + (uint64_t)i * prm.src_stride, prm.dst + (uint64_t)i * prm.dst_stride, prm.len,
                          prm.key_slot, prm.counter_base + i, 0u, prm.status ? prm.status + i : nullptr, prm.keys,
-                         prm.key_index, 0xffffffffu);
+                         prm.key_index, 0xffffffffu, i);
 }
 
 template __global__ void aead_xlane_kernel<true, 64>(DescParams);
@@ -299,3 +352,20 @@ template __global__ void aead_xlane_strided_kernel<true, 2>(StridedParams);
 template __global__ void aead_xlane_strided_kernel<false, 2>(StridedParams);
 
 }  // namespace wg
+
+// Checked build's record: out = {violations, first address, its packet, its lane};
+// reset != 0 clears it.  Returns 0, or -1 when this library is not the checked build.
+extern "C" int wg_gpu_debug_xlane_check(unsigned long long *out, int reset) {
+#if WG_XLANE_CHECK
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(wg::g_xlane_check), sizeof(wg::g_xlane_check)) != hipSuccess)
+    return -2;
+  if (reset) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(wg::g_xlane_check), z, sizeof z) != hipSuccess) return -2;
+  }
+  return 0;
+#else
+  (void)out; (void)reset;
+  return -1;
+#endif
+}

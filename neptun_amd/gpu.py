@@ -97,13 +97,25 @@ def _stream(stream) -> int:
 class GpuContext:
     """One GPU + device key table.  Replaces per-session ring keys."""
 
-    def __init__(self, device: int = 0, key_slots: int = 1):
-        self._lib = load()
+    def __init__(self, device: int = 0, key_slots: int = 1, lib_path: str | None = None):
+        # lib_path: another build of the same sources (the tests' checked build)
+        self._lib = load(lib_path) if lib_path else load()
         h = ctypes.c_void_p()
         check(self._lib.wg_gpu_ctx_create(device, key_slots, ctypes.byref(h)), "wg_gpu_ctx_create")
         self._h = h
         self.device = device
         self.key_slots = key_slots
+
+    def xlane_check(self, reset: bool = False):
+        """Checked build only: (violations, first address, its packet, its lane) of the
+        latency form's bounds audit since the last reset; None on the product build."""
+        out = (ctypes.c_ulonglong * 4)()
+        rc = self._lib.wg_gpu_debug_xlane_check(out, 1 if reset else 0)
+        if rc == -1:
+            return None
+        if rc != 0:
+            raise NeptunGpuError(f"wg_gpu_debug_xlane_check failed (rc={rc})")
+        return tuple(int(x) for x in out)
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -256,8 +268,9 @@ class GpuContext:
               "wg_gpu_ctx_set_slot_padding")
 
     def set_xlane_lanes(self, lanes: int) -> None:
-        """Latency form of the descriptor batches: n * G <= lanes runs G (64..8)
-        lanes per packet; 0 = off, < 0 = default."""
+        """Latency form of the descriptor and strided batches: n * G <= lanes runs G
+        (64..2, narrowed to the packets' keystream blocks) lanes per packet; 0 = off,
+        < 0 = default."""
         check(self._lib.wg_gpu_ctx_set_xlane_lanes(self._h, int(lanes)), "wg_gpu_ctx_set_xlane_lanes")
 
     def seal_strided(self, n: int, length: int, key_slot: int, counter_base: int, src,

@@ -129,7 +129,9 @@ class Engine:
         check(self._lib.wg_engine_create(ctx._h, ctypes.byref(h)), "wg_engine_create")
         self._h = h
 
-    def tunn(self, first_slot: int = 0) -> "Tunn":
+    def tunn(self, first_slot: int) -> "Tunn":
+        """A Tunn on this engine over key slots [first_slot, first_slot + 16) of the
+        context (refused if a live Tunn on the context holds any of them)."""
         return Tunn(self._ctx, first_slot, engine=self)
 
     def info(self) -> dict:
@@ -141,6 +143,20 @@ class Engine:
         if getattr(self, "_h", None):
             check(self._lib.wg_engine_destroy(self._h), "wg_engine_destroy")
             self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        # (its Tunns keep it alive; one attached through the C ABI alone keeps the
+        # engine too: wg_engine_destroy refuses while Tunns are attached)
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _multi(self, fn, name, tunns, blobs, dsts):
         n = len(blobs)

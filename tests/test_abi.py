@@ -31,10 +31,22 @@ def test_library_build_id_matches_the_sources(monkeypatch):
     from neptun_amd import _native
     lib = neptun_amd.load()
     assert lib.wg_gpu_build_id().decode() == _native.source_build_id()
-    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "_libs", {})
     monkeypatch.setattr(_native, "source_build_id", lambda: "0" * 16)
     with pytest.raises(_native.NeptunGpuError, match="other sources"):
         _native.load()
+
+
+def test_checked_build_is_a_separate_library():
+    """libneptun_gpu_checked.so (the latency form's bounds audit) comes from the same
+    sources; the product library reports that it is not the checked build."""
+    from neptun_amd import _native
+    lib = neptun_amd.load()
+    chk = _native.load(_native.CHECKED_LIB_PATH)
+    assert chk is not lib
+    assert chk.wg_gpu_build_id().decode() == _native.source_build_id()
+    out = (ctypes.c_ulonglong * 4)()
+    assert lib.wg_gpu_debug_xlane_check(out, 0) == -1
 
 
 def test_tunn_layouts_match_header():

@@ -99,8 +99,12 @@ def test_tunns_on_one_engine_add_no_threads_or_streams(big_ctx):
     assert threads_now() <= after_engine + 4  # (the HIP runtime may start a helper of its own)
     # a Tunn of another engine cannot join this engine's multi-peer batch
     other = Engine(big_ctx)
-    stray = other.tunn(0)
     from neptun_amd import NeptunGpuError
+    # key slots are the context's: a range a live Tunn holds is refused, whatever engine
+    with pytest.raises(NeptunGpuError, match="overlap"):
+        other.tunn(8)
+    tunns[4095].close()  # (its slots are free again)
+    stray = other.tunn(16 * 4095)
     with pytest.raises(NeptunGpuError, match="not on this engine"):
         eng.encapsulate_multi([tunns[0], stray], [b"x", b"y"], [bytearray(64), bytearray(64)])
     with pytest.raises(NeptunGpuError, match="still attached"):

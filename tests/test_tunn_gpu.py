@@ -470,6 +470,89 @@ def test_small_calls_back_to_back_match_sequential_tunn(gpu, monkeypatch, word):
     tg.close()
 
 
+def test_teardown_and_regrowth_after_word_completed_calls(gpu, torch_cuda, monkeypatch):
+    """What can outlive a call in this process, each followed at once by a
+    latency-form strided open and a host copy into fresh memory (the shape of the
+    round-5 driver fault: test_xlane_gpu's 8192-byte open, then a device-to-host copy):
+    a Tunn destroyed right after a word-completed call (no event recorded), staging
+    regrown (freed and reallocated) by a large call right after a word-completed one,
+    and registered pools unregistered and freed right after a registered small call.
+    Every call equals the sequential model; every later launch and copy is clean."""
+    import gc
+
+    import numpy as np
+    torch = torch_cuda
+    monkeypatch.setenv("WG_TUNN_FLAG", "64")
+    rng = random.Random(91)
+
+    def xlane_open_then_copy():
+        nrng = np.random.default_rng(5)
+        key = nrng.integers(0, 256, (1, 32), dtype=np.uint8)
+        gpu.set_keys(0, key, np.array([0x1234567], np.uint32))
+        n, P, S = 200, 8192, 8224
+        src = torch.from_numpy(nrng.integers(0, 256, n * S + 64, dtype=np.uint8)).cuda()
+        wire = torch.full((n * S + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        back = torch.full((n * S + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+        try:
+            gpu.set_xlane_lanes(n * 64)
+            gpu.seal_strided(n, P, 0, 7, src, S, wire, S, None)
+            gpu.open_strided(n, P + 32, 0, wire, S, back, S, None)
+            torch.cuda.synchronize()
+        finally:
+            gpu.set_xlane_lanes(-1)
+        b, s_np = back.cpu().numpy(), src.cpu().numpy()
+        w = wire.cpu().numpy()
+        for i in (0, n - 1):
+            assert w[i * S:i * S + P + 32].tobytes() == o.format_packet_data(
+                key[0].tobytes(), 0x1234567, 7 + i, s_np[i * S:i * S + P].tobytes())
+        assert np.array_equal(b[:n * S].reshape(n, S)[:, :P], s_np[:n * S].reshape(n, S)[:, :P])
+
+    def small_calls(tm, tg, sessions, ctr_state, n=50):
+        srcs = [ipv4(rng, rng.choice([64, 1350])) for _ in range(n)]
+        caps = [len(x) + 32 for x in srcs]
+        dm, dg = [bytearray(b"\xee" * c) for c in caps], [bytearray(b"\xee" * c) for c in caps]
+        check_same(tg.encapsulate_batch(srcs, dg), [tm.encapsulate(x, d) for x, d in zip(srcs, dm)], dg, dm,
+                   "small encap")
+        dgs = datagrams(rng, sessions, n, ctr_state)
+        caps = [max(len(d) - 16, 1) for d in dgs]
+        dm, dg = [bytearray(b"\xee" * c) for c in caps], [bytearray(b"\xee" * c) for c in caps]
+        check_same(tg.decapsulate_batch(dgs, dg), [tm.decapsulate(d, x) for d, x in zip(dgs, dm)], dg, dm,
+                   "small decap")
+
+    # 1. destroyed right after a word-completed call (and collected at once)
+    tm, tg, sessions = make_pair(gpu, rng)
+    small_calls(tm, tg, sessions, {})
+    tg.close()
+    del tg
+    gc.collect()
+    xlane_open_then_copy()
+    # 2. staging regrown right after a word-completed call, then small calls again
+    tm, tg, sessions = make_pair(gpu, rng)
+    st = {}
+    small_calls(tm, tg, sessions, st)
+    big = [ipv4(rng, 1350) for _ in range(40000)]
+    dm, dg = [bytearray(1382) for _ in big], [bytearray(1382) for _ in big]
+    check_same(tg.encapsulate_batch(big, dg), [tm.encapsulate(x, d) for x, d in zip(big, dm)], dg, dm, "big")
+    small_calls(tm, tg, sessions, st)
+    xlane_open_then_copy()
+    # 3. registered pools freed right after a registered small call
+    srcs = [ipv4(rng, 1350) for _ in range(50)]
+    caps = [len(x) + 32 for x in srcs]
+    a_src, a_dst = Arena(srcs, [0] * 50), Arena([b""] * 50, caps)
+    for a in (a_src, a_dst):
+        gpu.register_host(*a.window())
+    dm = [bytearray(b"\xee" * c) for c in caps]
+    res_m = [tm.encapsulate(x, d) for x, d in zip(srcs, dm)]
+    res_g = tg.encapsulate_ptrs(a_src.ptrs, a_src.lens, a_dst.ptrs, np.array(caps, np.uint32))
+    check_same(res_g, res_m, [bytearray(a_dst.get(k, caps[k])) for k in range(50)], dm, "registered small")
+    for a in (a_src, a_dst):
+        gpu.unregister_host(a.window()[0])
+    del a_src, a_dst, a
+    gc.collect()
+    xlane_open_then_copy()
+    tg.close()
+
+
 @pytest.mark.parametrize("chunk_kb", [None, "64"])
 def test_multi_engine_split_matches_sequential_tunn(torch_cuda, monkeypatch, chunk_kb):
     """wg_tunn_create_multi over two contexts on device 0 (the 1-GPU stand-in for

@@ -54,10 +54,32 @@ def seal_descs(sizes, soffs, ctrs, slots, rng):
     return d, pos + 64
 
 
-@pytest.fixture
-def xl(gpu):
-    yield gpu
-    gpu.set_xlane_lanes(-1)  # back to the default selection
+@pytest.fixture(scope="module")
+def gpu_checked(torch_cuda):
+    """A context on the checked build (libneptun_gpu_checked.so: every latency-form
+    access checked against its packet's extents, counted and not made)."""
+    from neptun_amd import GpuContext, _native
+    ctx = GpuContext(0, key_slots=4096, lib_path=_native.CHECKED_LIB_PATH)
+    yield ctx
+    ctx.close()
+
+
+@pytest.fixture(params=["product", "checked"])
+def xl(request, gpu):
+    """Every latency-form test runs on the product library and again on the checked
+    build, which must end it with no access outside a packet's own bytes."""
+    if request.param == "product":
+        yield gpu
+        gpu.set_xlane_lanes(-1)  # back to the default selection
+        return
+    ctx = request.getfixturevalue("gpu_checked")
+    ctx.xlane_check(reset=True)
+    yield ctx
+    ctx.set_xlane_lanes(-1)
+    bad = ctx.xlane_check(reset=True)
+    assert bad is not None and bad[0] == 0, \
+        f"latency form touched memory outside its packet: {bad[0]} accesses, first at {bad[1]:#x} " \
+        f"(packet {bad[2]}, lane {bad[3]})"
 
 
 @pytest.mark.parametrize("G", [64, 32, 16, 8])

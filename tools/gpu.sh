@@ -35,7 +35,7 @@ TAG=${1:?usage: tools/gpu.sh TAG STEP [STEP ...]}
 shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 
 run() {  # run LIMIT LOG CMD...: one step, its output in LOG, ends the call on failure
   local limit=$1 log=$2

@@ -13,7 +13,6 @@ import os
 import shutil
 import subprocess
 import sys
-import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
