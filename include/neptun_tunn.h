@@ -190,7 +190,13 @@ int wg_tunn_decapsulate_batch(wg_tunn *t, uint32_t n, const uint8_t *const *data
  * packets in order, tx_bytes / rx_bytes go to the packet's Tunn.  Every tunn[i]
  * must be attached to `e` (else WG_RC_INVALID_ARGUMENT, nothing done).  The call
  * takes each distinct Tunn's lock (in address order) for its duration, as the
- * single-Tunn calls take their Tunn's. */
+ * single-Tunn calls take their Tunn's.
+ * e == NULL: the Tunns may be attached to any engines (normally one engine per
+ * GPU, NepTUN's workers serving every peer, packet_workers.rs:113-131): the batch is
+ * split by engine, each engine's packets kept in batch order, the shares run
+ * concurrently (each on its engine's driver thread, one on the caller) and the
+ * results come back in packet order -- still equal to the sequential calls.  A Tunn
+ * of wg_tunn_create_multi (private engines) is refused. */
 int wg_tunn_encapsulate_multi(wg_engine *e, uint32_t n, wg_tunn *const *tunn,
                               const uint8_t *const *src, const uint32_t *src_len,
                               uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res);

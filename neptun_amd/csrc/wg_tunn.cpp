@@ -823,6 +823,11 @@ struct wg_engine {
   std::vector<Engine *> lanes, idle;
   uint32_t max_lanes = 8, tunns = 0;
   bool implicit = false;  // a context's default engine (wg_tunn_create): dies with its last Tunn
+  // multi-peer calls over several engines (wg_tunn_*_multi with e == NULL): this
+  // engine's share runs on its driver thread (made on first use, bound to the GPU's
+  // NUMA node), held by one such call at a time
+  Driver *driver = nullptr;
+  std::mutex driver_mu;
 };
 
 namespace {
@@ -2163,6 +2168,7 @@ int engine_make(wg_gpu_ctx *ctx, wg_engine **out) {
 
 void engine_free(wg_engine *g) {
   for (Engine *E : g->lanes) destroy_engine(E);
+  delete g->driver;
   delete g->pool;
   delete g;
 }
@@ -2834,28 +2840,124 @@ struct MultiCall {
   ~MultiCall() {}  // (the lease below returns the lane; the locks go last)
 };
 
-int wg_tunn_encapsulate_multi(wg_engine *e, uint32_t n, wg_tunn *const *tunn,
-                              const uint8_t *const *src, const uint32_t *src_len,
-                              uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res) {
-  if (!e || (n && (!tunn || !src || !src_len || !dst || !dst_cap || !res)))
-    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "encapsulate_multi: null", hipSuccess);
-  if (n == 0) return WG_RC_OK;
+static int multi_on_engine(bool seal, wg_engine *e, uint32_t n, wg_tunn *const *tunn, const uint8_t *const *in,
+                    const uint32_t *len, uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res) {
   MultiCall mc(e, n, tunn);
   if (mc.rc) return mc.rc;
   Lease lease(mc.owner, mc.lane);
-  return encap_impl(mc.owner, tunn, n, src, src_len, dst, dst_cap, res);
+  return seal ? encap_impl(mc.owner, tunn, n, in, len, dst, dst_cap, res)
+              : decap_impl(mc.owner, tunn, &mc.peers, n, in, len, dst, dst_cap, res);
+}
+
+// Multi-peer batches over several engines (e == NULL; normally one engine per GPU,
+// NepTUN's PacketWorkers serving every peer from one channel, packet_workers.rs:
+// 113-131, 178-233, with one Mutex<Tunn> per peer, device/peer.rs:29): the batch is
+// split by the packets' engines, each engine's packets kept in batch order -- a Tunn
+// belongs to one engine, so every Tunn still sees its packets in order and the
+// results equal the sequential calls -- and the shares run concurrently: each on its
+// engine's driver thread (while another such call holds that driver: on the caller),
+// the last on the caller.  Results are scattered back into packet order.
+struct EngineShare {
+  wg_engine *g = nullptr;
+  std::vector<uint32_t> idx;
+  std::vector<wg_tunn *> tunn;
+  std::vector<const uint8_t *> in;
+  std::vector<uint32_t> len, cap;
+  std::vector<uint8_t *> dst;
+  std::vector<wg_tunn_result> res;
+  int rc = WG_RC_OK;
+  bool on_driver = false;
+};
+
+static int multi_across(bool seal, uint32_t n, wg_tunn *const *tunn, const uint8_t *const *in, const uint32_t *len,
+                 uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res) {
+  thread_local std::vector<EngineShare> shares;
+  size_t used = 0, last = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    wg_engine *g = tunn[i] ? tunn[i]->group : nullptr;
+    if (!g)
+      return wg_pipe_fail(WG_RC_INVALID_ARGUMENT,
+                          "multi batch: a Tunn is null or has private engines (wg_tunn_create_multi)", hipSuccess);
+    if (last >= used || shares[last].g != g) {
+      last = 0;
+      while (last < used && shares[last].g != g) ++last;
+      if (last == used) {
+        if (used == shares.size()) shares.emplace_back();
+        EngineShare &S = shares[used++];
+        S.g = g;
+        S.idx.clear();
+        S.tunn.clear();
+        S.in.clear();
+        S.len.clear();
+        S.cap.clear();
+        S.dst.clear();
+        S.rc = WG_RC_OK;
+        S.on_driver = false;
+      }
+    }
+    EngineShare &S = shares[last];
+    S.idx.push_back(i);
+    S.tunn.push_back(tunn[i]);
+    S.in.push_back(in[i]);
+    S.len.push_back(len[i]);
+    S.dst.push_back(dst[i]);
+    S.cap.push_back(dst_cap[i]);
+  }
+  if (used == 1) return multi_on_engine(seal, shares[0].g, n, tunn, in, len, dst, dst_cap, res);
+  auto run_share = [seal](EngineShare &S) {
+    S.res.resize(S.idx.size());
+    return multi_on_engine(seal, S.g, (uint32_t)S.idx.size(), S.tunn.data(), S.in.data(), S.len.data(),
+                           S.dst.data(), S.cap.data(), S.res.data());
+  };
+  for (size_t k = 0; k + 1 < used; ++k) {
+    EngineShare &S = shares[k];
+    wg_engine *g = S.g;
+    if (!g->driver_mu.try_lock()) continue;
+    if (!g->driver) g->driver = new (std::nothrow) Driver(device_numa_node(g->device));
+    if (!g->driver) {
+      g->driver_mu.unlock();
+      continue;
+    }
+    S.on_driver = true;
+    EngineShare *ps = &S;
+    g->driver->submit([ps, run_share]() mutable {
+      DevGuard dg(ps->g->device);
+      return run_share(*ps);
+    });
+  }
+  int rc = WG_RC_OK;
+  for (size_t k = used; k-- > 0;)  // (the caller's shares while the drivers run theirs)
+    if (!shares[k].on_driver) shares[k].rc = run_share(shares[k]);
+  for (size_t k = 0; k < used; ++k) {
+    EngineShare &S = shares[k];
+    if (S.on_driver) {
+      S.rc = S.g->driver->wait();
+      S.g->driver_mu.unlock();
+    }
+    if (S.rc && !rc) rc = S.rc;
+    for (size_t j = 0; j < S.idx.size(); ++j) res[S.idx[j]] = S.res[j];
+  }
+  return rc;
+}
+
+int wg_tunn_encapsulate_multi(wg_engine *e, uint32_t n, wg_tunn *const *tunn,
+                              const uint8_t *const *src, const uint32_t *src_len,
+                              uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res) {
+  if (n && (!tunn || !src || !src_len || !dst || !dst_cap || !res))
+    return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "encapsulate_multi: null", hipSuccess);
+  if (n == 0) return WG_RC_OK;
+  if (!e) return multi_across(true, n, tunn, src, src_len, dst, dst_cap, res);
+  return multi_on_engine(true, e, n, tunn, src, src_len, dst, dst_cap, res);
 }
 
 int wg_tunn_decapsulate_multi(wg_engine *e, uint32_t n, wg_tunn *const *tunn,
                               const uint8_t *const *datagram, const uint32_t *len,
                               uint8_t *const *dst, const uint32_t *dst_cap, wg_tunn_result *res) {
-  if (!e || (n && (!tunn || !datagram || !len || !dst || !dst_cap || !res)))
+  if (n && (!tunn || !datagram || !len || !dst || !dst_cap || !res))
     return wg_pipe_fail(WG_RC_INVALID_ARGUMENT, "decapsulate_multi: null", hipSuccess);
   if (n == 0) return WG_RC_OK;
-  MultiCall mc(e, n, tunn);
-  if (mc.rc) return mc.rc;
-  Lease lease(mc.owner, mc.lane);
-  return decap_impl(mc.owner, tunn, &mc.peers, n, datagram, len, dst, dst_cap, res);
+  if (!e) return multi_across(false, n, tunn, datagram, len, dst, dst_cap, res);
+  return multi_on_engine(false, e, n, tunn, datagram, len, dst, dst_cap, res);
 }
 
 int wg_tunn_decrypt_batch(wg_tunn *t, uint32_t n, const uint8_t *const *datagram,

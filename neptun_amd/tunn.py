@@ -192,6 +192,39 @@ class Engine:
                                 src_ptrs, src_lens, dst_ptrs, dst_caps)
 
 
+def _multi_across(name, tunns, blobs, dsts):
+    L = tunns[0]._lib
+    n = len(blobs)
+    keep, sp, sl, dp, dc = _packet_arrays(blobs, dsts)
+    th = (ctypes.c_void_p * n)(*[t._h.value for t in tunns])
+    res = (TunnResult * n)()
+    check(getattr(L, name)(None, n, th, sp, sl, dp, dc, res), name)
+    return _results(res)
+
+
+def encapsulate_multi(tunns, srcs, dsts):
+    """packet i through tunns[i], the Tunns on any engines (one per GPU, say):
+    wg_tunn_encapsulate_multi with no engine -- split by engine, shares run
+    concurrently, results in packet order."""
+    return _multi_across("wg_tunn_encapsulate_multi", tunns, srcs, dsts)
+
+
+def decapsulate_multi(tunns, datagrams, dsts):
+    return _multi_across("wg_tunn_decapsulate_multi", tunns, datagrams, dsts)
+
+
+def multi_ptrs(seal: bool, tunn_ptrs, src_ptrs, src_lens, dst_ptrs, dst_caps, lib):
+    """The engine-free multi-peer call over raw addresses (numpy uint64 / uint32)."""
+    n = len(src_ptrs)
+    res = (TunnResult * n)()
+    vp = ctypes.c_void_p
+    name = "wg_tunn_encapsulate_multi" if seal else "wg_tunn_decapsulate_multi"
+    check(getattr(lib, name)(None, n, vp(tunn_ptrs.ctypes.data), vp(src_ptrs.ctypes.data),
+                             vp(src_lens.ctypes.data), vp(dst_ptrs.ctypes.data), vp(dst_caps.ctypes.data), res),
+          name)
+    return _results(res)
+
+
 class Tunn:
     """Tunn mirror bound to a GpuContext; uses 16 key slots from `first_slot`."""
 

@@ -317,3 +317,103 @@ def test_concurrent_calls_share_the_engine(big_ctx):
     for _, tg, _ in pairs:
         tg.close()
     eng.close()
+
+
+@pytest.fixture(scope="module")
+def two_ctx(torch_cuda):
+    """Two contexts on device 0: the 1-GPU stand-in for one engine per GPU."""
+    from neptun_amd import GpuContext
+    ctxs = [GpuContext(0, key_slots=2048 * 16), GpuContext(0, key_slots=2048 * 16)]
+    yield ctxs
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.parametrize("n_peers", [64, 4096])
+def test_multi_peer_batches_across_engines_match_sequential_tunns(two_ctx, n_peers):
+    """wg_tunn_*_multi with no engine: the peers' Tunns alternate between two engines
+    (two contexts -- on a node, one per GPU), every batch interleaves packets of all of
+    them; the call splits it by engine, runs the shares concurrently and returns the
+    results in packet order -- equal to the model's per-peer sequential calls, bytes,
+    counters, windows and stats (NepTUN's PacketWorkers over every peer,
+    packet_workers.rs:113-131, 178-233; one Mutex<Tunn> per peer, device/peer.rs:29)."""
+    from neptun_amd import Engine
+    from neptun_amd import tunn as T
+    rng = random.Random(7000 + n_peers)
+    engs = [Engine(c) for c in two_ctx]
+    pairs = []
+    for p in range(n_peers):
+        tm, tg = M.Tunn(), engs[p % 2].tunn((p // 2) * 16)
+        ses = []
+        if n_peers == 64 and p % 16 == 15:
+            pass  # (a peer without a session)
+        else:
+            for j in range(1 if n_peers > 64 else rng.choice((1, 2))):
+                local = (p * 8 + j * 3 + 1) & 0xFFFFFFFF
+                rk, sk, peer = rng.randbytes(32), rng.randbytes(32), rng.getrandbits(32)
+                for t in (tm, tg):
+                    t.set_time(10 * (j + 1))
+                    t.install_session(local, peer, rk, sk, True)
+                ses.append((local, peer, rk, sk))
+        pairs.append((tm, tg, ses))
+    ctr_state = [dict() for _ in pairs]
+    per = 3000 if n_peers == 64 else 4 * n_peers
+    for batch in range(2):
+        who = [rng.randrange(n_peers) for _ in range(per)]
+        srcs = [ipv4(rng, rng.choice([20, 64, 576, 1350, rng.randrange(20, 1500)])) for _ in who]
+        caps = [len(s) + 32 + rng.randrange(0, 3) * 16 for s in srcs]
+        dm = [bytearray(b"\xee" * c) for c in caps]
+        dg = [bytearray(b"\xee" * c) for c in caps]
+        res_m = [pairs[p][0].encapsulate(s, d) for p, s, d in zip(who, srcs, dm)]
+        res_g = T.encapsulate_multi([pairs[p][1] for p in who], srcs, dg)
+        check_same(res_g, res_m, dg, dm, f"across encap {batch}")
+        who = [rng.randrange(n_peers) for _ in range(per)]
+        dgs = []
+        for p in who:
+            ses = pairs[p][2]
+            dgs += datagrams(rng, ses, 1, ctr_state[p]) if ses else [o.format_packet_data(
+                rng.randbytes(32), 5, 0, ipv4(rng, 40))]
+        caps = [max(len(d) - 16, 0) for d in dgs]
+        dm = [bytearray(b"\xee" * c) for c in caps]
+        dg = [bytearray(b"\xee" * c) for c in caps]
+        res_m = [pairs[p][0].decapsulate(d, x) for p, d, x in zip(who, dgs, dm)]
+        res_g = T.decapsulate_multi([pairs[p][1] for p in who], dgs, dg)
+        check_same(res_g, res_m, dg, dm, f"across decap {batch}")
+    check_state(pairs)
+    # concurrent callers on disjoint peer sets: the engines' drivers are contended (a
+    # share whose driver another call holds runs on its caller)
+    if n_peers == 64:
+        errors = []
+
+        def worker(k):
+            try:
+                r = random.Random(k)
+                mine = [p for p in range(n_peers) if p % 4 == k]
+                for _ in range(10):
+                    who = [r.choice(mine) for _ in range(200)]
+                    srcs = [ipv4(r, r.choice([64, 1350])) for _ in who]
+                    dm = [bytearray(len(s) + 32) for s in srcs]
+                    dg = [bytearray(len(s) + 32) for s in srcs]
+                    res_m = [pairs[p][0].encapsulate(s, d) for p, s, d in zip(who, srcs, dm)]
+                    res_g = T.encapsulate_multi([pairs[p][1] for p in who], srcs, dg)
+                    check_same(res_g, res_m, dg, dm, f"concurrent {k}")
+            except Exception as e:  # (reported by the main thread)
+                errors.append(e)
+
+        ths = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert not errors, errors[0]
+        check_state(pairs)
+    # a Tunn of wg_tunn_create_multi (private engines) cannot join an engine-free batch
+    from neptun_amd import NeptunGpuError, Tunn
+    priv = Tunn(list(two_ctx), 2047 * 16)
+    with pytest.raises(NeptunGpuError, match="private engines"):
+        T.encapsulate_multi([pairs[0][1], priv], [b"x", b"y"], [bytearray(64), bytearray(64)])
+    priv.close()
+    for _, tg, _ in pairs:
+        tg.close()
+    for e in engs:
+        e.close()
