@@ -105,6 +105,15 @@ template <bool kSeal> __global__ void aead_desc_affine_kernel(DescParams prm);
 // part of the chip; wg_gpu.cpp picks G from the batch size.
 constexpr uint32_t kXlaneThreads = 256;
 template <bool kSeal, uint32_t G> __global__ void aead_xlane_kernel(DescParams prm);
+// ... with the batch's descriptors carried in the kernel arguments (the host can read
+// them: the Tunn's small calls, whose descriptors sit in pinned host memory that the
+// kernel would otherwise read over PCIe before anything else)
+constexpr uint32_t kXlaneInlineDescs = 64;
+struct XlaneInlineParams {
+  DescParams prm;
+  wg_packet_desc d[kXlaneInlineDescs];
+};
+template <bool kSeal, uint32_t G> __global__ void aead_xlane_inline_kernel(XlaneInlineParams ip);
 template <bool kSeal, uint32_t G> __global__ void aead_xlane_strided_kernel(StridedParams prm);
 
 // wg_plan.hip: counting sort of a descriptor batch by rounds (longest first)

@@ -289,6 +289,16 @@ static uint32_t xlane_min_group() {
   return g;
 }
 
+// (WG_XLANE_INLINE=0: small host-described batches read their descriptors from the
+// pinned host array like the others -- A/B only)
+static bool xlane_inline() {
+  static const bool on = [] {
+    const char *e = std::getenv("WG_XLANE_INLINE");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 static uint32_t xlane_group(const wg_gpu_ctx *ctx, uint32_t n) {
   static const long long env = [] {
     const char *e = std::getenv("WG_XLANE_LANES");
@@ -314,6 +324,7 @@ struct DescHint {
   uint32_t done_seq = 0;
   bool *flagged = nullptr;
   bool xlane_ok = true;  // false: the throughput forms only
+  bool host_descs = false;  // the host can read descs (pinned): small latency-form batches inline them
 };
 
 // The latency form's group for a batch: the budget's G (xlane_group), narrowed to
@@ -353,6 +364,26 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
       prm.done_seq = hint.done_seq;
       if (hint.flagged) *hint.flagged = true;
     }
+    const uint32_t form = 6u - (uint32_t)__builtin_ctz(G);  // 64 -> 0 ... 2 -> 5
+    const uint32_t per_block = wg::kXlaneThreads / G;
+    if (hint.host_descs && !order && n <= wg::kXlaneInlineDescs && xlane_inline()) {
+      // the descriptors travel in the kernel arguments: no PCIe read before the packets'
+      wg::XlaneInlineParams ip;
+      ip.prm = prm;
+      std::memcpy(ip.d, descs, (size_t)n * sizeof(wg_packet_desc));
+      using KI = void (*)(wg::XlaneInlineParams);
+      static const KI ikernels[2][6] = {
+          {wg::aead_xlane_inline_kernel<false, 64>, wg::aead_xlane_inline_kernel<false, 32>,
+           wg::aead_xlane_inline_kernel<false, 16>, wg::aead_xlane_inline_kernel<false, 8>,
+           wg::aead_xlane_inline_kernel<false, 4>, wg::aead_xlane_inline_kernel<false, 2>},
+          {wg::aead_xlane_inline_kernel<true, 64>, wg::aead_xlane_inline_kernel<true, 32>,
+           wg::aead_xlane_inline_kernel<true, 16>, wg::aead_xlane_inline_kernel<true, 8>,
+           wg::aead_xlane_inline_kernel<true, 4>, wg::aead_xlane_inline_kernel<true, 2>}};
+      hipLaunchKernelGGL(ikernels[seal ? 1 : 0][form], dim3((n + per_block - 1u) / per_block),
+                         dim3(wg::kXlaneThreads), 0, s, ip);
+      WG_HIP(hipGetLastError(), "batch: launch");
+      return WG_RC_OK;
+    }
     using K = void (*)(wg::DescParams);
     static const K kernels[2][6] = {  // [seal][64, 32, 16, 8, 4, 2]
         {wg::aead_xlane_kernel<false, 64>, wg::aead_xlane_kernel<false, 32>,
@@ -361,8 +392,6 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
         {wg::aead_xlane_kernel<true, 64>, wg::aead_xlane_kernel<true, 32>,
          wg::aead_xlane_kernel<true, 16>, wg::aead_xlane_kernel<true, 8>,
          wg::aead_xlane_kernel<true, 4>, wg::aead_xlane_kernel<true, 2>}};
-    const uint32_t form = 6u - (uint32_t)__builtin_ctz(G);  // 64 -> 0 ... 2 -> 5
-    const uint32_t per_block = wg::kXlaneThreads / G;
     hipLaunchKernelGGL(kernels[seal ? 1 : 0][form], dim3((n + per_block - 1u) / per_block),
                        dim3(wg::kXlaneThreads), 0, s, prm);
   } else if (WG_DESC_SYNC && src && dst) {
@@ -399,8 +428,9 @@ static int launch_desc(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs,
 int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *descs, uint32_t n,
                           const uint8_t *src, uint8_t *dst, int32_t *status, void *stream,
                           uint32_t max_len, bool host_mem, uint32_t *done_count, uint32_t *done_flag,
-                          uint32_t done_seq, bool *flagged, bool xlane_ok) {
+                          uint32_t done_seq, bool *flagged, bool xlane_ok, bool host_descs) {
   DescHint h;
+  h.host_descs = host_descs;
   h.max_len = max_len;
   h.host_mem = host_mem;
   h.done_count = done_count;

@@ -54,7 +54,8 @@ int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *desc
                           const uint8_t *src, uint8_t *dst, int32_t *status, void *stream,
                           uint32_t max_len, bool host_mem, uint32_t *done_count = nullptr,
                           uint32_t *done_flag = nullptr, uint32_t done_seq = 0,
-                          bool *flagged = nullptr, bool xlane_ok = true);  // wg_gpu.cpp
+                          bool *flagged = nullptr, bool xlane_ok = true,
+                          bool host_descs = false);  // wg_gpu.cpp
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out);  // wg_gpu.cpp
 int wg_ctx_claim_slots(wg_gpu_ctx *ctx, uint32_t first, uint32_t count);  // wg_gpu.cpp
 void wg_ctx_release_slots(wg_gpu_ctx *ctx, uint32_t first);              // wg_gpu.cpp
@@ -1084,6 +1085,12 @@ bool dma_runs() {  // (read per batch, like the other WG_TUNN_* knobs)
 // more than the kernel's PCIe reads of a few MB (WG_TUNN_DMA_MIN, default 8192; 64 packets
 // encapsulate 25 vs 37 us, decapsulate 34 vs 43; 4096: 346-385 vs 346-384 and 384-446 vs
 // 445-476; equal at 16,384; profiles/r05q_small_reg.jsonl, r05ab_tunn_small_reg.jsonl).
+// Registered decapsulate below dma_min(): the zero-copy open writes landing plaintexts
+// straight into the registered dsts (WG_TUNN_DIRECT_OUT=0: into staging, copied out)
+bool direct_out_small() {
+  const char *e = std::getenv("WG_TUNN_DIRECT_OUT");
+  return !e || std::atoi(e) != 0;
+}
 size_t dma_min() {
   const char *e = std::getenv("WG_TUNN_DMA_MIN");
   return e ? (size_t)std::max(0L, std::atol(e)) : 8192u;
@@ -1321,7 +1328,7 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
       // (the kernel reads the packets over PCIe: hint the latency form's choice)
       const int rc = wg_launch_desc_hinted(E.ctx, seal, S.h_desc, (uint32_t)m, in, out, S.h_st, S.stream,
                                            max_desc_len(S.h_desc, m), true, word ? S.d_count : nullptr,
-                                           word ? S.h_flag : nullptr, S.done_seq, &S.flagged);
+                                           word ? S.h_flag : nullptr, S.done_seq, &S.flagged, true, true);
       if (rc) return rc;
       if (timed) TUNN_HIP(hipEventRecord(S.ev[2], S.stream), "tunn: event");
     } else {
@@ -1714,18 +1721,18 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
   };
   // a DMA chunk's results: in-order decisions, repairs of the packets the speculation
   // missed, validation and copy-out
-  auto done_chunk = [&](Engine &E, const Chunk &ch, size_t j0) -> void {
-    if (dma_err) return;
-    decide_range(ch.k0, ch.k1, E.b_st + j0);
+  // after a speculated chunk's decisions: which outputs are in dst (landed: 2 = the
+  // kernel wrote the plaintext, the tag still to write; 1 = all of it) and the repairs
+  // of the packets the speculation missed; false (dma_err set) on an error
+  auto settle = [&](Engine &E, const Chunk &ch, uint8_t landed) -> bool {
     std::vector<size_t> rep;
-    const uint8_t landed = E.chunk_direct[&ch - E.chunks.data()] ? 2 : 1;  // 2: the tag still to write
     for (size_t k = ch.k0; k < ch.k1; ++k) {
       const bool lands = (t->sc->act[k] & 3) != 0;
       if (lands && !t->sc->spec[k]) rep.push_back(k);
       t->sc->out_dma[k] = lands && t->sc->spec[k] ? landed : 0;
       if (!lands && t->sc->spec[k]) {  // (cannot happen: see above)
         dma_err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: a speculated replay decision was not kept", hipSuccess);
-        return;
+        return false;
       }
     }
     if (!rep.empty()) {
@@ -1735,7 +1742,7 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       for (size_t k : rep) bytes += round128(len[t->sc->sel[k]]);
       if (const hipError_t e = reserve(A, bytes + 128, rep.size()); e != hipSuccess) {
         dma_err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair staging", e);
-        return;
+        return false;
       }
       uint64_t o = 0;
       for (size_t r = 0; r < rep.size(); ++r) {
@@ -1747,11 +1754,11 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       if (const int rc = wg_gpu_open_batch(E.ctx, A.h_desc, (uint32_t)rep.size(), A.h_in, A.h_out, A.h_st,
                                            A.stream)) {
         dma_err = rc;
-        return;
+        return false;
       }
       if (const hipError_t e = hipStreamSynchronize(A.stream); e != hipSuccess) {
         dma_err = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: repair open", e);
-        return;
+        return false;
       }
       for (size_t r = 0; r < rep.size(); ++r) {
         const size_t k = rep[r];
@@ -1763,6 +1770,12 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
         t->sc->out_dma[k] = 1;  // (in dst now)
       }
     }
+    return true;
+  };
+  auto done_chunk = [&](Engine &E, const Chunk &ch, size_t j0) -> void {
+    if (dma_err) return;
+    decide_range(ch.k0, ch.k1, E.b_st + j0);
+    if (!settle(E, ch, E.chunk_direct[&ch - E.chunks.data()] ? 2 : 1)) return;
     copy_out(E, ch, nullptr, nullptr);
   };
   auto dma_batch = [&](Engine &E) -> int {
@@ -1884,12 +1897,37 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
       direct = (reinterpret_cast<uint64_t>(datagram[i]) & 15u) == 0 &&
                dev_addr(E, datagram[i], len[i], E.dsrc[k - E.k0]);
     }
+    // direct output too (every dst registered and 16-byte aligned, one engine): the open
+    // kernel writes each plaintext the speculated replay decisions land straight into
+    // its dst and the others' into the pinned sink, as the DMA batches' direct output
+    // does; the in-order decisions then only add the tags (and repair what the
+    // speculation missed) -- no plaintext copy-out from staging
+    bool dout = direct && inline_decide && direct_out_small();
+    if (dout) {
+      E.ddst.resize(E.k1 - E.k0);
+      uint32_t pmax = 0;
+      for (size_t k = E.k0; dout && k < E.k1; ++k) {
+        const uint32_t i = t->sc->sel[k];
+        dout = (reinterpret_cast<uint64_t>(dst[i]) & 15u) == 0 &&
+               dev_addr(E, dst[i], len[i] - WG_DATA_OFFSET, E.ddst[k - E.k0]);
+        pmax = std::max(pmax, len[i] - (uint32_t)WG_DATA_OVERHEAD_SZ);
+      }
+      dout = dout && (pmax + 16 <= E.sink_cap || grow_sink(E, pmax + 16));
+    }
     auto pack = [&](const Chunk &ch, Staging &S) {
+      if (dout) {  // (packet order)
+        const double a = now_us();
+        for (size_t k = ch.k0; k < ch.k1; ++k) t->sc->spec[k] = speculate(k);
+        E.ph.pack_spec_us += now_us() - a;
+      }
       E.pool->run(ch.k1 - ch.k0, [&](size_t lo, size_t hi) {
         for (size_t kk = lo; kk < hi; ++kk) {
           const size_t k = ch.k0 + kk, j = k - E.k0;
           const uint32_t i = t->sc->sel[k];
-          if (direct) {
+          if (dout) {
+            S.h_desc[kk] = wg_packet_desc{E.dsrc[j], t->sc->spec[k] ? E.ddst[j] : E.sink_dev + 16, 0, len[i],
+                                          t->sc->slot[k]};
+          } else if (direct) {
             // dst is staging: the replay decision comes after the GPU (session.rs:279-300)
             S.h_desc[kk] = wg_packet_desc{E.dsrc[j], E.off[j] + WG_DATA_OFFSET, 0, len[i], t->sc->slot[k]};
           } else {
@@ -1902,12 +1940,18 @@ int open_selected(wg_tunn *t, const uint8_t *const *datagram, const uint32_t *le
     // statuses are back: decide in packet order (the copies follow in unpack)
     auto mid = [&](const Chunk &ch, Staging &S) -> int {
       if (inline_decide) decide_range(ch.k0, ch.k1, S.h_st);  // (several engines: after all are back)
+      if (dout && !dma_err) (void)settle(E, ch, 2);
       return 0;
     };
     auto unpack = [&](const Chunk &ch, Staging &S) {
-      if (inline_decide) copy_out(E, ch, S.h_out, S.h_desc);
+      if (dout) {
+        if (!dma_err) copy_out(E, ch, nullptr, nullptr);
+      } else if (inline_decide) {
+        copy_out(E, ch, S.h_out, S.h_desc);
+      }
     };
-    return run_chunks(E, false, pack, unpack, direct, false, NoHook(), mid);
+    const int r = run_chunks(E, false, pack, unpack, direct, dout, NoHook(), mid);
+    return r ? r : dma_err;
   };
   int rc = WG_RC_OK;
   if (multi) {

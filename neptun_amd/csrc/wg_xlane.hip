@@ -123,9 +123,35 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   const uint32_t in_bytes = (len + 15u) & ~15u;
   const uint32_t out_bytes = kSeal ? len + WG_DATA_OVERHEAD_SZ : (len >= WG_DATA_OVERHEAD_SZ ? len - WG_DATA_OVERHEAD_SZ : 0u);
   const XBounds B{(uint64_t)src, (uint64_t)src + in_bytes, (uint64_t)dst, (uint64_t)dst + out_bytes, pkt, l};
-  uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint32_t sidx = 0, n1 = 0, n2 = 0;
-  if (status == WG_STATUS_OK) {
+  if (status != WG_STATUS_OK) {  // group-uniform: nothing of the packet is read or written
+    if (l == 0u && st) *st = status;
+    return;
+  }
+
+  const uint32_t P = kSeal ? len : len - WG_DATA_OVERHEAD_SZ;
+  const uint8_t *in = kSeal ? src : src + WG_DATA_OFFSET;  // plaintext / ciphertext
+  uint8_t *out = kSeal ? dst + WG_DATA_OFFSET : dst;      // ciphertext / plaintext
+  const uint32_t NB = 1u + (P + 63u) / 64u;
+  const uint32_t C = (NB + G - 1u) / G;
+  const uint32_t Lu = (NB + C - 1u) / C;  // lanes in use; lane Lu - 1 holds block NB - 1
+  const uint32_t b0 = l * C, b1 = min(b0 + C, NB);
+
+  // the span's first input pieces go out with open's header load: over PCIe (the
+  // Tunn's zero-copy calls) one round trip instead of two.  A header that fails its
+  // checks below then only suppresses every store (wr): its packet's bytes are read
+  // but nothing of it is written.
+  auto load_block = [&](uint32_t b, uint4 (&x)[4]) {
+    const uint32_t off = 64u * (b - 1u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      x[q] = (b >= 1u && off + 16u * (uint32_t)q < P) ? xld16(in + off + 16u * (uint32_t)q, B) : make_uint4(0, 0, 0, 0);
+  };
+  uint4 x[4];
+  const bool any = b0 < NB;
+  if (any) load_block(b0, x);
+  uint32_t key[8];
+  uint32_t sidx, n1, n2;
+  {
     const uint4 a = ld16(keys + 32u * slot), b = ld16(keys + 32u * slot + 16u);
     key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
     key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
@@ -141,18 +167,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       n2 = h.w;
     }
   }
-  if (status != WG_STATUS_OK) {  // group-uniform: nothing of the packet is written
-    if (l == 0u && st) *st = status;
-    return;
-  }
-
-  const uint32_t P = kSeal ? len : len - WG_DATA_OVERHEAD_SZ;
-  const uint8_t *in = kSeal ? src : src + WG_DATA_OFFSET;  // plaintext / ciphertext
-  uint8_t *out = kSeal ? dst + WG_DATA_OFFSET : dst;      // ciphertext / plaintext
-  const uint32_t NB = 1u + (P + 63u) / 64u;
-  const uint32_t C = (NB + G - 1u) / G;
-  const uint32_t Lu = (NB + C - 1u) / C;  // lanes in use; lane Lu - 1 holds block NB - 1
-  const uint32_t b0 = l * C, b1 = min(b0 + C, NB);
+  const bool wr = kSeal || status == WG_STATUS_OK;  // (group-uniform)
 
   Poly ps;
   uint32_t kpieces = 0;  // pieces this lane absorbed
@@ -172,27 +187,18 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
           w[j] &= byte_mask((int)valid, j);
           c[j] &= byte_mask((int)valid, j);
         }
-        xstore_partial(out + o, w, (int)valid, B);
-      } else {
+        if (wr) xstore_partial(out + o, w, (int)valid, B);
+      } else if (wr) {
         xst16(out + o, w[0], w[1], w[2], w[3], B);
       }
       poly_block(ps, c[0], c[1], c[2], c[3]);
       ++kpieces;
     }
   };
-  auto load_block = [&](uint32_t b, uint4 (&x)[4]) {
-    const uint32_t off = 64u * (b - 1u);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      x[q] = (b >= 1u && off + 16u * (uint32_t)q < P) ? xld16(in + off + 16u * (uint32_t)q, B) : make_uint4(0, 0, 0, 0);
-  };
 
   // first block of the span (lane 0: block 0, the one-time key)
   uint32_t ks[16];
-  uint4 x[4];
-  const bool any = b0 < NB;
   if (any) {
-    load_block(b0, x);
     chacha20_block(ks, key, b0, n1, n2);
   } else {
 #pragma unroll
@@ -256,7 +262,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     if (l == 0u) xst16(dst, WG_MSG_DATA, sidx, n1, n2, B);  // header (session.rs:224-229)
   } else {
     bad = gshfl<G>(bad, Lu - 1u);
-    if (bad) {
+    if (bad && wr) {
       status = WG_STATUS_INVALID_AEAD_TAG;
       // never leave unauthenticated plaintext behind: this lane's own stores land first
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -312,6 +318,21 @@ __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams pr
   if (prm.done_flag) grid_done(prm.done_count, prm.done_flag, prm.done_seq);  // (kernel-uniform)
 }
 
+template <bool kSeal, uint32_t G>
+__global__ __launch_bounds__(kXlaneThreads) void aead_xlane_inline_kernel(XlaneInlineParams ip) {
+  const DescParams &prm = ip.prm;
+  const uint32_t gid = blockIdx.x * (kXlaneThreads / G) + threadIdx.x / G;  // packet (batch position)
+  const uint32_t l = threadIdx.x & (G - 1u);
+  if (gid < prm.n) {  // (the host keeps n <= kXlaneInlineDescs)
+    const wg_packet_desc d = ip.d[gid];
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(reinterpret_cast<uint64_t>(prm.src) + d.src_off);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uint64_t>(prm.dst) + d.dst_off);
+    xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, prm.status + gid,
+                           prm.keys, prm.key_index, prm.key_slots, gid);
+  }
+  if (prm.done_flag) grid_done(prm.done_count, prm.done_flag, prm.done_seq);  // (kernel-uniform)
+}
+
 // Strided batches (wg_gpu_seal_strided / wg_gpu_open_strided without slot padding):
 // packet i at src + i src_stride / dst + i dst_stride, one length and key slot, seal
 // counter counter_base + i; the host has checked alignment and the slot
@@ -337,6 +358,12 @@ template __global__ void aead_xlane_kernel<true, 4>(DescParams);
 template __global__ void aead_xlane_kernel<false, 4>(DescParams);
 template __global__ void aead_xlane_kernel<true, 2>(DescParams);
 template __global__ void aead_xlane_kernel<false, 2>(DescParams);
+
+#define WG_XLANE_INLINE(S, G) template __global__ void aead_xlane_inline_kernel<S, G>(XlaneInlineParams);
+WG_XLANE_INLINE(true, 64) WG_XLANE_INLINE(false, 64) WG_XLANE_INLINE(true, 32) WG_XLANE_INLINE(false, 32)
+WG_XLANE_INLINE(true, 16) WG_XLANE_INLINE(false, 16) WG_XLANE_INLINE(true, 8) WG_XLANE_INLINE(false, 8)
+WG_XLANE_INLINE(true, 4) WG_XLANE_INLINE(false, 4) WG_XLANE_INLINE(true, 2) WG_XLANE_INLINE(false, 2)
+#undef WG_XLANE_INLINE
 
 template __global__ void aead_xlane_strided_kernel<true, 64>(StridedParams);
 template __global__ void aead_xlane_strided_kernel<false, 64>(StridedParams);

@@ -266,3 +266,60 @@ def test_xlane_strided_matches_throughput_form_and_oracle(torch_cuda, xl, G, n, 
     for i in range(n):
         assert b[i * S:i * S + P].tobytes() == s_np[i * S:i * S + P].tobytes(), i
         assert (b[i * S + P:(i + 1) * S] == 0x5A).all(), i
+
+
+def test_tunn_small_calls_on_the_checked_build(gpu_checked, monkeypatch):
+    """The Tunn's small calls -- the latency form with descriptors in the kernel
+    arguments, the completion word, registered datagrams read and registered dsts
+    written in place on speculated replay decisions -- on the checked build: every
+    call equals the sequential model and no access leaves its packet."""
+    import random
+
+    from test_tunn_gpu import Arena, check_same, datagrams, ipv4, make_pair
+    monkeypatch.setenv("WG_TUNN_FLAG", "64")
+    ctx = gpu_checked
+    ctx.xlane_check(reset=True)
+    rng = random.Random(606)
+    tm, tg, sessions = make_pair(ctx, rng)
+    ctr_state, regs = {}, []
+    for call in range(60):
+        n = rng.choice([1, 7, 16, 50, 64])
+        registered = call % 3 != 0
+        if call % 2 == 0:
+            srcs = [ipv4(rng, rng.choice([20, 64, 1350, rng.randrange(20, 1500)])) for _ in range(n)]
+            caps = [len(s) + 32 for s in srcs]
+            dm = [bytearray(b"\xee" * c) for c in caps]
+            res_m = [tm.encapsulate(s, d) for s, d in zip(srcs, dm)]
+            if registered:
+                a_src, a_dst = Arena(srcs, [0] * n), Arena([b""] * n, caps)
+                for a in (a_src, a_dst):
+                    ctx.register_host(*a.window())
+                    regs.append(a)
+                res_g = tg.encapsulate_ptrs(a_src.ptrs, a_src.lens, a_dst.ptrs, np.array(caps, np.uint32))
+                dg = [bytearray(a_dst.get(k, caps[k])) for k in range(n)]
+            else:
+                dg = [bytearray(b"\xee" * c) for c in caps]
+                res_g = tg.encapsulate_batch(srcs, dg)
+            check_same(res_g, res_m, dg, dm, f"checked encap {call}")
+        else:
+            dgs = datagrams(rng, sessions, n, ctr_state)
+            caps = [max(len(d) - 16, 1) for d in dgs]
+            dm = [bytearray(b"\xee" * c) for c in caps]
+            res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+            if registered:
+                a_in, a_out = Arena(dgs, [0] * n), Arena([b""] * n, caps)
+                for a in (a_in, a_out):
+                    ctx.register_host(*a.window())
+                    regs.append(a)
+                res_g = tg.decapsulate_ptrs(a_in.ptrs, a_in.lens, a_out.ptrs, np.array(caps, np.uint32))
+                dg = [bytearray(a_out.get(k, caps[k])) for k in range(n)]
+            else:
+                dg = [bytearray(b"\xee" * c) for c in caps]
+                res_g = tg.decapsulate_batch(dgs, dg)
+            check_same(res_g, res_m, dg, dm, f"checked decap {call}")
+    assert tg.stats() == (tm.tx_bytes, tm.rx_bytes)
+    for a in regs:
+        ctx.unregister_host(a.window()[0])
+    tg.close()
+    bad = ctx.xlane_check(reset=True)
+    assert bad[0] == 0, f"{bad[0]} accesses outside their packet, first at {bad[1]:#x} (packet {bad[2]})"
