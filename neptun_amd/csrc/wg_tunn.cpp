@@ -589,6 +589,24 @@ __global__ __launch_bounds__(256) void scatter_kernel(const Scatter *__restrict_
 }
 
 // one pinned + device buffer set of the pipeline
+struct CombSlot {
+  wg_packet_desc *desc = nullptr;  // pinned (host-written; inlined into the launch when small)
+  int32_t *st = nullptr;           // pinned statuses
+  uint32_t *h_flag = nullptr, *d_count = nullptr;
+  uint32_t seq = 0;
+  hipStream_t stream = nullptr;
+  std::atomic<int> readers{0};  // calls of the launch that have not taken their statuses yet
+};
+struct CombSeg {
+  const wg_packet_desc *descs = nullptr;
+  uint32_t n = 0, max_len = 0;
+  uint64_t in_base = 0, out_base = 0;
+  // the leader's answer
+  std::atomic<int> ready{0};
+  int rc = WG_RC_OK;
+  CombSlot *slot = nullptr;
+  uint32_t off = 0, seq = 0;
+};
 struct Staging {
   uint8_t *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
   wg_packet_desc *h_desc = nullptr, *d_desc = nullptr;
@@ -615,6 +633,10 @@ struct Staging {
   uint32_t done_seq = 0;
   bool flagged = false;
   bool evented = true;  // `done` was recorded behind the chunk in flight
+  // the chunk in flight went out in a combined launch (Combiner below): its word,
+  // sequence number, statuses and slot are the combiner's
+  CombSeg *comb = nullptr;
+  CombSeg cseg;  // (this set's chunk, when it is posted to a combiner)
 };
 
 void free_buffers(Staging &s) {
@@ -745,6 +767,7 @@ struct Engine {
   Scratch scratch;            // the per-call arrays of the calls that borrow this lane
   wg_tunn *owner = nullptr;   // batch owner of the multi-peer calls on this lane
   Driver *driver = nullptr;   // multi-engine Tunns only (the single engine runs on the caller)
+  wg_engine *grp = nullptr;   // a lane: its shared engine (combined small launches)
   size_t k0 = 0, k1 = 0;      // this batch's share of the selected packets
   std::vector<Chunk> chunks;
   std::vector<uint64_t> off;  // staging offset of selected packet k0 + j inside its chunk
@@ -788,6 +811,8 @@ struct Engine {
   Staging aux;
 };
 
+struct Combiner;  // (combined small launches, below)
+
 }  // namespace
 
 struct wg_tunn {
@@ -829,6 +854,8 @@ struct wg_engine {
   // NUMA node), held by one such call at a time
   Driver *driver = nullptr;
   std::mutex driver_mu;
+  Combiner *comb[2] = {nullptr, nullptr};  // [seal]: small launches of concurrent calls
+  std::mutex comb_mu;                             // (making them)
 };
 
 namespace {
@@ -1183,7 +1210,12 @@ bool word_event() {
   const char *e = std::getenv("WG_TUNN_WORD_EVENT");
   return e && std::atoi(e) != 0;
 }
-hipError_t wait_chunk(Staging &S) {
+hipError_t comb_wait(Staging &S, uint32_t m);
+hipError_t wait_chunk(Staging &S, uint32_t m) {
+  if (S.comb) {
+    S.flagged = false;
+    return comb_wait(S, m);
+  }
   if (S.flagged) {
     S.flagged = false;
     const volatile uint32_t *f = S.h_flag;
@@ -1202,11 +1234,202 @@ hipError_t wait_chunk(Staging &S) {
   return S.evented ? hipEventSynchronize(S.done) : hipStreamSynchronize(S.stream);
 }
 
+// Combined small launches.  NepTUN's workers each hand over at most 50 packets
+// (packet_workers.rs:27) from up to num_cpus::get_physical() threads at once
+// (:113-131).  Each such call is one latency-form launch -- a few microseconds of
+// launch and a kernel bound by PCIe latency, not by its 50 packets -- so concurrent
+// calls on one engine queue their launches behind each other.  A combiner per engine
+// and direction merges them: a call posts its chunk (its descriptors, staging bases)
+// and the first poster becomes the leader, which waits for a free launch slot (at most
+// WG_COMBINE_DEPTH combined launches in flight: calls arriving meanwhile join the
+// next one), takes every posted chunk, writes one descriptor array (absolute
+// addresses) and makes ONE launch with one completion word for all of them; each
+// call then waits for that word, copies its statuses and goes on with its own
+// in-order decisions.  Per packet the kernel does exactly what the call's own launch
+// would have done.  (WG_COMBINE=0: every call launches alone.)
+constexpr uint32_t kCombSlots = 4, kCombMax = 2048, kCombSegMax = 256;
+struct Combiner {
+  std::mutex mu;
+  std::vector<CombSeg *> pending;
+  bool leader = false;
+  CombSlot slot[kCombSlots];
+  uint32_t next = 0;
+  wg_gpu_ctx *ctx = nullptr;
+  bool seal = false;
+  std::atomic<uint32_t> shared_calls{0};  // chunks that went out in a launch with another call's
+};
+
+bool combine_on() {  // (read per call)
+  const char *e = std::getenv("WG_COMBINE");
+  return !e || std::atoi(e) != 0;
+}
+uint32_t combine_depth() {  // combined launches in flight per engine and direction (1 .. kCombSlots)
+  const char *e = std::getenv("WG_COMBINE_DEPTH");
+  return e ? (uint32_t)std::min<long>(kCombSlots, std::max(1L, std::atol(e))) : 2u;
+}
+
+void comb_free(Combiner *C) {
+  if (!C) return;
+  for (CombSlot &S : C->slot) {
+    if (S.stream) (void)hipStreamSynchronize(S.stream);
+    (void)hipHostFree(S.desc);
+    (void)hipHostFree(S.st);
+    (void)hipHostFree(S.h_flag);
+    (void)hipFree(S.d_count);
+    if (S.stream) (void)hipStreamDestroy(S.stream);
+  }
+  delete C;
+}
+
+Combiner *comb_get(wg_engine *g, bool seal) {
+  std::lock_guard<std::mutex> lk(g->comb_mu);
+  if (Combiner *C = g->comb[seal ? 1 : 0]) return C;
+  Combiner *C = new (std::nothrow) Combiner;
+  if (!C) return nullptr;
+  C->ctx = g->ctx;
+  C->seal = seal;
+  DevGuard dg(g->device);
+  bool ok = true;
+  for (CombSlot &S : C->slot) {
+    ok = ok && hipHostMalloc((void **)&S.desc, kCombMax * sizeof(wg_packet_desc), hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipHostMalloc((void **)&S.st, kCombMax * 4, hipHostMallocDefault) == hipSuccess;
+    ok = ok && hipHostMalloc((void **)&S.h_flag, 64, hipHostMallocCoherent) == hipSuccess;
+    ok = ok && hipMalloc((void **)&S.d_count, 64) == hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMemsetAsync(S.d_count, 0, 64, S.stream) == hipSuccess && hipStreamSynchronize(S.stream) == hipSuccess;
+    if (ok) *S.h_flag = 0;
+  }
+  if (!ok) {
+    comb_free(C);
+    return nullptr;
+  }
+  g->comb[seal ? 1 : 0] = C;
+  return C;
+}
+
+// the launch of slot S has completed (its word, or a stream sync after 200 us)
+hipError_t comb_wait_word(const CombSlot &S, uint32_t seq) {
+  const volatile uint32_t *f = S.h_flag;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1;; ++i) {
+    if ((int32_t)(*f - seq) >= 0) {  // (this launch or a later one of the slot)
+      std::atomic_thread_fence(std::memory_order_acquire);
+      return hipSuccess;
+    }
+    if ((i & 255u) == 0u &&
+        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() > 200)
+      return hipStreamSynchronize(S.stream);
+    _mm_pause();
+  }
+}
+
+// One leader round: a free slot (at most `depth` launches in flight), every posted
+// chunk that fits, one launch.  Called with C.mu held and C.leader set; returns with
+// C.mu held.
+void comb_launch_round(Combiner &C, std::unique_lock<std::mutex> &lk) {
+  const uint32_t depth = combine_depth();
+  CombSlot &S = C.slot[C.next % depth];
+  lk.unlock();
+  // the slot's previous launch done and its statuses taken (calls arriving meanwhile
+  // join this round)
+  (void)comb_wait_word(S, S.seq);
+  while (S.readers.load(std::memory_order_acquire) != 0) _mm_pause();
+  lk.lock();
+  std::vector<CombSeg *> batch;
+  uint32_t n = 0, max_len = 0;
+  size_t k = 0;
+  for (; k < C.pending.size(); ++k) {
+    CombSeg *g = C.pending[k];
+    if (n + g->n > kCombMax && n) break;
+    batch.push_back(g);
+    n += g->n;
+    max_len = std::max(max_len, g->max_len);
+  }
+  C.pending.erase(C.pending.begin(), C.pending.begin() + (long)k);
+  ++C.next;
+  if (batch.size() > 1) C.shared_calls.fetch_add((uint32_t)batch.size(), std::memory_order_relaxed);
+  lk.unlock();
+  uint32_t off = 0;
+  for (CombSeg *g : batch) {
+    for (uint32_t j = 0; j < g->n; ++j) {
+      wg_packet_desc d = g->descs[j];
+      d.src_off += g->in_base;
+      d.dst_off += g->out_base;
+      S.desc[off + j] = d;
+    }
+    g->off = off;
+    off += g->n;
+  }
+  const uint32_t seq = S.seq + 1;
+  S.readers.store((int)batch.size(), std::memory_order_relaxed);
+  bool flagged = false;
+  int rc = wg_launch_desc_hinted(C.ctx, C.seal, S.desc, n, nullptr, nullptr, S.st, S.stream, max_len, true,
+                                 S.d_count, S.h_flag, seq, &flagged, true, true);
+  if (!rc && !flagged) {  // (not the latency form after all: the host publishes the word)
+    const hipError_t e = hipStreamSynchronize(S.stream);
+    if (e != hipSuccess) rc = wg_pipe_fail(WG_RC_HIP_ERROR, "tunn: combined launch", e);
+    else *(volatile uint32_t *)S.h_flag = seq;
+  }
+  if (rc) S.readers.store(0, std::memory_order_relaxed);
+  S.seq = seq;
+  for (CombSeg *g : batch) {
+    g->rc = rc;
+    g->slot = &S;
+    g->seq = seq;
+    g->ready.store(1, std::memory_order_release);
+  }
+  lk.lock();
+}
+
+// post a chunk; returns once it is launched (g->slot / seq / off) or failed (g->rc)
+int comb_submit(Combiner &C, CombSeg &g) {
+  g.ready.store(0, std::memory_order_relaxed);
+  g.rc = WG_RC_OK;
+  std::unique_lock<std::mutex> lk(C.mu);
+  C.pending.push_back(&g);
+  for (;;) {
+    if (!C.leader) {
+      C.leader = true;
+      // lead until this chunk is out (and whatever else is posted by then)
+      while (!g.ready.load(std::memory_order_acquire) && !C.pending.empty()) comb_launch_round(C, lk);
+      C.leader = false;
+      return g.rc;
+    }
+    lk.unlock();
+    for (uint32_t i = 0; !g.ready.load(std::memory_order_acquire); ++i) {
+      _mm_pause();
+      if ((i & 63u) == 63u) {  // the leader may have stepped down with this chunk still posted
+        lk.lock();
+        if (!C.leader && !g.ready.load(std::memory_order_acquire)) break;
+        lk.unlock();
+      }
+    }
+    if (g.ready.load(std::memory_order_acquire)) return g.rc;
+  }
+}
+
+// the combined launch's completion for a chunk: its word, then its statuses
+hipError_t comb_wait(Staging &S, uint32_t m) {
+  CombSeg *g = S.comb;
+  S.comb = nullptr;
+  const hipError_t e = comb_wait_word(*g->slot, g->seq);
+  if (e == hipSuccess) std::memcpy(S.h_st, g->slot->st + g->off, (size_t)m * 4);
+  g->slot->readers.fetch_sub(1, std::memory_order_acq_rel);
+  return e;
+}
+
 struct PipelineDrain {
   Engine &E;
   explicit PipelineDrain(Engine &e) : E(e) { drain(); }
   ~PipelineDrain() { drain(); }
   void drain() {
+    for (auto &S : E.st)
+      if (S.comb) {  // (an error path left a combined chunk unwaited: its kernel may still use the staging)
+        CombSeg *g = S.comb;
+        S.comb = nullptr;
+        (void)comb_wait_word(*g->slot, g->seq);
+        g->slot->readers.fetch_sub(1, std::memory_order_acq_rel);
+      }
     for (auto &S : E.st)
       if (S.busy) {
         (void)hipStreamSynchronize(S.stream);
@@ -1250,7 +1473,7 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
   auto stage_mid = [&](size_t c) -> int {
     Staging &S = E.st[c % sets];
     const double a = now_us();
-    TUNN_HIP(wait_chunk(S), "tunn: chunk wait");
+    TUNN_HIP(wait_chunk(S, (uint32_t)(E.chunks[c].k1 - E.chunks[c].k0)), "tunn: chunk wait");
     E.ph.wait_us += now_us() - a;
     const int mr = (int)mid(E.chunks[c], S);
     if (mr == -2)
@@ -1324,12 +1547,28 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
         *S.h_flag = 0;
         S.done_seq = 0;
       }
-      if (word) ++S.done_seq;
-      // (the kernel reads the packets over PCIe: hint the latency form's choice)
-      const int rc = wg_launch_desc_hinted(E.ctx, seal, S.h_desc, (uint32_t)m, in, out, S.h_st, S.stream,
-                                           max_desc_len(S.h_desc, m), true, word ? S.d_count : nullptr,
-                                           word ? S.h_flag : nullptr, S.done_seq, &S.flagged, true, true);
-      if (rc) return rc;
+      // (a call of one chunk only: a caller never holds a slot's statuses while it
+      // leads another round, whose slot may be that one)
+      if (word && nc == 1 && m <= kCombSegMax && E.grp && combine_on()) {
+        // one launch with the engine's other small calls of this direction (Combiner)
+        Combiner *C = comb_get(E.grp, seal);
+        if (!C) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn: combiner", hipSuccess);
+        S.cseg.descs = S.h_desc;
+        S.cseg.n = (uint32_t)m;
+        S.cseg.max_len = max_desc_len(S.h_desc, m);
+        S.cseg.in_base = reinterpret_cast<uint64_t>(in);
+        S.cseg.out_base = reinterpret_cast<uint64_t>(out);
+        if (const int rc = comb_submit(*C, S.cseg)) return rc;
+        S.comb = &S.cseg;
+        S.flagged = true;
+      } else {
+        if (word) ++S.done_seq;
+        // (the kernel reads the packets over PCIe: hint the latency form's choice)
+        const int rc = wg_launch_desc_hinted(E.ctx, seal, S.h_desc, (uint32_t)m, in, out, S.h_st, S.stream,
+                                             max_desc_len(S.h_desc, m), true, word ? S.d_count : nullptr,
+                                             word ? S.h_flag : nullptr, S.done_seq, &S.flagged, true, true);
+        if (rc) return rc;
+      }
       if (timed) TUNN_HIP(hipEventRecord(S.ev[2], S.stream), "tunn: event");
     } else {
       if (!S.in_dma)
@@ -2136,6 +2375,7 @@ int lane_acquire(wg_engine *g, Engine **out) {
     if (g->lanes.size() < g->max_lanes) {
       Engine *E = nullptr;
       if (const int rc = make_engine(g->ctx, false, 1, &E, g->pool, (unsigned)g->lanes.size())) return rc;
+      E->grp = g;
       g->lanes.push_back(E);
       *out = E;
       return WG_RC_OK;
@@ -2212,6 +2452,8 @@ int engine_make(wg_gpu_ctx *ctx, wg_engine **out) {
 
 void engine_free(wg_engine *g) {
   for (Engine *E : g->lanes) destroy_engine(E);
+  comb_free(g->comb[0]);
+  comb_free(g->comb[1]);
   delete g->driver;
   delete g->pool;
   delete g;
@@ -2288,6 +2530,11 @@ int wg_engine_get_info(const wg_engine *e, wg_engine_info *out) {
   out->max_lanes = e->max_lanes;
   out->pool_threads = e->pool->size();
   out->streams = out->lanes * kLaneStreams;
+  {
+    std::lock_guard<std::mutex> cl(const_cast<wg_engine *>(e)->comb_mu);
+    for (const Combiner *C : e->comb)
+      if (C) out->combined += C->shared_calls.load(std::memory_order_relaxed);
+  }
   return WG_RC_OK;
 }
 

@@ -47,7 +47,7 @@ class Phases(ctypes.Structure):
 class EngineInfo(ctypes.Structure):
     """wg_engine_info: what a shared engine holds."""
     _fields_ = [(f, ctypes.c_uint32) for f in ("tunns", "lanes", "max_lanes", "pool_threads", "streams",
-                                               "pad")]
+                                               "combined")]
 
 
 def _bind(L):
@@ -137,7 +137,7 @@ class Engine:
     def info(self) -> dict:
         i = EngineInfo()
         check(self._lib.wg_engine_get_info(self._h, ctypes.byref(i)), "wg_engine_get_info")
-        return {f: getattr(i, f) for f, _ in EngineInfo._fields_ if f != "pad"}
+        return {f: getattr(i, f) for f, _ in EngineInfo._fields_}
 
     def close(self):
         if getattr(self, "_h", None):

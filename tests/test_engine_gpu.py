@@ -319,6 +319,82 @@ def test_concurrent_calls_share_the_engine(big_ctx):
     eng.close()
 
 
+@pytest.mark.parametrize("depth", ["1", "2"])
+def test_concurrent_small_calls_combine_into_shared_launches(big_ctx, monkeypatch, depth):
+    """NepTUN's shape: 8 threads, each its own peer's Tunn on one engine, calls of 1-64
+    packets (staged and registered, encapsulate and decapsulate with damaged traffic)
+    at the same time.  Concurrent calls of one direction go out in shared launches
+    (the engine's combiner, WG_COMBINE_DEPTH in flight) -- and every call still equals
+    its peer's sequential model."""
+    from neptun_amd import Engine
+
+    from test_tunn_gpu import Arena
+    monkeypatch.setenv("WG_TUNN_FLAG", "64")
+    monkeypatch.setenv("WG_COMBINE_DEPTH", depth)
+    rng = random.Random(808 + int(depth))
+    eng = Engine(big_ctx)
+    pairs = peers_with_sessions(rng, eng, 8, first=600, sessions=(1, 2))
+    errors = []
+    seeds = [rng.getrandbits(32) for _ in pairs]
+
+    def work(k):
+        try:
+            r = random.Random(seeds[k])
+            tm, tg, ses = pairs[k]
+            ctr_state = {}
+            for call in range(150):
+                n = r.choice([1, 16, 50, 50, 64])
+                reg = call % 3 == 1
+                if call % 2 == 0:
+                    srcs = [ipv4(r, r.choice([64, 1350, r.randrange(20, 1500)])) for _ in range(n)]
+                    caps = [len(x) + 32 for x in srcs]
+                    dm = [bytearray(b"\xee" * c) for c in caps]
+                    res_m = [tm.encapsulate(x, d) for x, d in zip(srcs, dm)]
+                    if reg:
+                        a, b = Arena(srcs, [0] * n), Arena([b""] * n, caps)
+                        for x in (a, b):
+                            big_ctx.register_host(*x.window())
+                        res_g = tg.encapsulate_ptrs(a.ptrs, a.lens, b.ptrs, np.array(caps, np.uint32))
+                        dg = [bytearray(b.get(j, caps[j])) for j in range(n)]
+                        for x in (a, b):
+                            big_ctx.unregister_host(x.window()[0])
+                    else:
+                        dg = [bytearray(b"\xee" * c) for c in caps]
+                        res_g = tg.encapsulate_batch(srcs, dg)
+                    check_same(res_g, res_m, dg, dm, f"thread {k} encap {call}")
+                else:
+                    dgs = datagrams(r, ses, n, ctr_state)
+                    caps = [max(len(d) - 16, 1) for d in dgs]
+                    dm = [bytearray(b"\xee" * c) for c in caps]
+                    res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+                    if reg:
+                        a, b = Arena(dgs, [0] * n), Arena([b""] * n, caps)
+                        for x in (a, b):
+                            big_ctx.register_host(*x.window())
+                        res_g = tg.decapsulate_ptrs(a.ptrs, a.lens, b.ptrs, np.array(caps, np.uint32))
+                        dg = [bytearray(b.get(j, caps[j])) for j in range(n)]
+                        for x in (a, b):
+                            big_ctx.unregister_host(x.window()[0])
+                    else:
+                        dg = [bytearray(b"\xee" * c) for c in caps]
+                        res_g = tg.decapsulate_batch(dgs, dg)
+                    check_same(res_g, res_m, dg, dm, f"thread {k} decap {call}")
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(len(pairs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[0]
+    check_state(pairs)
+    assert eng.info()["combined"] > 0, "no two concurrent small calls shared a launch"
+    for _, tg, _ in pairs:
+        tg.close()
+    eng.close()
+
+
 @pytest.fixture(scope="module")
 def two_ctx(torch_cuda):
     """Two contexts on device 0: the 1-GPU stand-in for one engine per GPU."""
