@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise tools/gpu_pmc_sizes.sh: per payload size, the descriptor kernels' HBM
+"""Summarise tools/gpu.sh step pmc-sizes: per payload size, the descriptor kernels' HBM
 bytes per packet against the algorithmic bytes (seal reads P, writes P + 32; open
 the reverse) and against what 32-byte-sector rounding of the packet's own bytes
 plus its 32-byte descriptor and 4-byte order entry would give.

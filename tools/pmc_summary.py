@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSVs (tools/pmc.sh output) per kernel: mean per dispatch.
+"""Summarise rocprofv3 --pmc CSVs (tools/gpu.sh step pmc-cmd output) per kernel: mean per dispatch.
 
 Derived numbers (per launch): HBM bytes with the gfx950 corrections of
 MI355X_MICROARCH.md "HBM": FETCH_SIZE (KiB) reads half of a wide streaming read
