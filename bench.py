@@ -448,10 +448,15 @@ def cpu_baseline(threads: int, cpus: dict, curve=(), size: int = 1350, op: str =
     # share of a machine other jobs also load is what gets measured
     t_ok = max(t for t, e in eff.items() if e >= 0.8)
     all_cores = threads >= cpus["physical_cores"]  # (a share that covers every core: measured)
+    # the baseline is the best measured thread count (on a shared grant more threads can
+    # measure less than fewer); the share's own point stays beside it
+    t_best = max(pts, key=lambda t: pts[t])
     out = {
-        "value": round(many["gbps_op"], 3),
+        "value": round(pts[t_best], 3),
         "unit": "Gbit/s",
-        "cores": threads,
+        "cores": t_best,
+        "value_at_share": round(many["gbps_op"], 3),
+        "threads_at_share": threads,
         "kind": "port",
         "cpu_model": cpus["model"],
         "physical_cores": cpus["physical_cores"],
@@ -461,10 +466,11 @@ def cpu_baseline(threads: int, cpus: dict, curve=(), size: int = 1350, op: str =
                    f" is the figure), one session "
                    f"per thread, NepTUN framing (session.rs:205-302) over OpenSSL 3 EVP_chacha20_poly1305 "
                    f"(stand-in for ring 0.17 asm; the Rust reference cannot be built here), each thread "
-                   f"pinned to its own physical core, median of 9 reps on {threads} threads = this job's "
-                   f"CPU share ({cpus['allowed_cpus']} CPUs in the affinity mask, {cpus['logical_cpus']} "
+                   f"pinned to its own physical core, median of 9 reps; value = the best measured thread "
+                   f"count ({t_best}) of {sorted(pts)} up to this job's CPU share of {threads} "
+                   f"({cpus['allowed_cpus']} CPUs in the affinity mask, {cpus['logical_cpus']} "
                    f"logical / {cpus['physical_cores']} physical cores on the machine, {cpus['model']}); "
-                   f"1 thread: {one['gbps_op']:.3f} Gbit/s"),
+                   f"1 thread: {one['gbps_op']:.3f} Gbit/s, {threads} threads: {many['gbps_op']:.3f} Gbit/s"),
         "one_core_gbps": round(one["gbps_op"], 3),
         "size": size, "op": op,
         "seal_gbps": round(many["seal_gbps_best"], 3), "open_gbps": round(many["open_gbps_best"], 3),
@@ -485,7 +491,7 @@ def cpu_baseline(threads: int, cpus: dict, curve=(), size: int = 1350, op: str =
                                     f"the machine"),
     }
     if all_cores:
-        out["all_physical_cores_gbps"] = out["value"]
+        out["all_physical_cores_gbps"] = out["value_at_share"]
         out["all_physical_cores_note"] = f"measured: the {threads} threads cover every physical core"
         del out["all_physical_cores_extrapolated_gbps"]
     return out

@@ -39,10 +39,13 @@ def test_cpu_baseline_fields():
     cpus = bench.host_cpus()
     t = max(1, min(2, cpus["physical_cores"], cpus["allowed_cpus"]))
     d = bench.cpu_baseline(t, cpus, [1])
-    assert d["cores"] == t and d["kind"] == "port" and d["value"] > 0
+    assert d["threads_at_share"] == t and d["kind"] == "port" and d["value"] > 0
     assert set(d["threads_gbps"]) == {"1", str(t)} and d["scaling_efficiency"]["1"] == 1.0
+    # value: the best measured thread count, its point beside the share's
+    assert d["value"] == max(d["threads_gbps"].values()) and d["threads_gbps"][str(d["cores"])] == d["value"]
+    assert d["value_at_share"] == d["threads_gbps"][str(t)]
     if t >= cpus["physical_cores"]:
-        assert d["all_physical_cores_gbps"] == d["value"]
+        assert d["all_physical_cores_gbps"] == d["value_at_share"]
     else:
         assert d["all_physical_cores_extrapolated_gbps"] > 0
         assert d["all_physical_cores_upper_bound_gbps"] >= d["all_physical_cores_extrapolated_gbps"] * 0.999
