@@ -399,7 +399,7 @@ def test_concurrent_small_calls_combine_into_shared_launches(big_ctx, monkeypatc
 def two_ctx(torch_cuda):
     """Two contexts on device 0: the 1-GPU stand-in for one engine per GPU."""
     from neptun_amd import GpuContext
-    ctxs = [GpuContext(0, key_slots=2048 * 16), GpuContext(0, key_slots=2048 * 16)]
+    ctxs = [GpuContext(0, key_slots=2049 * 16), GpuContext(0, key_slots=2049 * 16)]
     yield ctxs
     for c in ctxs:
         c.close()
@@ -485,7 +485,7 @@ def test_multi_peer_batches_across_engines_match_sequential_tunns(two_ctx, n_pee
         check_state(pairs)
     # a Tunn of wg_tunn_create_multi (private engines) cannot join an engine-free batch
     from neptun_amd import NeptunGpuError, Tunn
-    priv = Tunn(list(two_ctx), 2047 * 16)
+    priv = Tunn(list(two_ctx), 2048 * 16)  # (past the peers' slots)
     with pytest.raises(NeptunGpuError, match="private engines"):
         T.encapsulate_multi([pairs[0][1], priv], [b"x", b"y"], [bytearray(64), bytearray(64)])
     priv.close()
