@@ -5,6 +5,9 @@
  *
  *   tunn_threads T B [calls] [P]   -> one JSON line per run
  * GW_PRIVATE_ENGINES=1: one engine per Tunn (else the context's default engine).
+ * TT_REGISTER=1: every thread's buffers registered (wg_gpu_register_host): registered calls.
+ * The line also gives how many calls went out in a launch shared with another call
+ * (wg_engine_info.combined: the engine's combiner, WG_COMBINE).
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -24,6 +27,7 @@ static double now(void) {
 }
 
 typedef struct {
+  wg_gpu_ctx *ctx;
   wg_tunn *a, *b;
   uint32_t B, calls, P;
   double t_enc, t_dec;
@@ -38,6 +42,12 @@ static void *run(void *arg) {
   uint8_t **wd = calloc(B, sizeof *wd), **bd = calloc(B, sizeof *bd);
   uint32_t *len = calloc(B, 4), *cap = calloc(B, 4), *wlen = calloc(B, 4);
   wg_tunn_result *res = calloc(B, sizeof *res);
+  const int reg = getenv("TT_REGISTER") && atoi(getenv("TT_REGISTER"));
+  if (reg && (wg_gpu_register_host(j->ctx, src, (uint64_t)B * slot) || wg_gpu_register_host(j->ctx, wire, (uint64_t)B * slot) ||
+              wg_gpu_register_host(j->ctx, back, (uint64_t)B * slot))) {
+    j->rc = 99;
+    return NULL;
+  }
   for (uint32_t i = 0; i < B; ++i) {
     uint8_t *p = src + (size_t)i * slot + 16;
     memset(p, (int)i, P);
@@ -63,6 +73,11 @@ static void *run(void *arg) {
     for (uint32_t i = 0; i < B && !j->rc; ++i)
       if (res[i].kind != WG_TUNN_WRITE_TO_TUNNEL) j->rc = 100 + res[i].status;
   }
+  if (reg) {
+    wg_gpu_unregister_host(j->ctx, src);
+    wg_gpu_unregister_host(j->ctx, wire);
+    wg_gpu_unregister_host(j->ctx, back);
+  }
   free(src); free(wire); free(back); free(sp); free(wp); free(wd); free(bd); free(len); free(cap); free(wlen);
   free(res);
   return NULL;
@@ -81,6 +96,7 @@ int main(int argc, char **argv) {
   for (int i = 0; i < 32; ++i) k1[i] = (uint8_t)(3 * i + 1), k2[i] = (uint8_t)(7 * i + 5);
   for (uint32_t t = 0; t < T; ++t) {
     job_t *j = &jobs[t];
+    j->ctx = ctx;
     j->B = B, j->calls = calls, j->P = P;
     int rc;
 #ifdef TT_ENGINES
@@ -132,12 +148,21 @@ int main(int argc, char **argv) {
     ADD(copy_out_us) ADD(prep_us)
   }
   const double calls_all = (double)T * calls;
-  printf("{\"threads\": %u, \"batch\": %u, \"P\": %u, \"calls_per_thread\": %u, \"seconds\": %.4f, "
+  uint32_t combined = 0;
+#ifdef TT_ENGINES
+  {
+    wg_engine_info info;
+    if (!getenv("GW_PRIVATE_ENGINES") && wg_engine_get_info(wg_tunn_engine(jobs[0].a), &info) == 0)
+      combined = info.combined;
+  }
+#endif
+  printf("{\"threads\": %u, \"batch\": %u, \"P\": %u, \"calls_per_thread\": %u, \"registered\": %d, "
+         "\"combined_calls\": %u, \"seconds\": %.4f, "
          "\"roundtrip_gbps\": %.2f, \"encap_ms_per_call\": %.3f, \"decap_ms_per_call\": %.3f, "
          "\"encap_us\": {\"checks\": %.1f, \"pack\": %.1f, \"submit\": %.1f, \"wait\": %.1f, \"copy_out\": %.1f}, "
          "\"decap_us\": {\"checks\": %.1f, \"pack\": %.1f, \"submit\": %.1f, \"wait\": %.1f, \"decide\": %.1f, "
          "\"copy_out\": %.1f}}\n",
-         T, B, P, calls, secs, calls_all * B * P * 8.0 / secs / 1e9, te / calls_all * 1e3, td / calls_all * 1e3,
+         T, B, P, calls, getenv("TT_REGISTER") && atoi(getenv("TT_REGISTER")), combined, secs, calls_all * B * P * 8.0 / secs / 1e9, te / calls_all * 1e3, td / calls_all * 1e3,
          sa.checks_us / calls_all, sa.pack_us / calls_all, sa.submit_us / calls_all, sa.wait_us / calls_all,
          sa.copy_out_us / calls_all, sb.checks_us / calls_all, sb.pack_us / calls_all, sb.submit_us / calls_all,
          sb.wait_us / calls_all, sb.decide_us / calls_all, sb.copy_out_us / calls_all);
