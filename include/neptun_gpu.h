@@ -215,6 +215,17 @@ int wg_gpu_ctx_set_slot_padding(wg_gpu_ctx *ctx, int writable);
 int wg_gpu_ctx_set_xlane_lanes(wg_gpu_ctx *ctx, int64_t lanes);
 
 /*
+ * Split waves of the uniform strided batches (new; BASELINE's AEAD bench size 8192 B,
+ * chacha20poly1305_benching.rs:37-55): a batch whose waves of 64 packets fill only part
+ * of the chip runs each wave as `parts` jobs over consecutive rounds of its packets,
+ * and a finish kernel combines their Poly1305 sums (tags, checks, statuses).  parts
+ * < 0: the library's choice (a fill model, WG_SPLIT_K from the environment overrides);
+ * 1: never; 2, 4 or 8: that many where it divides the packets' keystream rounds into
+ * parts of at least 8 (else unsplit).  Results are identical either way.
+ */
+int wg_gpu_ctx_set_split(wg_gpu_ctx *ctx, int parts);
+
+/*
  * Handshake-side crypto, batched.  Device pointers,
  * asynchronous on `stream`.
  *   wg_gpu_x25519_batch: out[i] = X25519(scalars[i], points[i]) (RFC 7748;

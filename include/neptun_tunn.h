@@ -96,8 +96,9 @@ int wg_tunn_create_on(wg_engine *e, uint32_t first_slot, wg_tunn **out);
 /* what an engine holds: attached Tunns, lanes made so far, pool threads (incl. the
  * calling thread's share: workers + 1), HIP streams made so far (lanes' only), and
  * how many small calls' chunks went out in a launch shared with another concurrent
- * call (WG_COMBINE: one latency-form launch for the engine's concurrent small calls
- * of one direction, at most WG_COMBINE_DEPTH such launches in flight, default 2) */
+ * call (WG_COMBINE=1, off by default: one latency-form launch for the engine's
+ * concurrent small calls of one direction, at most WG_COMBINE_DEPTH such launches in
+ * flight, default 2) */
 typedef struct wg_engine_info {
   uint32_t tunns, lanes, max_lanes, pool_threads, streams;
   uint32_t combined;

@@ -1043,6 +1043,17 @@ struct PacketJob {
   int32_t status;
 };
 
+// One part of a split wave (StridedParams::split): rounds [r0, r1) of its 64 packets;
+// the lane's accumulator goes to h[idx] / h4[idx]
+struct SplitPart {
+  uint32_t r0, r1, idx;
+  uint4 *h;
+  uint32_t *h4;
+};
+#if WG_SPLIT && WG_POLY_RADIX26
+#error "split waves hand over radix-2^32 accumulators: build WG_POLY_RADIX26 with -DWG_SPLIT=0"
+#endif
+
 // The owner lane's side of a packet: everything but the cooperative memory
 // moves.  kUniform = every lane of the wave is live with the same length
 // (strided batches); then P, W and the round count are wave-uniform.
@@ -1053,11 +1064,12 @@ struct PacketJob {
 // (pre unused) -- the keystream keeps the in-place first diagonal round.
 // kInDesc: uniform geometry inside a descriptor kernel (the affine groups).
 template <bool kSeal, bool kUniform, bool kSync, bool kUKey = false, bool kLaneKeys = false,
-          bool kInDesc = false, class Stage, class Geom>
+          bool kInDesc = false, bool kSplit = false, class Stage, class Geom>
 __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, PacketJob job,
                                          const uint8_t *keys, const uint32_t *key_index,
                                          int32_t *status_out, const SessionKey *pre = nullptr,
-                                         uint64_t next_hdr = 0, bool hdr_ready = false) {
+                                         uint64_t next_hdr = 0, bool hdr_ready = false,
+                                         const SplitPart *sp = nullptr) {
   // run grid (Ranges): kG = grid coordinate of text byte 0
   constexpr bool kText = Geom::kTextGrid;
   constexpr uint32_t kG = kText ? 0u : 16u;
@@ -1084,8 +1096,16 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   uint32_t my_runs = job.status == WG_STATUS_OK ? (W - (16u - kG) + kRun - 1) / kRun : 0u;
   uint32_t rounds;
   uint32_t p_min = 0u;  // descriptor batches, phase-locked: the wave's shortest live payload
+  // a split part runs rounds [r_begin, r_end) (wave-uniform; the phase-locked calls
+  // still match: every part has the same number of keystream rounds, see wg_gpu.cpp)
+  constexpr bool split = kUniform && kSync && kSplit;
+  uint32_t r_begin = 0u;
   if constexpr (kUniform) {
     rounds = my_runs;  // uniform: job.len is a kernel argument
+    if constexpr (split) {
+      r_begin = sp->r0;
+      rounds = min(sp->r1, my_runs);
+    }
   } else if constexpr (kSync) {
     p_min = wave_min32(my_runs ? P : 0xffffffffu);
     uint32_t ls = lane;  // (opaque: no kernel-lifetime LDS addresses to hold and spill)
@@ -1129,7 +1149,7 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   uint32_t tag_bad = 0u;  // pf: the tag check's result, from the last round
   if constexpr (kPfBuild) {
     const uint32_t last = rounds - 1u, gend = W - (16u - kG);
-    pf = rounds >= 2u && (wt >> 7) == last && (q == 0u || ((wt + 16u) >> 7) == last) &&
+    pf = !split && rounds >= 2u && (wt >> 7) == last && (q == 0u || ((wt + 16u) >> 7) == last) &&
          gend <= kRun * last + 112u;
   }
 
@@ -1141,9 +1161,18 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     // round 0's DMA (wave-uniform call site).  Open computes it per lane as
     // soon as the lane's header has landed: locking it there made every wave
     // wait for the slowest header (-4 %).
-    if constexpr ((kSync && kSeal && WG_SYNC_KEY_BLOCK) || kSyncOpenKey)
+    if (!kText && split && r_begin > 0u) {  // (split: compile-time)
+      // a later part: block 0 and block 2 r_begin, whose last 16 bytes are chunk 0 of
+      // the part's first round (the wire grid's carry, apply_chunk0) -- one call with
+      // the barriers of a single block, so every part's calls still match
+      uint32_t kc[16];
+      chacha20_block_pair_sync(ks, kc, key, 0u, 2u * r_begin, n1, n2);
+      ks_save[0] = kc[12]; ks_save[1] = kc[13]; ks_save[2] = kc[14]; ks_save[3] = kc[15];
+    } else if constexpr ((kSync && kSeal && WG_SYNC_KEY_BLOCK) || kSyncOpenKey) {
       chacha20_block_sync(ks, key, 0u, n1, n2);
-    else chacha20_block(ks, key, 0u, n1, n2);
+    } else {
+      chacha20_block(ks, key, 0u, n1, n2);
+    }
     poly_init(poly, ks);
     // s, read back for the tag.  An inline-asm LDS write: the compiler cannot
     // tell the park from the run buffer that round 0's LDS-DMA (in flight
@@ -1234,11 +1263,15 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     }
     if ((wt >> 7) == r) {
       // all ciphertext is MACed: LE64(aad_len=0) | LE64(ct_len), then the tag
-      poly_block(poly, 0u, 0u, P, 0u);
-      uint32_t tag[4];
-      const uint4 sp = S.park[tl];
-      const uint32_t s[4] = {sp.x, sp.y, sp.z, sp.w};
-      poly_finish(poly, s, tag);
+      // (a split part holds only its share of the MAC: zeros here, the finish kernel
+      // writes the tag over them)
+      uint32_t tag[4] = {0u, 0u, 0u, 0u};
+      if (!split) {
+        poly_block(poly, 0u, 0u, P, 0u);
+        const uint4 sp4 = S.park[tl];
+        const uint32_t s[4] = {sp4.x, sp4.y, sp4.z, sp4.w};
+        poly_finish(poly, s, tag);
+      }
       const uint32_t ka = (wt >> 4) & 7u;
       uint32_t ct[4] = {0, 0, 0, 0};
       if (q) {
@@ -1300,8 +1333,8 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     // open: each lane fetches its own header ahead of round 0's DMA, so the
     // round-0 keystream waits for 16 bytes, not for the whole stage
     // (round 0's DMA is issued before the loop so the header is consumed, and
-    // its registers freed, before the loop body)
-    if (rounds) {
+    // its registers freed, before the loop body; a split part: its first round's)
+    if (rounds > r_begin) {
       uint4 hdr = make_uint4(0u, 0u, 0u, 0u);
       if constexpr (!kSeal && kUniform && WG_HDR_DMA && !WG_ABLATE_NO_MEM) {
         // Uniform open: the 64 headers go to the tag park by one LDS-DMA piece
@@ -1313,7 +1346,7 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // tag park is free until round 0's tag bytes land (open_keep_tail).
         if (my_runs && !(kPfBuild && hdr_ready))
           dma_global<WG_HDR_NT != 0>(lds_offset(&S.tagp[0]), reinterpret_cast<const uint8_t *>(job.in_base - (16u - kG)));
-        stage_in<kSeal>(run, g, lane, 0);  // exactly 8 pieces (round 0 is straight-line)
+        stage_in<kSeal>(run, g, lane, r_begin);  // exactly 8 pieces (the first round is straight-line)
         u32x4 h;
         if (kPfBuild && hdr_ready)  // (landed during the previous group: its rounds waited vmcnt(0))
           asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
@@ -1339,7 +1372,7 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
         // them through every group and spills them: ~40 scratch reloads per group)
         uint32_t ln0 = lane;
         if constexpr (kOpaqueDesc) asm volatile("" : "+v"(ln0));
-        stage_in<kSeal>(run, g, ln0, 0);
+        stage_in<kSeal>(run, g, ln0, r_begin);
 #endif
       }
       if (kSeal && !WG_ABLATE_NO_KEYBLOCK) one_time_key();  // while round 0's DMA is in flight (every wave: phase-locked)
@@ -1371,7 +1404,7 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 #endif
       WG_STAMP_AT(kSeal, r, 0);
 #if !WG_ABLATE_NO_MEM
-      if (r > 0) stage_in<kSeal>(run, g, ln, r);
+      if (r > r_begin) stage_in<kSeal>(run, g, ln, r);
 #endif
       if constexpr (kPfBuild) {  // the next group's headers into the (free) tag park
         if (pf && r == 1u && next_hdr)
@@ -1443,7 +1476,7 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
 #endif
       WG_STAMP_AT(kSeal, r, 5);
     };
-    for (uint32_t r = 0; r < rounds; ++r) do_round(r);
+    for (uint32_t r = r_begin; r < rounds; ++r) do_round(r);
   } else {
     uint4 *run = S.run[0];
     for (uint32_t r = 0; r < rounds; ++r) {
@@ -1478,6 +1511,13 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     }
   }
 
+  if constexpr (split) {
+    // this part's share of the MAC (the finish kernel combines the parts; the open's
+    // header statuses, tag check and zeroing are its too)
+    sp->h[sp->idx] = make_uint4(poly.h0, poly.h1, poly.h2, poly.h3);
+    sp->h4[sp->idx] = poly.h4;
+    return false;
+  }
   if (!kSeal && job.status == WG_STATUS_OK) {
     uint32_t diff = 0;
     if (kPfBuild && pf) {
@@ -1545,11 +1585,12 @@ struct GroupWalk {
 // uniform geometry; kTail = true is a one-wave launch for the n % 64 packets
 // left over (generic geometry), so the hot kernel carries no generic path.
 // one wave's 64 packets [pkt0, pkt0 + 64) of a strided batch
-template <bool kSeal, bool kTail, bool kText, class Stage>
+template <bool kSeal, bool kTail, bool kText, class Stage, bool kSplit = false>
 __device__ __forceinline__ bool strided_group(Stage &stage, const StridedParams &prm,
                                               uint32_t pkt0, uint32_t lane,
                                               const SessionKey *sk = nullptr,
-                                              uint64_t next_hdr = 0, bool hdr_ready = false) {
+                                              uint64_t next_hdr = 0, bool hdr_ready = false,
+                                              const SplitPart *sp = nullptr) {
   const uint32_t i = pkt0 + lane;
   PacketJob job;
   job.slot = prm.key_slot;
@@ -1586,8 +1627,8 @@ __device__ __forceinline__ bool strided_group(Stage &stage, const StridedParams 
     }
 #endif
     // (the text grid exists only in the phase-locked form)
-    return run_wave<kSeal, true, WG_SYNC != 0 || kText>(stage, g, lane, job, prm.keys, prm.key_index, st,
-                                                        sk, next_hdr, hdr_ready);
+    return run_wave<kSeal, true, WG_SYNC != 0 || kText, false, false, false, kSplit>(
+        stage, g, lane, job, prm.keys, prm.key_index, st, sk, next_hdr, hdr_ready, sp);
   } else {
     job.status = i < prm.n ? WG_STATUS_OK : -1;  // -1: lane past the batch end
     LdsGeom g{stage};
@@ -1596,8 +1637,8 @@ __device__ __forceinline__ bool strided_group(Stage &stage, const StridedParams 
   }
 }
 
-template <bool kSeal, bool kTail, bool kText>
-__device__ __forceinline__ void strided_body(const StridedParams &prm) {
+template <bool kSeal, bool kTail, bool kText, bool kSplit = false>
+__device__ __forceinline__ void strided_body(const StridedParams &prm, const SplitArgs *sa = nullptr) {
   using Stage = typename std::conditional<kTail, WaveStage, WaveStageUniform>::type;
   constexpr uint32_t kWaves = (kTail ? kBlockThreads : kStridedThreads) / 64u;
   __shared__ Stage stage[kWaves];
@@ -1651,6 +1692,31 @@ __device__ __forceinline__ void strided_body(const StridedParams &prm) {
       const uint32_t odd = mode == 1u ? (b & 1u) : mode == 2u ? ((b >> 8) & 1u) : ((b >> 3) & 1u);
       vwave = (wave + kWaves - 2u * odd) % kWaves;
     }
+#if WG_SPLIT && WG_SYNC
+    if constexpr (kSplit) {  // (a kernel of its own: the unsplit kernels keep their registers)
+      // split waves: unit u = part * W64 + wave-of-packets (part-major: the waves of a
+      // workgroup run the same round range), a part's rounds [part q, part q + q), the
+      // last part to the packets' end
+      const uint32_t w64 = prm.n / 64u, units = w64 * sa->split;
+      uint32_t u_first = blockIdx.x * kWaves + wave, u_end = units, u_step = gridDim.x * kWaves;
+      if (prm.spread) {  // (one pass: this workgroup's even share of the units)
+        u_first = spread_lo(units, blockIdx.x, gridDim.x) + vwave;
+        u_end = spread_lo(units, blockIdx.x + 1u, gridDim.x);
+        u_step = kWaves;
+      }
+      for (uint32_t u = u_first; u < u_end; u += u_step) {
+        const uint32_t part = u / w64, pkt0 = (u - part * w64) * 64u;
+        SplitPart spt;
+        spt.r0 = part * sa->split_q;
+        spt.r1 = part + 1u == sa->split ? 0xffffffffu : spt.r0 + sa->split_q;
+        spt.idx = pkt0 + lane;
+        spt.h = sa->part_h + (size_t)part * (w64 * 64u);
+        spt.h4 = sa->part_h4 + (size_t)part * (w64 * 64u);
+        strided_group<kSeal, false, kText, Stage, true>(stage[wave], prm, pkt0, lane, &sk, 0, false, &spt);
+      }
+      return;
+    }
+#endif
     for (uint32_t grp = g_first; grp < g_end; grp += g_step) {
       const uint32_t pkt0 = prm.spread ? (s_lo + vwave) * 64u : (grp * kWaves + wave) * 64u;
       // only the last group can be partial, and it is this workgroup's last
@@ -1680,6 +1746,115 @@ __global__ __launch_bounds__(kTail ? kBlockThreads : kStridedThreads,
                              kTail ? WG_WAVES_PER_SIMD : kStridedMinWaves) void
 aead_strided_kernel(StridedParams prm) {
   strided_body<kSeal, kTail, false>(prm);
+}
+
+// The split waves' finish (StridedParams::split): one thread per packet of the full
+// waves.  The parts' accumulators are Horner sums over their own ciphertext pieces,
+// so the packet's is h = (..(h_0 r^k_1 + h_1) r^k_2 + ..) + h_last (k_j: part j's
+// pieces), taken in radix 2^26 (powers of r are not clamped, wg_crypto.h f26_*); then
+// the length block and + s as always (RFC 8439 2.8).  Seal writes the tag over the
+// zeros the last part left; open checks the header (noise/mod.rs:170-180,
+// session.rs:275-277) and the tag, zeroes a failed packet's plaintext (ring's
+// open_within), and every packet gets its status here.
+template <bool kSeal, bool kText>
+__global__ __launch_bounds__(256) void aead_strided_finish_kernel(StridedSplitParams sp) {
+  const StridedParams &prm = sp.prm;
+  const SplitArgs &sa = sp.sa;
+  const uint32_t n = prm.n & ~63u;
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t P = kSeal ? prm.len : prm.len - WG_DATA_OVERHEAD_SZ;  // (open: len >= 32, the host checks)
+  const uint8_t *src = prm.src + (uint64_t)i * prm.src_stride;
+  uint8_t *dst = prm.dst + (uint64_t)i * prm.dst_stride;
+  uint32_t key[8];
+  {
+    const uint8_t *kp = prm.keys + 32u * prm.key_slot;
+    const uint4 a = ld16(kp), b = ld16(kp + 16u);
+    key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
+    key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
+  }
+  const uint32_t sidx = prm.key_index[prm.key_slot];
+  int32_t status = WG_STATUS_OK;
+  uint32_t n1, n2;
+  if (kSeal) {
+    const uint64_t c = prm.counter_base + i;
+    n1 = (uint32_t)c;
+    n2 = (uint32_t)(c >> 32);
+  } else {
+    const uint4 h = ld16(src);
+    if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
+    else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;
+    n1 = h.z;
+    n2 = h.w;
+  }
+  if (status == WG_STATUS_OK) {
+    uint32_t ks[16];
+    chacha20_block(ks, key, 0u, n1, n2);
+    Poly ps;
+    poly_init(ps, ks);
+    const F26 r26 = f26_from32(ps.r0, ps.r1, ps.r2, ps.r3, 0u);
+    // pieces (16-byte ciphertext chunks, the last one partial) of rounds [a, b): text
+    // offsets m = 128 r - 16 + 16 k (wire grid: chunk 0 of round 0 is the header) or
+    // m = 128 r + 16 k (text grid), those with m < P
+    const uint32_t P16 = (P + 15u) & ~15u;
+    auto pieces = [&](uint32_t a, uint32_t b) -> uint32_t {
+      const uint32_t lo = kText ? min(128u * a, P16) : min(a ? 128u * a - 16u : 0u, P16);
+      const uint32_t hi = kText ? min(128u * b, P16) : min(b ? 128u * b - 16u : 0u, P16);
+      return (hi - lo) / 16u;
+    };
+    const size_t stride = (size_t)n;
+    F26 acc;
+    for (uint32_t j = 0; j < sa.split; ++j) {
+      const uint4 hq = sa.part_h[j * stride + i];
+      const F26 hj = f26_from32(hq.x, hq.y, hq.z, hq.w, sa.part_h4[j * stride + i]);
+      if (j == 0) {
+        acc = hj;
+      } else {
+        const uint32_t a = j * sa.split_q, b = j + 1u == sa.split ? 0x7fffffffu / 128u : a + sa.split_q;
+        const uint32_t k = pieces(a, b);
+        acc = f26_add(k ? f26_mul(acc, f26_pow(r26, k)) : acc, hj);
+      }
+    }
+    f26_to32(acc, ps.h0, ps.h1, ps.h2, ps.h3, ps.h4);
+    poly_block(ps, 0u, 0u, P, 0u);  // le64(AAD len = 0) | le64(P)
+    const uint32_t s4[4] = {ks[4], ks[5], ks[6], ks[7]};
+    uint32_t tag[4];
+    poly_finish(ps, s4, tag);
+    if (kSeal) {
+      uint8_t *t = dst + WG_DATA_OFFSET + P;  // (session.rs:247-252)
+      if ((P & 15u) == 0u) {
+        st16(t, tag[0], tag[1], tag[2], tag[3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t[q] = (uint8_t)(tag[q / 4] >> (8 * (q % 4)));
+      }
+    } else {
+      // received tag: bytes [16 + P, 32 + P) of the datagram, in two aligned pieces
+      const uint8_t *in = src + WG_DATA_OFFSET;
+      const uint32_t o = P & ~15u;
+      const uint4 ta = ld16(in + o);
+      const uint4 tb = (P & 15u) ? ld16(in + o + 16u) : make_uint4(0, 0, 0, 0);
+      const uint32_t tw[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+      uint32_t bad = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bad |= bytes_at(tw, (int)(P & 15u) + 4 * j) ^ tag[j];
+      if (bad) {
+        status = WG_STATUS_INVALID_AEAD_TAG;
+        for (uint32_t off = 0; off + 16u <= P; off += 16u) st16(dst + off, 0u, 0u, 0u, 0u);
+        if (P & 15u) {
+          const uint32_t z[4] = {0, 0, 0, 0};
+          store_partial(dst + (P & ~15u), z, (int)(P & 15u));
+        }
+      }
+    }
+  }
+  if (prm.status) prm.status[i] = status;
+}
+
+// the split waves' kernels (StridedParams::split > 1; kText: open on the text grid)
+template <bool kSeal, bool kText>
+__global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_strided_split_kernel(StridedSplitParams sp) {
+  strided_body<kSeal, false, kText, true>(sp.prm, &sp.sa);
 }
 
 // open on the text grid (Ranges): destinations whose plaintext slots start on
@@ -1911,6 +2086,12 @@ __global__ __launch_bounds__(kStridedThreads, kStridedMinWaves) void aead_desc_a
   desc_sync_body<kSeal, true, true>(prm);
 }
 
+template __global__ void aead_strided_split_kernel<true, false>(StridedSplitParams);
+template __global__ void aead_strided_split_kernel<false, false>(StridedSplitParams);
+template __global__ void aead_strided_split_kernel<false, true>(StridedSplitParams);
+template __global__ void aead_strided_finish_kernel<true, false>(StridedSplitParams);
+template __global__ void aead_strided_finish_kernel<false, false>(StridedSplitParams);
+template __global__ void aead_strided_finish_kernel<false, true>(StridedSplitParams);
 template __global__ void aead_strided_kernel<true, false>(StridedParams);
 template __global__ void aead_strided_kernel<false, false>(StridedParams);
 template __global__ void aead_strided_kernel<true, true>(StridedParams);

@@ -63,6 +63,27 @@ struct StridedParams {
   uint32_t spread;            // 1: under-filled launch, even wave shares in one pass (WG_SPREAD)
 };
 
+// Split (under-filled launches of long packets, wg_gpu.cpp): every wave of 64 packets
+// is cut into `split` parts of split_q keystream rounds each, every part a wave job of
+// its own, so that the grid fills the chip; the parts' Poly1305 accumulators go to
+// part_h / part_h4 ([part][packet]) and aead_strided_finish_kernel combines them,
+// writes the tags (seal) or checks them (open) and the statuses.  (Kernels of their
+// own with their own argument block: the unsplit kernels are compiled as before.)
+struct SplitArgs {
+  uint32_t split, split_q;
+  uint4 *part_h;
+  uint32_t *part_h4;
+};
+struct StridedSplitParams {
+  StridedParams prm;
+  SplitArgs sa;
+};
+#ifndef WG_SPLIT
+#define WG_SPLIT 1
+#endif
+template <bool kSeal, bool kText> __global__ void aead_strided_split_kernel(StridedSplitParams sp);
+template <bool kSeal, bool kText> __global__ void aead_strided_finish_kernel(StridedSplitParams sp);
+
 struct DescParams {
   const uint8_t *keys;
   const uint32_t *key_index;

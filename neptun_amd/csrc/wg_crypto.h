@@ -201,16 +201,19 @@ __device__ __forceinline__ void chacha20_block_sync(uint32_t (&ks)[16], const ui
 // keystream blocks blk and blk+1 (same key and nonce) into ka, kb.  kShared:
 // the first diagonal round on the blocks' common words (below); the descriptor
 // kernels (per-lane keys) keep the in-place form, where it cost one more spill.
+// chacha20_block_pair_sync: any two blocks blk, blk_b of one key and nonce (they too
+// differ in word 12 only) -- the split strided kernels' first call of a part, block 0
+// (the Poly1305 key) with the block whose last 16 bytes the part's first round needs.
 template <bool kShared = WG_SHARED_DIAG>
-__device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_t (&kb)[16],
-                                                     const uint32_t k[8], uint32_t blk,
-                                                     uint32_t n1, uint32_t n2) {
+__device__ __forceinline__ void chacha20_block_pair_sync(uint32_t (&ka)[16], uint32_t (&kb)[16],
+                                                         const uint32_t k[8], uint32_t blk, uint32_t blk_b,
+                                                         uint32_t n1, uint32_t n2) {
   uint32_t p0 = kSigma0, p1 = kSigma1, p2 = kSigma2, p3 = kSigma3;
   uint32_t p4 = k[0], p5 = k[1], p6 = k[2], p7 = k[3], p8 = k[4], p9 = k[5], p10 = k[6], p11 = k[7];
   uint32_t p12 = blk, p13 = 0, p14 = n1, p15 = n2;
   uint32_t q0 = kSigma0, q1 = kSigma1, q2 = kSigma2, q3 = kSigma3;
   uint32_t q4 = k[0], q5 = k[1], q6 = k[2], q7 = k[3], q8 = k[4], q9 = k[5], q10 = k[6], q11 = k[7];
-  uint32_t q12 = blk + 1u, q13 = 0, q14 = n1, q15 = n2;
+  uint32_t q12 = blk_b, q13 = 0, q14 = n1, q15 = n2;
   // the first column round stays compiler-scheduled: with a wave-uniform key
   // and counter its wave-uniform columns run on the scalar unit
   WG_QR(p0, p4, p8, p12) WG_QR(p1, p5, p9, p13) WG_QR(p2, p6, p10, p14) WG_QR(p3, p7, p11, p15)
@@ -315,7 +318,13 @@ __device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_
   kb[0] = q0 + kSigma0; kb[1] = q1 + kSigma1; kb[2] = q2 + kSigma2; kb[3] = q3 + kSigma3;
   kb[4] = q4 + k[0]; kb[5] = q5 + k[1]; kb[6] = q6 + k[2]; kb[7] = q7 + k[3];
   kb[8] = q8 + k[4]; kb[9] = q9 + k[5]; kb[10] = q10 + k[6]; kb[11] = q11 + k[7];
-  kb[12] = q12 + blk + 1u; kb[13] = q13; kb[14] = q14 + n1; kb[15] = q15 + n2;
+  kb[12] = q12 + blk_b; kb[13] = q13; kb[14] = q14 + n1; kb[15] = q15 + n2;
+}
+template <bool kShared = WG_SHARED_DIAG>
+__device__ __forceinline__ void chacha20_block2_sync(uint32_t (&ka)[16], uint32_t (&kb)[16],
+                                                     const uint32_t k[8], uint32_t blk,
+                                                     uint32_t n1, uint32_t n2) {
+  chacha20_block_pair_sync<kShared>(ka, kb, k, blk, blk + 1u, n1, n2);
 }
 
 // ---------------------------------------------------------------------------

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +31,7 @@ struct wg_gpu_ctx {
   uint32_t cus = 0;                // compute units (persistent strided grid)
   bool pad_slots = false;          // wg_gpu_ctx_set_slot_padding
   int64_t xlane_lanes = -1;        // wg_gpu_ctx_set_xlane_lanes (< 0: default)
+  int split_parts = -1;            // wg_gpu_ctx_set_split (< 0: default)
   struct Range {
     uint64_t host, bytes, dev;
   };
@@ -484,6 +486,39 @@ int wg_gpu_plan_batch(wg_gpu_ctx *ctx, int seal, const wg_packet_desc *descs, ui
   return WG_RC_OK;
 }
 
+// Split waves (StridedParams::split): a launch whose full waves fill only part of the
+// persistent grid's wave slots (cus x 16: 4 per SIMD) leaves SIMDs with 2-3 waves,
+// whose phase-locked rounds then issue far below the VALU rate: 172,544 x 8192 B ran
+// at 0.456 of HBM with 2,696 waves on 4,096 slots, the same packets as a full grid of
+// 4,096 waves at 0.544 (profiles/r06c_bench_p8192_*).  Cutting every wave into K parts
+// of its rounds (K divides the keystream rounds, >= 8 rounds a part) multiplies the
+// wave jobs by K; K is chosen by a fill model -- per pass of up to `slots` jobs, time
+// ~ occupancy / (K e(occupancy)), e(o) = o^0.45 fitted to those two runs -- plus 1.5 %
+// per extra part (its Poly1305 key block and the finish kernel's combine).
+// WG_SPLIT_K: 1 = never, 2/4/8 = forced where it divides, unset = the model.
+static uint32_t split_parts(const wg_gpu_ctx *ctx, uint32_t waves, uint32_t rk) {
+  static const long env = [] {
+    const char *e = std::getenv("WG_SPLIT_K");
+    return e ? std::atol(e) : -1L;
+  }();
+  auto ok = [&](uint32_t K) { return K == 1u || (rk % K == 0u && rk / K >= 8u); };
+  const long forced = ctx->split_parts >= 1 ? ctx->split_parts : env;
+  if (forced >= 1) return forced <= 8 && ok((uint32_t)forced) ? (uint32_t)forced : 1u;
+  const double slots = (double)ctx->cus * 16.0;
+  auto model = [&](uint32_t K) {
+    double t = 0.0;
+    for (double u = (double)waves * K; u > 0.0; u -= slots) {
+      const double occ = std::min(u, slots) / slots;
+      t += occ / (K * std::pow(occ, 0.45));
+    }
+    return t * (1.0 + 0.015 * (K - 1u));
+  };
+  uint32_t best = 1u;
+  for (uint32_t K : {2u, 4u, 8u})
+    if (ok(K) && model(K) < model(best)) best = K;
+  return best;
+}
+
 static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, uint32_t key_slot,
                           uint64_t counter_base, const uint8_t *src, uint64_t src_stride,
                           uint8_t *dst, uint64_t dst_stride, int32_t *status, void *stream) {
@@ -551,13 +586,39 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     }
   }
   const uint32_t full_waves = n / 64u;
+  // (open with datagrams shorter than 32 bytes fails every packet at parse: never split)
+  const uint32_t split = WG_SPLIT && full_waves && (seal || len >= WG_DATA_OVERHEAD_SZ)
+                             ? split_parts(ctx, full_waves, ((seal ? len : len - WG_DATA_OVERHEAD_SZ) + 127u) / 128u)
+                             : 1u;
+  void *scratch = nullptr;
+  wg::StridedSplitParams sp;
+  if (split > 1u) {
+    // the parts' accumulators, stream-ordered (concurrent launches on other streams
+    // get their own): [part][packet] 16 + 4 bytes
+    const size_t m = (size_t)full_waves * 64u * split;
+    WG_HIP(hipMallocAsync(&scratch, m * 20u, s), "strided: split scratch");
+    sp.sa.split = split;
+    sp.sa.split_q = ((seal ? len : len - WG_DATA_OVERHEAD_SZ) + 127u) / 128u / split;
+    sp.sa.part_h = static_cast<uint4 *>(scratch);
+    sp.sa.part_h4 = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + m * 16u);
+  }
   if (full_waves) {
     // persistent: kStridedBlocksPerCU resident workgroups per CU walk the
-    // workgroup-sized packet groups (wg_aead.hip aead_strided_kernel)
-    const dim3 grid = persistent_grid(ctx, full_waves, prm.spread);
+    // workgroup-sized packet groups (wg_aead.hip aead_strided_kernel); split: the
+    // waves' parts
+    const dim3 grid = persistent_grid(ctx, full_waves * split, prm.spread);
     // (strided kernels: the spread's live-wave rotation, wg_aead.hip strided_body)
     if (prm.spread) prm.spread |= spread_rot() << 8;
-    if (seal)
+    sp.prm = prm;
+    if (split > 1u) {
+      if (seal)
+        hipLaunchKernelGGL((wg::aead_strided_split_kernel<true, false>), grid, dim3(wg::kStridedThreads), 0, s, sp);
+      else if (text_grid)
+        hipLaunchKernelGGL((wg::aead_strided_split_kernel<false, true>), grid, dim3(wg::kStridedThreads), 0, s, sp);
+      else
+        hipLaunchKernelGGL((wg::aead_strided_split_kernel<false, false>), grid, dim3(wg::kStridedThreads), 0, s,
+                           sp);
+    } else if (seal)
       hipLaunchKernelGGL((wg::aead_strided_kernel<true, false>), grid, dim3(wg::kStridedThreads),
                          0, s, prm);
     else if (text_grid)
@@ -566,6 +627,16 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     else
       hipLaunchKernelGGL((wg::aead_strided_kernel<false, false>), grid, dim3(wg::kStridedThreads),
                          0, s, prm);
+    if (split > 1u) {
+      const dim3 fg((full_waves * 64u + 255u) / 256u);
+      if (seal)
+        hipLaunchKernelGGL((wg::aead_strided_finish_kernel<true, false>), fg, dim3(256), 0, s, sp);
+      else if (text_grid)
+        hipLaunchKernelGGL((wg::aead_strided_finish_kernel<false, true>), fg, dim3(256), 0, s, sp);
+      else
+        hipLaunchKernelGGL((wg::aead_strided_finish_kernel<false, false>), fg, dim3(256), 0, s, sp);
+      WG_HIP(hipFreeAsync(scratch, s), "strided: split scratch");
+    }
   }
   if (n % 64u) {  // the last, partial wave: generic per-lane geometry
     if (seal)
@@ -602,6 +673,12 @@ int wg_gpu_ctx_set_slot_padding(wg_gpu_ctx *ctx, int writable) {
 int wg_gpu_ctx_set_xlane_lanes(wg_gpu_ctx *ctx, int64_t lanes) {
   if (!ctx) return fail(WG_RC_INVALID_ARGUMENT, "set_xlane_lanes: null context");
   ctx->xlane_lanes = lanes < 0 ? -1 : lanes;
+  return WG_RC_OK;
+}
+
+int wg_gpu_ctx_set_split(wg_gpu_ctx *ctx, int parts) {
+  if (!ctx) return fail(WG_RC_INVALID_ARGUMENT, "set_split: null context");
+  ctx->split_parts = parts < 0 ? -1 : parts;
   return WG_RC_OK;
 }
 

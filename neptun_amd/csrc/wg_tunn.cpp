@@ -1246,7 +1246,10 @@ hipError_t wait_chunk(Staging &S, uint32_t m) {
 // addresses) and makes ONE launch with one completion word for all of them; each
 // call then waits for that word, copies its statuses and goes on with its own
 // in-order decisions.  Per packet the kernel does exactly what the call's own launch
-// would have done.  (WG_COMBINE=0: every call launches alone.)
+// would have done.  Off by default (WG_COMBINE=1 turns it on): measured at 8 threads
+// x 50 packets it LOST -- 43 vs 53 Gbit/s staged, 38 vs 54 registered
+// (profiles/r06d_tt_*): the calls' time is the kernel's PCIe round trips, which a
+// shared launch does not shorten, and the slot wait (12 us) came on top.
 constexpr uint32_t kCombSlots = 4, kCombMax = 2048, kCombSegMax = 256;
 struct Combiner {
   std::mutex mu;
@@ -1261,7 +1264,7 @@ struct Combiner {
 
 bool combine_on() {  // (read per call)
   const char *e = std::getenv("WG_COMBINE");
-  return !e || std::atoi(e) != 0;
+  return e && std::atoi(e) != 0;
 }
 uint32_t combine_depth() {  // combined launches in flight per engine and direction (1 .. kCombSlots)
   const char *e = std::getenv("WG_COMBINE_DEPTH");

@@ -273,6 +273,11 @@ class GpuContext:
         < 0 = default."""
         check(self._lib.wg_gpu_ctx_set_xlane_lanes(self._h, int(lanes)), "wg_gpu_ctx_set_xlane_lanes")
 
+    def set_split(self, parts: int) -> None:
+        """Split waves of the strided batches (wg_gpu_ctx_set_split): < 0 the library's
+        choice, 1 never, 2 / 4 / 8 forced where they divide the keystream rounds."""
+        check(self._lib.wg_gpu_ctx_set_split(self._h, int(parts)), "wg_gpu_ctx_set_split", self._lib)
+
     def seal_strided(self, n: int, length: int, key_slot: int, counter_base: int, src,
                      src_stride: int, dst, dst_stride: int, status=None, stream=None) -> None:
         check(self._lib.wg_gpu_seal_strided(self._h, n, length, key_slot, counter_base, _ptr(src),

@@ -330,6 +330,7 @@ def test_concurrent_small_calls_combine_into_shared_launches(big_ctx, monkeypatc
 
     from test_tunn_gpu import Arena
     monkeypatch.setenv("WG_TUNN_FLAG", "64")
+    monkeypatch.setenv("WG_COMBINE", "1")  # (off by default: DESIGN 8)
     monkeypatch.setenv("WG_COMBINE_DEPTH", depth)
     rng = random.Random(808 + int(depth))
     eng = Engine(big_ctx)
