@@ -703,7 +703,9 @@ __device__ __forceinline__ void stage_in(uint4 *run, const UniformGeomT<kText> &
   }
 }
 
-template <bool kSeal, bool kText>
+// kSkip0 (a split part's first round, wire grid): chunk 0 of every packet is the
+// previous part's (its last piece, finished there) and is not stored
+template <bool kSeal, bool kText, bool kSkip0 = false>
 __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> &g, uint32_t lane,
                                           uint32_t r) {
   using R = Ranges<kSeal, kText>;
@@ -723,7 +725,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
   // output (zero_outside) -- and rounds past the output's line end store nothing
   const bool full = WG_FULL_LINES && g.pad && dead == 0;
   if (full && kRun * r >= hi) return;
-  if (WG_ABLATE_ALL_INTERIOR || full || (kRun * r >= R::out_lo() && kRun * r + kRun <= hi && dead == 0)) {
+  if (!kSkip0 && (WG_ABLATE_ALL_INTERIOR || full || (kRun * r >= R::out_lo() && kRun * r + kRun <= hi && dead == 0))) {
     // interior round: 8 full-chunk stores at round-independent per-lane offsets
     // (all 8 LDS reads first: the asm stores are memory barriers to the
     // compiler, which otherwise serialises read -> wait -> store per piece)
@@ -745,7 +747,7 @@ __device__ __forceinline__ void stage_out(uint4 *run, const UniformGeomT<kText> 
   for (uint32_t j = 0; j < kChunks; ++j) {
     const uint32_t k = (j & 1u) ? k1 : k0;
     const uint32_t w = kRun * r + 16u * k;
-    const bool gone = !kSeal && ((((uint32_t)(dead >> (8u * j))) >> y) & 1u);
+    const bool gone = (!kSeal && ((((uint32_t)(dead >> (8u * j))) >> y) & 1u)) || (kSkip0 && k == 0u);
     const bool ok = !gone && w >= R::out_lo() && w < hi;
     if (g.pad) {  // (wave-uniform) the partial chunk and the rest of its line, zero-filled
       const int valid = ok ? (int)min(hi - w, 16u) : 0;
@@ -1161,14 +1163,7 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     // round 0's DMA (wave-uniform call site).  Open computes it per lane as
     // soon as the lane's header has landed: locking it there made every wave
     // wait for the slowest header (-4 %).
-    if (!kText && split && r_begin > 0u) {  // (split: compile-time)
-      // a later part: block 0 and block 2 r_begin, whose last 16 bytes are chunk 0 of
-      // the part's first round (the wire grid's carry, apply_chunk0) -- one call with
-      // the barriers of a single block, so every part's calls still match
-      uint32_t kc[16];
-      chacha20_block_pair_sync(ks, kc, key, 0u, 2u * r_begin, n1, n2);
-      ks_save[0] = kc[12]; ks_save[1] = kc[13]; ks_save[2] = kc[14]; ks_save[3] = kc[15];
-    } else if constexpr ((kSync && kSeal && WG_SYNC_KEY_BLOCK) || kSyncOpenKey) {
+    if constexpr ((kSync && kSeal && WG_SYNC_KEY_BLOCK) || kSyncOpenKey) {
       chacha20_block_sync(ks, key, 0u, n1, n2);
     } else {
       chacha20_block(ks, key, 0u, n1, n2);
@@ -1414,6 +1409,9 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       // descriptor batches: a round every live packet fills with ciphertext
       // (wave-uniform) runs without per-chunk length tests, tail masks or tag work
       const bool full = !kUniform && WG_DESC_FULL_ROUNDS && kRun * r + 112u <= p_min;
+      // a later split part's first round (wire grid): its chunk 0 -- the tail of block
+      // 2 r -- is the previous part's last piece, done there (no carry block here)
+      const bool skip0 = split && !kText && r == r_begin && r_begin > 0u;
       auto landed = [&]() {
 #if WG_MEM_PRIO && !WG_MEM_PRIO_AT
         __builtin_amdgcn_s_setprio(WG_MEM_PRIO);
@@ -1441,14 +1439,14 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
             apply_blocks<kSeal, kText, true>(run, ln, r, Pr, ka, kb, poly, ks_save);
           }
         } else if (my_runs) {
-          apply_chunk0<kSeal, kText>(run, ln, r, Pr, poly, ks_save);
+          if (!skip0) apply_chunk0<kSeal, kText>(run, ln, r, Pr, poly, ks_save);
           apply_blocks<kSeal, kText>(run, ln, r, Pr, ka, kb, poly, ks_save);
           if (kSeal) seal_tail(run, r);
         }
       } else {
         landed();
         if (my_runs && !WG_ABLATE_NO_CRYPT) {
-          apply_chunk0<kSeal, kText>(run, ln, r, Pr, poly, ks_save);
+          if (!skip0) apply_chunk0<kSeal, kText>(run, ln, r, Pr, poly, ks_save);
           if (kSeal) seal_tail(run, r);
         }
       }
@@ -1472,7 +1470,12 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
       __builtin_amdgcn_s_setprio(WG_MEM_PRIO);
 #endif
 #if !WG_ABLATE_NO_MEM
-      stage_out<kSeal>(run, g, ln, r);
+      if constexpr (split && !kText) {
+        if (skip0) stage_out<kSeal, kText, true>(run, g, ln, r);
+        else stage_out<kSeal>(run, g, ln, r);
+      } else {
+        stage_out<kSeal>(run, g, ln, r);
+      }
 #endif
       WG_STAMP_AT(kSeal, r, 5);
     };
@@ -1512,6 +1515,19 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   }
 
   if constexpr (split) {
+    if constexpr (!kText) {
+      // (wire grid, all parts but the last) chunk 0 of the next part's first round: the
+      // tail of block 2 r_end, whose keystream this part holds (ks_save) -- a whole
+      // 16-byte piece (the packets' ciphertext goes on past the next part's start)
+      if (sp->r1 != 0xffffffffu && my_runs) {
+        const uint32_t w = kRun * rounds;
+        const u32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4 *>(job.in_base + w);
+        const uint32_t o0 = v.x ^ ks_save[0], o1 = v.y ^ ks_save[1], o2 = v.z ^ ks_save[2], o3 = v.w ^ ks_save[3];
+        if (kSeal) poly_block(poly, o0, o1, o2, o3);
+        else poly_block(poly, v.x, v.y, v.z, v.w);
+        gstore16<false>(reinterpret_cast<uint8_t *>(job.out_base + w), make_uint4(o0, o1, o2, o3));
+      }
+    }
     // this part's share of the MAC (the finish kernel combines the parts; the open's
     // header statuses, tag check and zeroing are its too)
     sp->h[sp->idx] = make_uint4(poly.h0, poly.h1, poly.h2, poly.h3);
@@ -1793,14 +1809,12 @@ __global__ __launch_bounds__(256) void aead_strided_finish_kernel(StridedSplitPa
     Poly ps;
     poly_init(ps, ks);
     const F26 r26 = f26_from32(ps.r0, ps.r1, ps.r2, ps.r3, 0u);
-    // pieces (16-byte ciphertext chunks, the last one partial) of rounds [a, b): text
-    // offsets m = 128 r - 16 + 16 k (wire grid: chunk 0 of round 0 is the header) or
-    // m = 128 r + 16 k (text grid), those with m < P
+    // pieces (16-byte ciphertext chunks, the last one partial) of the part over rounds
+    // [a, b): text [128 a, 128 b) on both grids (on the wire grid a part also finishes
+    // chunk 0 of the next part's first round and skips its own first), those below P
     const uint32_t P16 = (P + 15u) & ~15u;
     auto pieces = [&](uint32_t a, uint32_t b) -> uint32_t {
-      const uint32_t lo = kText ? min(128u * a, P16) : min(a ? 128u * a - 16u : 0u, P16);
-      const uint32_t hi = kText ? min(128u * b, P16) : min(b ? 128u * b - 16u : 0u, P16);
-      return (hi - lo) / 16u;
+      return (min(128u * b, P16) - min(128u * a, P16)) / 16u;
     };
     const size_t stride = (size_t)n;
     F26 acc;
