@@ -1051,6 +1051,7 @@ struct SplitPart {
   uint32_t r0, r1, idx;
   uint4 *h;
   uint32_t *h4;
+  uint4 *rs;  // part 0 only (else null): the packet's r and s for the finish kernel
 };
 #if WG_SPLIT && WG_POLY_RADIX26
 #error "split waves hand over radix-2^32 accumulators: build WG_POLY_RADIX26 with -DWG_SPLIT=0"
@@ -1532,6 +1533,10 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
     // header statuses, tag check and zeroing are its too)
     sp->h[sp->idx] = make_uint4(poly.h0, poly.h1, poly.h2, poly.h3);
     sp->h4[sp->idx] = poly.h4;
+    if (sp->rs) {  // (part 0: the Poly1305 key, so the finish kernel computes no block)
+      sp->rs[2u * sp->idx] = make_uint4(poly.r0, poly.r1, poly.r2, poly.r3);
+      sp->rs[2u * sp->idx + 1u] = S.park[lane];
+    }
     return false;
   }
   if (!kSeal && job.status == WG_STATUS_OK) {
@@ -1728,6 +1733,7 @@ __device__ __forceinline__ void strided_body(const StridedParams &prm, const Spl
         spt.idx = pkt0 + lane;
         spt.h = sa->part_h + (size_t)part * (w64 * 64u);
         spt.h4 = sa->part_h4 + (size_t)part * (w64 * 64u);
+        spt.rs = part == 0u ? sa->rs : nullptr;
         strided_group<kSeal, false, kText, Stage, true>(stage[wave], prm, pkt0, lane, &sk, 0, false, &spt);
       }
       return;
@@ -1782,32 +1788,19 @@ __global__ __launch_bounds__(256) void aead_strided_finish_kernel(StridedSplitPa
   const uint32_t P = kSeal ? prm.len : prm.len - WG_DATA_OVERHEAD_SZ;  // (open: len >= 32, the host checks)
   const uint8_t *src = prm.src + (uint64_t)i * prm.src_stride;
   uint8_t *dst = prm.dst + (uint64_t)i * prm.dst_stride;
-  uint32_t key[8];
-  {
-    const uint8_t *kp = prm.keys + 32u * prm.key_slot;
-    const uint4 a = ld16(kp), b = ld16(kp + 16u);
-    key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
-    key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
-  }
-  const uint32_t sidx = prm.key_index[prm.key_slot];
   int32_t status = WG_STATUS_OK;
-  uint32_t n1, n2;
-  if (kSeal) {
-    const uint64_t c = prm.counter_base + i;
-    n1 = (uint32_t)c;
-    n2 = (uint32_t)(c >> 32);
-  } else {
+  if (!kSeal) {
+    const uint32_t sidx = prm.key_index[prm.key_slot];
     const uint4 h = ld16(src);
     if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
     else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;
-    n1 = h.z;
-    n2 = h.w;
   }
   if (status == WG_STATUS_OK) {
-    uint32_t ks[16];
-    chacha20_block(ks, key, 0u, n1, n2);
+    // the Poly1305 key part 0 computed (r clamped, s)
+    const uint4 rq = sa.rs[2u * i], sq = sa.rs[2u * i + 1u];
+    const uint32_t rk[8] = {rq.x, rq.y, rq.z, rq.w, 0u, 0u, 0u, 0u};
     Poly ps;
-    poly_init(ps, ks);
+    poly_init(ps, rk);
     const F26 r26 = f26_from32(ps.r0, ps.r1, ps.r2, ps.r3, 0u);
     // pieces (16-byte ciphertext chunks, the last one partial) of the part over rounds
     // [a, b): text [128 a, 128 b) on both grids (on the wire grid a part also finishes
@@ -1817,21 +1810,25 @@ __global__ __launch_bounds__(256) void aead_strided_finish_kernel(StridedSplitPa
       return (min(128u * b, P16) - min(128u * a, P16)) / 16u;
     };
     const size_t stride = (size_t)n;
+    // parts 1 .. K-2 have the same piece count (8 Q): their power of r once
+    const uint32_t k_mid = pieces(sa.split_q, 2u * sa.split_q);
+    const F26 r_mid = sa.split > 2u ? f26_pow(r26, k_mid) : r26;
     F26 acc;
     for (uint32_t j = 0; j < sa.split; ++j) {
       const uint4 hq = sa.part_h[j * stride + i];
       const F26 hj = f26_from32(hq.x, hq.y, hq.z, hq.w, sa.part_h4[j * stride + i]);
       if (j == 0) {
         acc = hj;
+      } else if (j + 1u < sa.split) {
+        acc = f26_add(f26_mul(acc, r_mid), hj);
       } else {
-        const uint32_t a = j * sa.split_q, b = j + 1u == sa.split ? 0x7fffffffu / 128u : a + sa.split_q;
-        const uint32_t k = pieces(a, b);
+        const uint32_t k = pieces(j * sa.split_q, 0x7fffffffu / 128u);
         acc = f26_add(k ? f26_mul(acc, f26_pow(r26, k)) : acc, hj);
       }
     }
     f26_to32(acc, ps.h0, ps.h1, ps.h2, ps.h3, ps.h4);
     poly_block(ps, 0u, 0u, P, 0u);  // le64(AAD len = 0) | le64(P)
-    const uint32_t s4[4] = {ks[4], ks[5], ks[6], ks[7]};
+    const uint32_t s4[4] = {sq.x, sq.y, sq.z, sq.w};
     uint32_t tag[4];
     poly_finish(ps, s4, tag);
     if (kSeal) {

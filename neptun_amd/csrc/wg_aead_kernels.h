@@ -73,6 +73,7 @@ struct SplitArgs {
   uint32_t split, split_q;
   uint4 *part_h;
   uint32_t *part_h4;
+  uint4 *rs;  // [packet][2]: part 0's clamped r and s (the finish kernel's Poly1305 key)
 };
 struct StridedSplitParams {
   StridedParams prm;

@@ -594,13 +594,14 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
   wg::StridedSplitParams sp;
   if (split > 1u) {
     // the parts' accumulators, stream-ordered (concurrent launches on other streams
-    // get their own): [part][packet] 16 + 4 bytes
-    const size_t m = (size_t)full_waves * 64u * split;
-    WG_HIP(hipMallocAsync(&scratch, m * 20u, s), "strided: split scratch");
+    // get their own): [part][packet] 16 + 4 bytes, then [packet] r and s (32 bytes)
+    const size_t np = (size_t)full_waves * 64u, m = np * split;
+    WG_HIP(hipMallocAsync(&scratch, m * 20u + np * 32u, s), "strided: split scratch");
     sp.sa.split = split;
     sp.sa.split_q = ((seal ? len : len - WG_DATA_OVERHEAD_SZ) + 127u) / 128u / split;
     sp.sa.part_h = static_cast<uint4 *>(scratch);
-    sp.sa.part_h4 = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + m * 16u);
+    sp.sa.rs = reinterpret_cast<uint4 *>(static_cast<uint8_t *>(scratch) + m * 16u);
+    sp.sa.part_h4 = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + m * 16u + np * 32u);
   }
   if (full_waves) {
     // persistent: kStridedBlocksPerCU resident workgroups per CU walk the

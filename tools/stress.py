@@ -11,7 +11,9 @@ unordered twin, and every third a batch with a random key slot per packet (a
 4096-slot table: the affine descriptor kernel against the plan-ordered one).  The
 unordered descriptor launch draws its form at random (round 5): the throughput kernels,
 the default selection, or the latency form with a forced group of 2 .. 64 lanes per
-packet (wg_xlane.hip) -- and so does the descriptor open.  A one-in-a-million
+packet (wg_xlane.hip) -- and so does the descriptor open.  Round 6: long packets (up to
+8192 B) too, and the strided seal draws its split (wg_gpu_ctx_set_split: the default
+choice, unsplit, or K = 2 / 4 / 8 parts per wave with the finish kernel).  A one-in-a-million
 corruption in any form shows up as a mismatch between forms that share no kernel.
 Prints one JSON summary line.
 
@@ -62,7 +64,10 @@ def main():
             sizes = rng.choice([0, 64, 256, 576, 1350, 1500, 8900], n)
             S = 9088
         else:
-            P = int(rng.choice([64, 576, 1350, 1420, int(rng.integers(0, 2000))]))
+            P = int(rng.choice([64, 576, 1350, 1420, int(rng.integers(0, 2000)), 4096, 8192,
+                                int(rng.integers(2000, 9000))]))
+            if P > 2000:
+                n = min(n, 262144 + int(rng.integers(0, 64)))
             sizes = np.full(n, P, np.int64)
             S = synth.round_up(P + 32 + int(rng.choice([0, 16, 96])), 16)
         sizes_t = torch.from_numpy(sizes.astype(np.int64)).to(dev)
@@ -94,7 +99,11 @@ def main():
             w = torch.full((n * S + 64,), 0xA5, dtype=torch.uint8, device=dev)
             st = torch.full((n,), -1, dtype=torch.int32, device=dev)
             if form == "strided":
+                K = int(rng.choice([-1, 1, 2, 4, 8]))
+                ctx.set_split(K)
+                form = f"strided-split{K}"
                 ctx.seal_strided(n, int(sizes[0]), 0, ctr0, pt, S, w, S, st)
+                ctx.set_split(-1)
             elif form == "desc-ordered":
                 order = torch.zeros(n, dtype=torch.int32, device=dev)
                 scratch = torch.zeros(262144 // 4, dtype=torch.int32, device=dev)
@@ -126,7 +135,12 @@ def main():
             ctx.open_batch(torch.from_numpy(d2.view(np.uint8)).to(dev), n, outs[0], back, st2)
             ctx.set_xlane_lanes(0)
         else:
+            K = int(rng.choice([-1, 1, 2, 4, 8]))
+            ctx.set_split(K)
+            tag = f"open-strided-split{K}"
+            stats["forms"][tag] = stats["forms"].get(tag, 0) + 1
             ctx.open_strided(n, int(sizes[0]) + 32, 0, outs[0], S, back, S, st2)
+            ctx.set_split(-1)
         torch.cuda.synchronize()
         if int((st2 != 0).sum()):
             bad.append({"what": "open status", "failed": int((st2 != 0).sum())})
