@@ -131,6 +131,14 @@ class StridedWorkload:
         self.kernels = {"seal": "aead_strided_kernel<true, false>",
                         "open": "aead_strided_open_text_kernel" if self.layout == "neptun"
                         else "aead_strided_kernel<false, false>"}
+        # under-filled grids of long packets run split waves (wg_gpu_ctx_set_split):
+        # the split kernel + the finish kernel, both inside the timed launch
+        ks = {"seal": self.ctx.split_parts(True, n, P), "open": self.ctx.split_parts(False, n, P + 32)}
+        text = self.layout == "neptun"
+        for op, k in ks.items():
+            if k > 1:
+                tpl = "<true, false>" if op == "seal" else "<false, true>" if text else "<false, false>"
+                self.kernels[op] = f"aead_strided_split_kernel{tpl} (K = {k}) + aead_strided_finish_kernel{tpl}"
         # the committed PMC summaries were profiled per size on the default slot shape
         default_shape = n == packets_for(args) and S == synth.round_up(P + 32, 128) and (
             self.layout == "neptun" or self.pad)

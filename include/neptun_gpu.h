@@ -220,10 +220,18 @@ int wg_gpu_ctx_set_xlane_lanes(wg_gpu_ctx *ctx, int64_t lanes);
  * of the chip runs each wave as `parts` jobs over consecutive rounds of its packets,
  * and a finish kernel combines their Poly1305 sums (tags, checks, statuses).  parts
  * < 0: the library's choice (a fill model, WG_SPLIT_K from the environment overrides);
- * 1: never; 2, 4 or 8: that many where it divides the packets' keystream rounds into
- * parts of at least 8 (else unsplit).  Results are identical either way.
+ * 1: never; 2 .. 8: that many where every part keeps at least 8 of the packets'
+ * keystream rounds (else unsplit; part 0 takes the rounds the count does not divide).
+ * Results are identical either way.
  */
 int wg_gpu_ctx_set_split(wg_gpu_ctx *ctx, int parts);
+
+/*
+ * The parts (>= 1; 1 = unsplit) a strided batch of n packets of `len` input bytes
+ * would run its full waves in, on the throughput form (batches that take the latency
+ * form are never split).  For tools and benches: the kernels a launch makes.
+ */
+int wg_gpu_strided_split_parts(wg_gpu_ctx *ctx, int seal, uint32_t n, uint32_t len);
 
 /*
  * Handshake-side crypto, batched.  Device pointers,

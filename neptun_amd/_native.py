@@ -60,6 +60,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.argtypes = [vp, vp, vp, u32, vp, vp, vp, vp]
     L.wg_gpu_ctx_set_xlane_lanes.argtypes = [vp, c.c_int64]
     L.wg_gpu_ctx_set_split.argtypes = [vp, c.c_int]
+    L.wg_gpu_strided_split_parts.argtypes = [vp, c.c_int, u32, u32]
     L.wg_gpu_register_host.argtypes = [vp, vp, u64]
     L.wg_gpu_unregister_host.argtypes = [vp, vp]
     L.wg_gpu_host_device_address.argtypes = [vp, vp, u64, c.POINTER(u64)]

@@ -1099,8 +1099,8 @@ __device__ __forceinline__ bool run_wave(Stage &S, Geom &g, uint32_t lane, Packe
   uint32_t my_runs = job.status == WG_STATUS_OK ? (W - (16u - kG) + kRun - 1) / kRun : 0u;
   uint32_t rounds;
   uint32_t p_min = 0u;  // descriptor batches, phase-locked: the wave's shortest live payload
-  // a split part runs rounds [r_begin, r_end) (wave-uniform; the phase-locked calls
-  // still match: every part has the same number of keystream rounds, see wg_gpu.cpp)
+  // a split part runs rounds [r_begin, r_end) (wave-uniform; parts differ by at most
+  // the rem rounds of part 0, see strided_body)
   constexpr bool split = kUniform && kSync && kSplit;
   uint32_t r_begin = 0u;
   if constexpr (kUniform) {
@@ -1716,8 +1716,12 @@ __device__ __forceinline__ void strided_body(const StridedParams &prm, const Spl
 #if WG_SPLIT && WG_SYNC
     if constexpr (kSplit) {  // (a kernel of its own: the unsplit kernels keep their registers)
       // split waves: unit u = part * W64 + wave-of-packets (part-major: the waves of a
-      // workgroup run the same round range), a part's rounds [part q, part q + q), the
-      // last part to the packets' end
+      // workgroup mostly run the same part), a part's rounds [part q + rem, part q + q +
+      // rem) (part 0 from 0: it carries the rem < K rounds K does not divide), the last
+      // part to the packets' end.  Parts of unequal length may share a workgroup: the
+      // strided rounds meet only at the phase-locked s_barriers, which pace the waves and
+      // guard no LDS (each wave stages its own), so a wave one round ahead stays locked
+      // one step off, and a wave that ends leaves the barrier
       const uint32_t w64 = prm.n / 64u, units = w64 * sa->split;
       uint32_t u_first = blockIdx.x * kWaves + wave, u_end = units, u_step = gridDim.x * kWaves;
       if (prm.spread) {  // (one pass: this workgroup's even share of the units)
@@ -1728,8 +1732,8 @@ __device__ __forceinline__ void strided_body(const StridedParams &prm, const Spl
       for (uint32_t u = u_first; u < u_end; u += u_step) {
         const uint32_t part = u / w64, pkt0 = (u - part * w64) * 64u;
         SplitPart spt;
-        spt.r0 = part * sa->split_q;
-        spt.r1 = part + 1u == sa->split ? 0xffffffffu : spt.r0 + sa->split_q;
+        spt.r0 = part == 0u ? 0u : part * sa->split_q + sa->split_rem;
+        spt.r1 = part + 1u == sa->split ? 0xffffffffu : (part + 1u) * sa->split_q + sa->split_rem;
         spt.idx = pkt0 + lane;
         spt.h = sa->part_h + (size_t)part * (w64 * 64u);
         spt.h4 = sa->part_h4 + (size_t)part * (w64 * 64u);
@@ -1811,7 +1815,8 @@ __global__ __launch_bounds__(256) void aead_strided_finish_kernel(StridedSplitPa
     };
     const size_t stride = (size_t)n;
     // parts 1 .. K-2 have the same piece count (8 Q): their power of r once
-    const uint32_t k_mid = pieces(sa.split_q, 2u * sa.split_q);
+    const uint32_t pq = sa.split_q, prem = sa.split_rem;
+    const uint32_t k_mid = pieces(pq + prem, 2u * pq + prem);
     const F26 r_mid = sa.split > 2u ? f26_pow(r26, k_mid) : r26;
     F26 acc;
     for (uint32_t j = 0; j < sa.split; ++j) {
@@ -1822,7 +1827,7 @@ __global__ __launch_bounds__(256) void aead_strided_finish_kernel(StridedSplitPa
       } else if (j + 1u < sa.split) {
         acc = f26_add(f26_mul(acc, r_mid), hj);
       } else {
-        const uint32_t k = pieces(j * sa.split_q, 0x7fffffffu / 128u);
+        const uint32_t k = pieces(j * pq + prem, 0x7fffffffu / 128u);
         acc = f26_add(k ? f26_mul(acc, f26_pow(r26, k)) : acc, hj);
       }
     }

@@ -64,13 +64,14 @@ struct StridedParams {
 };
 
 // Split (under-filled launches of long packets, wg_gpu.cpp): every wave of 64 packets
-// is cut into `split` parts of split_q keystream rounds each, every part a wave job of
-// its own, so that the grid fills the chip; the parts' Poly1305 accumulators go to
+// is cut into `split` parts, every part a wave job of its own, so that the grid fills
+// the chip: part 0 takes rounds [0, split_q + split_rem), part j > 0 rounds
+// [j split_q + split_rem, (j + 1) split_q + split_rem), the last part to the end; the parts' Poly1305 accumulators go to
 // part_h / part_h4 ([part][packet]) and aead_strided_finish_kernel combines them,
 // writes the tags (seal) or checks them (open) and the statuses.  (Kernels of their
 // own with their own argument block: the unsplit kernels are compiled as before.)
 struct SplitArgs {
-  uint32_t split, split_q;
+  uint32_t split, split_q, split_rem;
   uint4 *part_h;
   uint32_t *part_h4;
   uint4 *rs;  // [packet][2]: part 0's clamped r and s (the finish kernel's Poly1305 key)

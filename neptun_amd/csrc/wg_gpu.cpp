@@ -491,17 +491,19 @@ int wg_gpu_plan_batch(wg_gpu_ctx *ctx, int seal, const wg_packet_desc *descs, ui
 // whose phase-locked rounds then issue far below the VALU rate: 172,544 x 8192 B ran
 // at 0.456 of HBM with 2,696 waves on 4,096 slots, the same packets as a full grid of
 // 4,096 waves at 0.544 (profiles/r06c_bench_p8192_*).  Cutting every wave into K parts
-// of its rounds (K divides the keystream rounds, >= 8 rounds a part) multiplies the
-// wave jobs by K; K is chosen by a fill model -- per pass of up to `slots` jobs, time
-// ~ occupancy / (K e(occupancy)), e(o) = o^0.45 fitted to those two runs -- plus 1.5 %
-// per extra part (its Poly1305 key block and the finish kernel's combine).
-// WG_SPLIT_K: 1 = never, 2/4/8 = forced where it divides, unset = the model.
+// of its rounds (K = 2 .. 8, >= 8 rounds a part; part 0 takes the rounds K does not
+// divide) multiplies the wave jobs by K; K is chosen by a fill model -- per pass of up
+// to `slots` jobs, time ~ occupancy / (K e(occupancy)), e(o) = o^0.45 fitted to those
+// two runs -- plus 1.5 % per extra part (its Poly1305 key block and the finish kernel's
+// combine).  172,544 x 8192 B (2,696 waves): K = 3, 8,088 jobs in 1.97 passes (K = 4,
+// the best divisor of the 64 rounds, leaves a third pass at 0.63).
+// WG_SPLIT_K: 1 = never, 2 .. 8 = forced where a part keeps 8 rounds, unset = the model.
 static uint32_t split_parts(const wg_gpu_ctx *ctx, uint32_t waves, uint32_t rk) {
   static const long env = [] {
     const char *e = std::getenv("WG_SPLIT_K");
     return e ? std::atol(e) : -1L;
   }();
-  auto ok = [&](uint32_t K) { return K == 1u || (rk % K == 0u && rk / K >= 8u); };
+  auto ok = [&](uint32_t K) { return K == 1u || rk / K >= 8u; };
   const long forced = ctx->split_parts >= 1 ? ctx->split_parts : env;
   if (forced >= 1) return forced <= 8 && ok((uint32_t)forced) ? (uint32_t)forced : 1u;
   const double slots = (double)ctx->cus * 16.0;
@@ -514,9 +516,18 @@ static uint32_t split_parts(const wg_gpu_ctx *ctx, uint32_t waves, uint32_t rk) 
     return t * (1.0 + 0.015 * (K - 1u));
   };
   uint32_t best = 1u;
-  for (uint32_t K : {2u, 4u, 8u})
+  for (uint32_t K = 2u; K <= 8u; ++K)
     if (ok(K) && model(K) < model(best)) best = K;
   return best;
+}
+
+// the parts of a throughput-form strided batch's full waves (1: unsplit); (open with
+// datagrams shorter than 32 bytes fails every packet at parse: never split)
+static uint32_t strided_split(const wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len) {
+  const uint32_t full_waves = n / 64u;
+  return WG_SPLIT && full_waves && (seal || len >= WG_DATA_OVERHEAD_SZ)
+             ? split_parts(ctx, full_waves, ((seal ? len : len - WG_DATA_OVERHEAD_SZ) + 127u) / 128u)
+             : 1u;
 }
 
 static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, uint32_t key_slot,
@@ -586,10 +597,7 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     }
   }
   const uint32_t full_waves = n / 64u;
-  // (open with datagrams shorter than 32 bytes fails every packet at parse: never split)
-  const uint32_t split = WG_SPLIT && full_waves && (seal || len >= WG_DATA_OVERHEAD_SZ)
-                             ? split_parts(ctx, full_waves, ((seal ? len : len - WG_DATA_OVERHEAD_SZ) + 127u) / 128u)
-                             : 1u;
+  const uint32_t split = strided_split(ctx, seal, n, len);
   void *scratch = nullptr;
   wg::StridedSplitParams sp;
   if (split > 1u) {
@@ -598,7 +606,9 @@ static int launch_strided(wg_gpu_ctx *ctx, bool seal, uint32_t n, uint32_t len, 
     const size_t np = (size_t)full_waves * 64u, m = np * split;
     WG_HIP(hipMallocAsync(&scratch, m * 20u + np * 32u, s), "strided: split scratch");
     sp.sa.split = split;
-    sp.sa.split_q = ((seal ? len : len - WG_DATA_OVERHEAD_SZ) + 127u) / 128u / split;
+    const uint32_t rk = ((seal ? len : len - WG_DATA_OVERHEAD_SZ) + 127u) / 128u;
+    sp.sa.split_q = rk / split;
+    sp.sa.split_rem = rk - split * sp.sa.split_q;
     sp.sa.part_h = static_cast<uint4 *>(scratch);
     sp.sa.rs = reinterpret_cast<uint4 *>(static_cast<uint8_t *>(scratch) + m * 16u);
     sp.sa.part_h4 = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + m * 16u + np * 32u);
@@ -681,6 +691,11 @@ int wg_gpu_ctx_set_split(wg_gpu_ctx *ctx, int parts) {
   if (!ctx) return fail(WG_RC_INVALID_ARGUMENT, "set_split: null context");
   ctx->split_parts = parts < 0 ? -1 : parts;
   return WG_RC_OK;
+}
+
+int wg_gpu_strided_split_parts(wg_gpu_ctx *ctx, int seal, uint32_t n, uint32_t len) {
+  if (!ctx) return fail(WG_RC_INVALID_ARGUMENT, "strided_split_parts: null context");
+  return (int)strided_split(ctx, seal != 0, n, len);
 }
 
 int wg_gpu_register_host(wg_gpu_ctx *ctx, void *base, uint64_t bytes) {

@@ -275,8 +275,16 @@ class GpuContext:
 
     def set_split(self, parts: int) -> None:
         """Split waves of the strided batches (wg_gpu_ctx_set_split): < 0 the library's
-        choice, 1 never, 2 / 4 / 8 forced where they divide the keystream rounds."""
+        choice, 1 never, 2 .. 8 forced where every part keeps >= 8 keystream rounds."""
         check(self._lib.wg_gpu_ctx_set_split(self._h, int(parts)), "wg_gpu_ctx_set_split", self._lib)
+
+    def split_parts(self, seal: bool, n: int, length: int) -> int:
+        """Parts a throughput-form strided batch's waves would run in (1: unsplit),
+        wg_gpu_strided_split_parts."""
+        k = self._lib.wg_gpu_strided_split_parts(self._h, int(bool(seal)), int(n), int(length))
+        if k < 1:
+            check(k, "wg_gpu_strided_split_parts", self._lib)
+        return int(k)
 
     def seal_strided(self, n: int, length: int, key_slot: int, counter_base: int, src,
                      src_stride: int, dst, dst_stride: int, status=None, stream=None) -> None:

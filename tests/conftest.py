@@ -1,3 +1,4 @@
+import gc
 import os
 import sys
 
@@ -6,6 +7,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# the HIP runtime's error log (level 1: errors only) on stderr, which pytest shows with
+# a failing test: a GPU memory fault then names its address and the faulting agent
+os.environ.setdefault("AMD_LOG_LEVEL", "1")
 
 
 def pytest_configure(config):
@@ -32,13 +36,16 @@ def gpu(torch_cuda):
 @pytest.fixture(autouse=True)
 def _gpu_fault_attribution(request):
     """A GPU memory fault is reported asynchronously, at some later HIP call.  After
-    every gpu test: drain the device and make one device-to-host copy, so a fault
-    surfaces in the teardown of the test whose work caused it."""
+    every gpu test: collect the test's garbage (Tunns, engines and contexts left in
+    reference cycles are destroyed here, not by a collection during a later test),
+    drain the device and make one device-to-host copy, so a fault surfaces in the
+    teardown of the test whose work caused it."""
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
     torch = sys.modules.get("torch")
     if torch is None or not torch.cuda.is_initialized():
         return
+    gc.collect()
     torch.cuda.synchronize()
     torch.ones(1, device="cuda").cpu()

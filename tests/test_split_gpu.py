@@ -19,8 +19,10 @@ from tools import synth
 pytestmark = pytest.mark.gpu
 
 KIDX = 0x2468ACE1
-# (payload, the K that divide its keystream rounds into parts of >= 8 rounds)
-CASES = [(8192, 2), (8192, 4), (8192, 8), (8190, 4), (8177, 8), (4096, 2), (4000, 4), (2048, 2)]
+# (payload, K with parts of >= 8 keystream rounds; K that do not divide the rounds
+# give part 0 the remainder)
+CASES = [(8192, 2), (8192, 3), (8192, 4), (8192, 5), (8192, 7), (8192, 8), (8190, 4), (8177, 6), (8177, 8),
+         (4096, 2), (4096, 3), (4000, 4), (2048, 2)]
 
 
 @pytest.fixture
@@ -135,3 +137,35 @@ def test_split_choice_fills_the_grid(torch_cuda, split_ctx):
         assert int((st != 0).sum()) == 0
         assert torch.equal(w1, wd), P
         del w1, wd, src
+
+
+@pytest.mark.parametrize("K", [3, 7])
+def test_split_parts_of_unequal_length_share_workgroups(torch_cuda, split_ctx, K):
+    """203 waves of 8192-byte packets at K = 3 / 7: more jobs than the grid's 512
+    workgroups, so workgroups take 2-3 consecutive jobs and some straddle a part
+    boundary -- part 0 (22 / 10 rounds) beside part 1 (21 / 9) in one workgroup.
+    Seal and the wire-grid open equal the unsplit kernels' byte for byte."""
+    torch = torch_cuda
+    ctx = split_ctx
+    rng = np.random.default_rng(100 + K)
+    key = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+    ctx.set_keys(0, key, np.array([KIDX], np.uint32))
+    P, n = 8192, 64 * 203
+    S = synth.round_up(P + 32, 128)
+    src = synth.device_payloads(n, P, S, "cuda", seed=11 + K, offset=16)
+    w1, st1 = _seal(torch, ctx, 1, n, P, S, src, False, 99)
+    wk, stk = _seal(torch, ctx, K, n, P, S, src, False, 99)
+    assert int((st1 != 0).sum()) == 0 and int((stk != 0).sum()) == 0
+    assert torch.equal(w1, wk), "split seal differs from the unsplit kernels"
+    got, s_np = wk.cpu().numpy(), src.cpu().numpy()
+    for i in (0, 203 * 32 + 5, n - 1):
+        want = o.format_packet_data(key[0].tobytes(), KIDX, 99 + i, s_np[i * S + 16:i * S + 16 + P].tobytes())
+        assert got[i * S:i * S + P + 32].tobytes() == want, i
+    ctx.set_split(K)
+    back = torch.full((n * S + 256,), 0x5A, dtype=torch.uint8, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    ctx.open_strided(n, P + 32, 0, wk, S, back.data_ptr() + 16, S, st)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum()) == 0
+    b = back[: n * S].view(n, S)
+    assert torch.equal(b[:, 16:16 + P], src[: n * S].view(n, S)[:, 16:16 + P])
