@@ -10,6 +10,15 @@ if ROOT not in sys.path:
 # the HIP runtime's error log (level 1: errors only) on stderr, which pytest shows with
 # a failing test: a GPU memory fault then names its address and the faulting agent
 os.environ.setdefault("AMD_LOG_LEVEL", "1")
+# Device-to-host copies into pageable memory (every tensor.cpu() here) take the HIP
+# runtime's staged path at every size.  From 1 MiB the runtime otherwise locks the
+# pageable destination on the fly ("Locking to pool", tools/probes/d2h_path.py) and the
+# copy engine writes the user pages directly; both hipErrorIllegalAddress failures of
+# the suite (GPUTEST_r05: a 1,664,064-byte back.cpu(); r06h: a 4,386,816-byte
+# d_dst.cpu()) were raised inside such a copy, after a clean device synchronize
+# (DESIGN.md §6).  The library's own copies land in pinned staging or registered
+# memory (the host pipe asks its callers for pinned buffers, neptun_gpu.h).
+os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", "1000000")
 
 
 def pytest_configure(config):
