@@ -98,10 +98,15 @@ int wg_tunn_create_on(wg_engine *e, uint32_t first_slot, wg_tunn **out);
  * how many small calls' chunks went out in a launch shared with another concurrent
  * call (WG_COMBINE=1, off by default: one latency-form launch for the engine's
  * concurrent small calls of one direction, at most WG_COMBINE_DEPTH such launches in
- * flight, default 2) */
+ * flight, default 2); how many small calls' chunks were served by the engine's
+ * resident kernel instead of a launch of their own (WG_TUNN_SRV, on by default:
+ * chunks of up to 64 packets whose completion is the kernel's word) and how many
+ * times that kernel was launched (a lease of 1 s, renewed by the next call; a new
+ * launch after a key-table update) */
 typedef struct wg_engine_info {
   uint32_t tunns, lanes, max_lanes, pool_threads, streams;
   uint32_t combined;
+  uint64_t served, service_launches;
 } wg_engine_info;
 int wg_engine_get_info(const wg_engine *e, wg_engine_info *out);
 /* the engine a Tunn is attached to (NULL: a multi-GPU Tunn with private engines) */

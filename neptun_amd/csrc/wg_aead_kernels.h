@@ -66,8 +66,9 @@ struct StridedParams {
 // Split (under-filled launches of long packets, wg_gpu.cpp): every wave of 64 packets
 // is cut into `split` parts, every part a wave job of its own, so that the grid fills
 // the chip: part 0 takes rounds [0, split_q + split_rem), part j > 0 rounds
-// [j split_q + split_rem, (j + 1) split_q + split_rem), the last part to the end; the parts' Poly1305 accumulators go to
-// part_h / part_h4 ([part][packet]) and aead_strided_finish_kernel combines them,
+// [j split_q + split_rem, (j + 1) split_q + split_rem), the last part to the end; the
+// parts' Poly1305 accumulators go to part_h / part_h4 ([part][packet]) and
+// aead_strided_finish_kernel combines them,
 // writes the tags (seal) or checks them (open) and the statuses.  (Kernels of their
 // own with their own argument block: the unsplit kernels are compiled as before.)
 struct SplitArgs {
@@ -138,6 +139,42 @@ struct XlaneInlineParams {
 };
 template <bool kSeal, uint32_t G> __global__ void aead_xlane_inline_kernel(XlaneInlineParams ip);
 template <bool kSeal, uint32_t G> __global__ void aead_xlane_strided_kernel(StridedParams prm);
+
+// Resident service (wg_xlane.hip xlane_service_kernel, host side wg_tunn.cpp Service):
+// the Tunn's small calls posted to slots in pinned host memory instead of a launch
+// each.  Slot s is served by workgroups [s kSrvGroup, (s + 1) kSrvGroup) of the grid,
+// kSrvGroup x kXlaneThreads lanes, G per packet.  The host writes op / n / G and the
+// descriptors (absolute device addresses in src_off / dst_off), then seq; the
+// workgroups poll {seq, op, n, G} as one 16-byte load, run the packets exactly as the
+// latency-form kernels do (statuses into st), and the last of them to finish stores
+// seq to `done`.  A workgroup leaves when the host sets *stop or its lease runs out
+// (s_memrealtime), so the grid always drains.
+constexpr uint32_t kSrvSlots = 8, kSrvGroup = 4, kSrvDescs = 64;
+constexpr uint32_t kSrvLanes = kSrvGroup * kXlaneThreads;
+struct alignas(128) SrvSlot {
+  uint32_t seq, op, n, G;  // op: 1 seal, 0 open; seq written last
+  uint32_t pad0[28];
+  wg_packet_desc d[kSrvDescs];
+  int32_t st[kSrvDescs];
+  alignas(128) uint32_t done;
+  uint32_t pad1[31];
+  // (SrvParams::stamp) s_memrealtime of the request's phases: seen, acquired, the
+  // packets done, their stores acknowledged (workgroup 0 of the slot), published (the
+  // last workgroup)
+  uint64_t stamp[5];
+  uint64_t pad2[11];
+};
+struct SrvParams {
+  SrvSlot *slots;
+  const uint32_t *stop;
+  uint32_t *d_count;  // [slot * 32]: arrivals of the slot's workgroups (HBM)
+  const uint8_t *keys;
+  const uint32_t *key_index;
+  uint32_t key_slots;
+  uint64_t lease_ticks;  // s_memrealtime ticks (100 MHz) from each workgroup's start
+  uint32_t stamp;        // 1: record SrvSlot::stamp (WG_TUNN_SRV_STAMP, a diagnostic)
+};
+__global__ void xlane_service_kernel(SrvParams p);
 
 // wg_plan.hip: counting sort of a descriptor batch by rounds (longest first)
 constexpr uint32_t kPlanBins = 256;   // rounds 0..254, 255+ share the top bin

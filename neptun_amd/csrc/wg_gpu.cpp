@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <map>
 #include <cstdio>
@@ -40,7 +41,12 @@ struct wg_gpu_ctx {
   // install_session writes its slots, so two Tunns may never share one
   std::vector<std::pair<uint32_t, uint32_t>> claims;
   std::mutex mu;                   // serialises key-table and route-table updates
+  // key-table updates completed so far (wg_gpu_set_keys): a resident kernel holding the
+  // table in its caches since an older generation is relaunched (wg_tunn.cpp Service)
+  std::atomic<uint64_t> key_gen{0};
 };
+
+void wg_srv_ctx_closing(wg_gpu_ctx *ctx);  // wg_tunn.cpp: resident kernels on this context stop
 
 // open into line-aligned plaintext slots on the text grid (1) or on the wire grid
 // with its output runs straddling the destination's lines (0: A/B only)
@@ -109,6 +115,9 @@ void wg_ctx_release_slots(wg_gpu_ctx *ctx, uint32_t first) {
       return;
     }
 }
+uint64_t wg_ctx_key_gen(const wg_gpu_ctx *ctx) { return ctx->key_gen.load(std::memory_order_acquire); }
+const uint8_t *wg_ctx_keys(const wg_gpu_ctx *ctx) { return ctx->d_keys; }
+const uint32_t *wg_ctx_key_index(const wg_gpu_ctx *ctx) { return ctx->d_key_index; }
 // snapshot of the registered ranges as (host, bytes, dev) triples, sorted by host
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out) {
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -218,6 +227,7 @@ int wg_gpu_ctx_create(int device, uint32_t key_slots, wg_gpu_ctx **out) {
 int wg_gpu_ctx_destroy(wg_gpu_ctx *ctx) {
   if (!ctx) return WG_RC_OK;
   DeviceGuard g(ctx->device);
+  wg_srv_ctx_closing(ctx);
   (void)hipDeviceSynchronize();
   (void)hipFree(ctx->d_keys);
   (void)hipFree(ctx->d_key_index);
@@ -247,6 +257,7 @@ int wg_gpu_set_keys(wg_gpu_ctx *ctx, uint32_t first_slot, uint32_t n, const uint
                         hipMemcpyHostToDevice, s),
          "set_keys: index copy");
   WG_HIP(hipStreamSynchronize(s), "set_keys: sync");
+  ctx->key_gen.fetch_add(1, std::memory_order_acq_rel);
   return WG_RC_OK;
 }
 

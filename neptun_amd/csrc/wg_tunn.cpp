@@ -46,6 +46,7 @@
 
 #include "neptun_gpu.h"
 #include "neptun_tunn.h"
+#include "wg_aead_kernels.h"
 
 int wg_pipe_fail(int rc, const char *what, hipError_t e);  // wg_gpu.cpp
 int wg_ctx_device(const wg_gpu_ctx *ctx);                   // wg_gpu.cpp
@@ -59,6 +60,9 @@ int wg_launch_desc_hinted(wg_gpu_ctx *ctx, bool seal, const wg_packet_desc *desc
 void wg_ctx_reg_snapshot(wg_gpu_ctx *ctx, std::vector<uint64_t> &out);  // wg_gpu.cpp
 int wg_ctx_claim_slots(wg_gpu_ctx *ctx, uint32_t first, uint32_t count);  // wg_gpu.cpp
 void wg_ctx_release_slots(wg_gpu_ctx *ctx, uint32_t first);              // wg_gpu.cpp
+uint64_t wg_ctx_key_gen(const wg_gpu_ctx *ctx);                          // wg_gpu.cpp
+const uint8_t *wg_ctx_keys(const wg_gpu_ctx *ctx);                       // wg_gpu.cpp
+const uint32_t *wg_ctx_key_index(const wg_gpu_ctx *ctx);                 // wg_gpu.cpp
 
 // ---------------------------------------------------------------------------
 // replay window: ReceivingKeyCounterValidator, session.rs:40-157
@@ -597,6 +601,7 @@ struct CombSlot {
   hipStream_t stream = nullptr;
   std::atomic<int> readers{0};  // calls of the launch that have not taken their statuses yet
 };
+struct Service;  // (the resident service of the small calls, below)
 struct CombSeg {
   const wg_packet_desc *descs = nullptr;
   uint32_t n = 0, max_len = 0;
@@ -637,6 +642,10 @@ struct Staging {
   // sequence number, statuses and slot are the combiner's
   CombSeg *comb = nullptr;
   CombSeg cseg;  // (this set's chunk, when it is posted to a combiner)
+  // the chunk in flight was posted to the engine's resident service (Service below):
+  // its slot and sequence number
+  Service *srv = nullptr;
+  uint32_t srv_slot = 0, srv_seq = 0;
 };
 
 void free_buffers(Staging &s) {
@@ -855,7 +864,8 @@ struct wg_engine {
   Driver *driver = nullptr;
   std::mutex driver_mu;
   Combiner *comb[2] = {nullptr, nullptr};  // [seal]: small launches of concurrent calls
-  std::mutex comb_mu;                             // (making them)
+  std::mutex comb_mu;                             // (making them, and the service)
+  Service *srv = nullptr;                         // resident service of the small calls
 };
 
 namespace {
@@ -1211,10 +1221,15 @@ bool word_event() {
   return e && std::atoi(e) != 0;
 }
 hipError_t comb_wait(Staging &S, uint32_t m);
+hipError_t srv_wait(Staging &S, uint32_t m);
 hipError_t wait_chunk(Staging &S, uint32_t m) {
   if (S.comb) {
     S.flagged = false;
     return comb_wait(S, m);
+  }
+  if (S.srv) {
+    S.flagged = false;
+    return srv_wait(S, m);
   }
   if (S.flagged) {
     S.flagged = false;
@@ -1421,6 +1436,341 @@ hipError_t comb_wait(Staging &S, uint32_t m) {
   return e;
 }
 
+// ---------------------------------------------------------------------------
+// Resident service of the small calls (wg_xlane.hip xlane_service_kernel).
+//
+// A launch per small call costs its ~5 us of launch and, with concurrent callers,
+// its turn on the process's hardware queues: 8 threads x 50 packets held each call
+// 25-28 us against 13-15 alone (profiles/r06d_tt).  A resident kernel does not: it
+// polls kSrvSlots request slots in pinned host memory (a probe of the bare mechanism:
+// 3.9 us from post to done, 3.7 M calls/s from 16 threads, other streams' kernels
+// unaffected, profiles/r06l/doorbell_*.jsonl), and a call is a post -- its descriptors
+// with absolute addresses, then the sequence number -- and a spin on the slot's done
+// word.  Per packet the kernel runs xlane_packet exactly as the latency-form launches.
+//
+// Lifetime: the kernel's workgroups leave on *stop or when their lease (kSrvLeaseUs
+// from their start) runs out.  A call posts only while the lease has more than
+// kSrvMarginUs left on the host's clock (the kernel's workgroups started after the
+// launch, so their leases end later); otherwise, or when the context's key table
+// changed since the launch (a resident kernel may hold the old keys in its caches),
+// the first caller to see it waits for the calls in flight, stops the kernel and
+// launches the next.  A watchdog thread per service stops the kernel once no call has
+// been posted for WG_TUNN_SRV_IDLE_US (1000): a resident kernel counts as device work
+// to hipDeviceSynchronize, which therefore waits for the engine to go idle that long.
+// The watchdog and a poster meet Dekker-style (live / inflight, sequentially
+// consistent): a posted call's kernel is never stopped under it.
+// WG_TUNN_SRV=0 turns it off (the calls launch as before).
+constexpr int64_t kSrvLeaseUs = 1000000, kSrvMarginUs = 5000;
+int64_t srv_idle_us() {  // (read per watchdog round)
+  const char *e = std::getenv("WG_TUNN_SRV_IDLE_US");
+  return e ? std::max(100L, std::atol(e)) : 1000L;
+}
+int64_t srv_lease_us() {  // (WG_TUNN_SRV_LEASE_US: tests renew it often; read per launch)
+  const char *e = std::getenv("WG_TUNN_SRV_LEASE_US");
+  return e ? std::max(2000L, std::atol(e)) : kSrvLeaseUs;
+}
+
+struct Service {
+  wg_gpu_ctx *ctx = nullptr;
+  int device = 0;
+  wg::SrvSlot *slots = nullptr;  // pinned, coherent
+  uint32_t *stop = nullptr;      // pinned, coherent
+  uint32_t *d_count = nullptr;   // HBM
+  hipStream_t stream = nullptr;
+  std::mutex mu;                 // restarts
+  std::atomic<int> inflight{0};  // posted calls not yet waited for
+  std::atomic<uint32_t> free_mask{(1u << wg::kSrvSlots) - 1u};
+  std::atomic<bool> live{false};
+  std::atomic<int64_t> post_until{0};  // steady-clock us: no post to the running kernel after
+  std::atomic<uint64_t> key_gen{0};
+  uint32_t seq[wg::kSrvSlots] = {};    // (each touched by its slot's holder only)
+  std::atomic<uint64_t> calls{0}, launches{0};
+  std::atomic<int64_t> last_post{0};   // steady-clock us
+  std::thread watch;                   // the idle stop
+  std::atomic<bool> quit{false};
+  // WG_TUNN_SRV_STAMP=path (a diagnostic): per request the device's phase stamps and
+  // the host's post-to-seen time, summed; written to path when the service ends
+  const char *stamp_path = nullptr;
+  std::mutex stamp_mu;
+  double st_sum[6] = {};  // us: seen->acquired, ->packets, ->acked, ->published, device total, host total
+  uint64_t st_n = 0;
+  int64_t post_us[wg::kSrvSlots] = {};
+};
+
+bool srv_on() {  // (read per call)
+  const char *e = std::getenv("WG_TUNN_SRV");
+  return !e || std::atoi(e) != 0;
+}
+int64_t steady_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// every live service is told to stop at exit (host memory only: registered after the
+// HIP runtime's own exit handlers, so it runs before them)
+std::mutex g_srv_mu;
+std::vector<Service *> g_srvs;
+void srv_atexit() {
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  bool any = false;
+  for (Service *V : g_srvs)
+    if (V->live.load()) {
+      __atomic_store_n(V->stop, 1u, __ATOMIC_RELEASE);
+      any = true;
+    }
+  if (any) std::this_thread::sleep_for(std::chrono::milliseconds(2));  // (the workgroups poll every ~2 us)
+}
+
+// stop the kernel and wait (bounded) for its grid to drain; false: it did not
+bool srv_halt(Service &V) {
+  if (!V.stream) return true;
+  __atomic_store_n(V.stop, 1u, __ATOMIC_RELEASE);
+  V.live.store(false, std::memory_order_seq_cst);
+  const int64_t t0 = steady_us();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(V.stream);
+    if (q != hipErrorNotReady) return true;  // (done, or the stream's error)
+    if (steady_us() - t0 > 3 * kSrvLeaseUs) return false;
+    std::this_thread::yield();
+  }
+}
+
+void srv_watch(Service *V) {
+  while (!V->quit.load(std::memory_order_acquire)) {
+    std::this_thread::sleep_for(std::chrono::microseconds(250));
+    const int64_t idle = srv_idle_us();
+    if (!V->live.load(std::memory_order_acquire) || steady_us() - V->last_post.load() < idle) continue;
+    std::lock_guard<std::mutex> lk(V->mu);
+    if (!V->live.load() || steady_us() - V->last_post.load() < idle) continue;
+    V->live.store(false, std::memory_order_seq_cst);
+    if (V->inflight.load(std::memory_order_seq_cst) != 0) {  // (a post got in: keep it)
+      V->live.store(true, std::memory_order_seq_cst);
+      continue;
+    }
+    __atomic_store_n(V->stop, 1u, __ATOMIC_RELEASE);  // (the next post syncs the stream)
+  }
+}
+
+void srv_stamp_dump(Service *V) {
+  if (!V->stamp_path || !V->st_n) return;
+  if (FILE *f = std::fopen(V->stamp_path, "a")) {
+    const double n = (double)V->st_n;
+    std::fprintf(f,
+                 "{\"requests\": %llu, \"us\": {\"seen_to_acquired\": %.2f, \"acquired_to_packets\": %.2f, "
+                 "\"packets_to_acked\": %.2f, \"acked_to_published\": %.2f, \"device_seen_to_published\": %.2f, "
+                 "\"host_post_to_seen_done\": %.2f}}\n",
+                 (unsigned long long)V->st_n, V->st_sum[0] / n, V->st_sum[1] / n, V->st_sum[2] / n, V->st_sum[3] / n,
+                 V->st_sum[4] / n, V->st_sum[5] / n);
+    std::fclose(f);
+  }
+}
+
+void srv_free(Service *V) {
+  if (!V) return;
+  srv_stamp_dump(V);
+  {
+    std::lock_guard<std::mutex> lk(g_srv_mu);
+    g_srvs.erase(std::remove(g_srvs.begin(), g_srvs.end(), V), g_srvs.end());
+  }
+  V->quit.store(true, std::memory_order_release);
+  if (V->watch.joinable()) V->watch.join();
+  DevGuard dg(V->device);
+  if (!srv_halt(*V)) return;  // (a grid that does not drain keeps its memory: leaked, not freed under it)
+  if (V->stream) (void)hipStreamDestroy(V->stream);
+  (void)hipHostFree(V->slots);
+  (void)hipHostFree(V->stop);
+  (void)hipFree(V->d_count);
+  delete V;
+}
+
+Service *srv_get(wg_engine *g) {
+  std::lock_guard<std::mutex> lk(g->comb_mu);
+  if (g->srv) return g->srv;
+  Service *V = new (std::nothrow) Service;
+  if (!V) return nullptr;
+  V->ctx = g->ctx;
+  V->device = g->device;
+  DevGuard dg(g->device);
+  bool ok = hipHostMalloc((void **)&V->slots, sizeof(wg::SrvSlot) * wg::kSrvSlots, hipHostMallocCoherent) == hipSuccess;
+  ok = ok && hipHostMalloc((void **)&V->stop, 64, hipHostMallocCoherent) == hipSuccess;
+  ok = ok && hipMalloc((void **)&V->d_count, wg::kSrvSlots * 32 * 4) == hipSuccess;
+  ok = ok && hipStreamCreateWithFlags(&V->stream, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && hipMemsetAsync(V->d_count, 0, wg::kSrvSlots * 32 * 4, V->stream) == hipSuccess &&
+       hipStreamSynchronize(V->stream) == hipSuccess;
+  if (!ok) {
+    srv_free(V);
+    return nullptr;
+  }
+  std::memset(V->slots, 0, sizeof(wg::SrvSlot) * wg::kSrvSlots);
+  *V->stop = 0;
+  V->stamp_path = std::getenv("WG_TUNN_SRV_STAMP");
+  {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(srv_atexit); });
+    std::lock_guard<std::mutex> lk2(g_srv_mu);
+    g_srvs.push_back(V);
+  }
+  V->watch = std::thread(srv_watch, V);
+  g->srv = V;
+  return V;
+}
+
+bool srv_stale(const Service &V) {
+  return !V.live.load(std::memory_order_seq_cst) || steady_us() > V.post_until.load(std::memory_order_acquire) ||
+         wg_ctx_key_gen(V.ctx) != V.key_gen.load(std::memory_order_acquire);
+}
+
+}  // namespace
+
+// a context is being destroyed (wg_gpu.cpp): the services reading its key table stop first
+void wg_srv_ctx_closing(wg_gpu_ctx *ctx) {
+  std::lock_guard<std::mutex> lk(g_srv_mu);
+  for (Service *V : g_srvs)
+    if (V->ctx == ctx) {
+      std::lock_guard<std::mutex> lk2(V->mu);
+      DevGuard dg(V->device);
+      (void)srv_halt(*V);
+    }
+}
+
+namespace {
+
+// a fresh kernel (the caller holds no inflight count)
+int srv_restart(Service &V) {
+  std::lock_guard<std::mutex> lk(V.mu);
+  if (!srv_stale(V)) return WG_RC_OK;
+  while (V.inflight.load(std::memory_order_acquire) != 0) _mm_pause();  // (posted calls finish first)
+  DevGuard dg(V.device);
+  // the previous kernel (live, or stopped by the watchdog and still draining) gone
+  __atomic_store_n(V.stop, 1u, __ATOMIC_RELEASE);
+  V.live.store(false, std::memory_order_seq_cst);
+  TUNN_HIP(hipStreamSynchronize(V.stream), "tunn: service stop");
+  __atomic_store_n(V.stop, 0u, __ATOMIC_RELEASE);
+  TUNN_HIP(hipMemsetAsync(V.d_count, 0, wg::kSrvSlots * 32 * 4, V.stream), "tunn: service counters");
+  // (a key update that completes after this read is seen as a new generation next time)
+  const uint64_t gen = wg_ctx_key_gen(V.ctx);
+  const int64_t t_launch = steady_us(), lease = srv_lease_us();
+  wg::SrvParams prm{V.slots, V.stop, V.d_count, wg_ctx_keys(V.ctx), wg_ctx_key_index(V.ctx),
+                    wg_gpu_ctx_key_slots(V.ctx), (uint64_t)lease * 100u, V.stamp_path ? 1u : 0u};
+  hipLaunchKernelGGL(wg::xlane_service_kernel, dim3(wg::kSrvSlots * wg::kSrvGroup), dim3(wg::kXlaneThreads), 0,
+                     V.stream, prm);
+  TUNN_HIP(hipGetLastError(), "tunn: service launch");
+  V.key_gen.store(gen, std::memory_order_release);
+  V.post_until.store(t_launch + lease - std::min(kSrvMarginUs, lease / 4), std::memory_order_release);
+  V.last_post.store(t_launch);  // (the watchdog's idle clock starts now)
+  V.live.store(true, std::memory_order_seq_cst);
+  V.launches.fetch_add(1, std::memory_order_relaxed);
+  return WG_RC_OK;
+}
+
+// lanes per packet for a request, chosen as the latency-form launches choose them
+// (wg_gpu.cpp xlane_group_hinted) within the slot's kSrvLanes lanes and the kernel's
+// G = 64 ... 8; 0: not a service request
+uint32_t srv_group(uint32_t n, uint32_t max_len, bool seal) {
+  if (n * 8u > wg::kSrvLanes) return 0u;
+  const uint32_t P = seal ? max_len : (max_len > WG_DATA_OVERHEAD_SZ ? max_len - WG_DATA_OVERHEAD_SZ : 0u);
+  const uint32_t nb = 1u + (P + 63u) / 64u;  // keystream blocks of the longest packet
+  uint32_t g = 8u;
+  while (g < nb && g < 64u) g *= 2u;
+  uint32_t G = 64u;
+  while (n * G > wg::kSrvLanes) G /= 2u;
+  return std::min(G, g);
+}
+
+// Post chunk S (m packets, its descriptors relative to in / out) to the service.
+// Returns WG_RC_OK (posted: S.srv set), 1 (not taken: no free slot or too large --
+// the caller launches), or an error.
+int srv_post(Service &V, Staging &S, bool seal, uint32_t m, const uint8_t *in, const uint8_t *out) {
+  if (m == 0 || m > wg::kSrvDescs) return 1;
+  const uint32_t G = srv_group(m, max_desc_len(S.h_desc, m), seal);
+  if (!G) return 1;
+  uint32_t fm = V.free_mask.load(std::memory_order_acquire), bit;
+  do {
+    if (!fm) return 1;
+    bit = (uint32_t)__builtin_ctz(fm);
+  } while (!V.free_mask.compare_exchange_weak(fm, fm & ~(1u << bit), std::memory_order_acq_rel));
+  for (;;) {
+    V.inflight.fetch_add(1, std::memory_order_seq_cst);
+    if (!srv_stale(V)) break;
+    V.inflight.fetch_sub(1, std::memory_order_seq_cst);
+    if (const int rc = srv_restart(V)) {
+      V.free_mask.fetch_or(1u << bit, std::memory_order_acq_rel);
+      return rc;
+    }
+  }
+  wg::SrvSlot &sl = V.slots[bit];
+  const uint64_t ib = reinterpret_cast<uint64_t>(in), ob = reinterpret_cast<uint64_t>(out);
+  for (uint32_t j = 0; j < m; ++j) {
+    wg_packet_desc d = S.h_desc[j];
+    d.src_off += ib;
+    d.dst_off += ob;
+    sl.d[j] = d;
+  }
+  sl.op = seal ? 1u : 0u;
+  sl.n = m;
+  sl.G = G;
+  const uint32_t q = ++V.seq[bit];
+  const int64_t tp = steady_us();
+  V.last_post.store(tp, std::memory_order_relaxed);
+  V.post_us[bit] = tp;
+  __atomic_store_n(&sl.seq, q, __ATOMIC_RELEASE);
+  S.srv = &V;
+  S.srv_slot = bit;
+  S.srv_seq = q;
+  V.calls.fetch_add(1, std::memory_order_relaxed);
+  return WG_RC_OK;
+}
+
+// the posted chunk's done word, then its statuses; the slot and the inflight count
+// are given back on every path
+hipError_t srv_wait(Staging &S, uint32_t m) {
+  Service &V = *S.srv;
+  S.srv = nullptr;
+  wg::SrvSlot &sl = V.slots[S.srv_slot];
+  hipError_t e = hipSuccess;
+  const int64_t t0 = steady_us();
+  for (uint32_t i = 1;; ++i) {
+    if (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) == S.srv_seq) break;
+    if ((i & 1023u) == 0u) {
+      const int64_t dt = steady_us() - t0;
+      if (dt > 200) {  // (a slow answer: is the kernel still there?)
+        const hipError_t q = hipStreamQuery(V.stream);
+        if (q == hipSuccess) {  // ended without answering (never expected: see the lease)
+          if (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) == S.srv_seq) break;
+          e = hipErrorLaunchFailure;
+          break;
+        }
+        if (q != hipErrorNotReady) {
+          e = q;
+          break;
+        }
+        if (dt > 2 * std::max(kSrvLeaseUs, srv_lease_us())) {
+          e = hipErrorLaunchTimeOut;
+          break;
+        }
+      }
+    }
+    _mm_pause();
+  }
+  if (e == hipSuccess) {
+    std::memcpy(S.h_st, sl.st, (size_t)m * 4);
+    if (V.stamp_path) {
+      const double host = (double)(steady_us() - V.post_us[S.srv_slot]);
+      const uint64_t *t = sl.stamp;
+      std::lock_guard<std::mutex> lk(V.stamp_mu);
+      for (int k = 0; k < 4; ++k) V.st_sum[k] += (double)(t[k + 1] - t[k]) / 100.0;
+      V.st_sum[4] += (double)(t[4] - t[0]) / 100.0;
+      V.st_sum[5] += host;
+      ++V.st_n;
+    }
+  } else {
+    V.live.store(false, std::memory_order_release);  // (the next post restarts it)
+  }
+  V.inflight.fetch_sub(1, std::memory_order_acq_rel);
+  V.free_mask.fetch_or(1u << S.srv_slot, std::memory_order_acq_rel);
+  return e;
+}
+
 struct PipelineDrain {
   Engine &E;
   explicit PipelineDrain(Engine &e) : E(e) { drain(); }
@@ -1433,6 +1783,8 @@ struct PipelineDrain {
         (void)comb_wait_word(*g->slot, g->seq);
         g->slot->readers.fetch_sub(1, std::memory_order_acq_rel);
       }
+    for (auto &S : E.st)
+      if (S.srv) (void)srv_wait(S, 0);  // (an error path left a posted chunk unwaited)
     for (auto &S : E.st)
       if (S.busy) {
         (void)hipStreamSynchronize(S.stream);
@@ -1552,7 +1904,17 @@ int run_chunks(Engine &E, bool seal, Pack pack, Unpack unpack, bool abs_src = fa
       }
       // (a call of one chunk only: a caller never holds a slot's statuses while it
       // leads another round, whose slot may be that one)
-      if (word && nc == 1 && m <= kCombSegMax && E.grp && combine_on()) {
+      int posted = 1;  // (the engine's resident service took the chunk: 0)
+      if (word && nc == 1 && E.grp && srv_on()) {
+        if (Service *V = srv_get(E.grp)) {
+          posted = srv_post(*V, S, seal, (uint32_t)m, in, out);
+          if (posted < 0) return posted;
+          if (posted == 0) S.flagged = true;
+        }
+      }
+      if (posted == 0) {
+        // (posted: no launch, no event -- srv_wait)
+      } else if (word && nc == 1 && m <= kCombSegMax && E.grp && combine_on()) {
         // one launch with the engine's other small calls of this direction (Combiner)
         Combiner *C = comb_get(E.grp, seal);
         if (!C) return wg_pipe_fail(WG_RC_OUT_OF_MEMORY, "tunn: combiner", hipSuccess);
@@ -2454,6 +2816,7 @@ int engine_make(wg_gpu_ctx *ctx, wg_engine **out) {
 }
 
 void engine_free(wg_engine *g) {
+  srv_free(g->srv);
   for (Engine *E : g->lanes) destroy_engine(E);
   comb_free(g->comb[0]);
   comb_free(g->comb[1]);
@@ -2537,6 +2900,10 @@ int wg_engine_get_info(const wg_engine *e, wg_engine_info *out) {
     std::lock_guard<std::mutex> cl(const_cast<wg_engine *>(e)->comb_mu);
     for (const Combiner *C : e->comb)
       if (C) out->combined += C->shared_calls.load(std::memory_order_relaxed);
+    if (const Service *V = e->srv) {
+      out->served = V->calls.load(std::memory_order_relaxed);
+      out->service_launches = V->launches.load(std::memory_order_relaxed);
+    }
   }
   return WG_RC_OK;
 }

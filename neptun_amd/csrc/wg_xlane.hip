@@ -104,14 +104,36 @@ __device__ __forceinline__ F26 f26_zero() {
 
 }  // namespace
 
+// LDS staging of packets in host memory (kStage: the Tunn's zero-copy small calls).
+// The lane-span layout has every lane read and write its own blocks 16 bytes at a time,
+// C 64-byte blocks apart: over PCIe each piece is a request of its own.  50 packets of
+// 1350 B from 8 concurrent callers are then ~0.9 G read requests and as many 16-byte
+// writes per second -- with their headers about the whole upstream PCIe link, where 8
+// callers flattened at 54 Gbit/s with launches and with the resident service alike
+// (profiles/r06n/tt_*).  Staged, the group moves its packet through LDS: its G lanes
+// load consecutive pieces (one load instruction covers G x 16 contiguous bytes, which
+// the memory pipeline merges), every lane then reads and writes its blocks in LDS, and
+// the group stores the output the same contiguous way -- the same bytes in 4-8x fewer,
+// larger transactions, and every input piece in flight at once (one round trip).
+constexpr uint32_t kXlaneStagePieces = 3072;  // 48 KiB of 16-byte pieces per workgroup
+template <uint32_t G>
+__device__ __forceinline__ constexpr uint32_t stage_cap() {  // pieces per group
+  return kXlaneStagePieces / (kXlaneThreads / G);
+}
+// (cross-lane LDS traffic inside one wave: the wave's LDS operations complete in order;
+// this keeps the compiler from moving a lane's read above another lane's write)
+__device__ __forceinline__ void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // One packet on the G lanes of its group (l = the lane's index in the group): the
 // checks, the spread keystream / Poly1305 spans, the combine, the tag.  align: the
 // packet's offsets OR-ed (misaligned -> WG_STATUS_MISALIGNED); st: its status (or null).
-template <bool kSeal, uint32_t G>
+// kStage: through the group's LDS region gb (stage_cap<G>() pieces; the caller checks
+// that the packet's (P + 31) / 16 pieces fit).
+template <bool kSeal, uint32_t G, bool kStage = false>
 __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uint8_t *dst, uint32_t len,
                                              uint32_t slot, uint64_t counter, uint64_t align, int32_t *st,
                                              const uint8_t *keys, const uint32_t *key_index, uint32_t key_slots,
-                                             uint32_t pkt) {
+                                             uint32_t pkt, uint4 *gb = nullptr) {
   int32_t status = WG_STATUS_OK;
   if (!kSeal && slot == WG_KEY_SLOT_INVALID_PACKET) status = WG_STATUS_INVALID_PACKET;
   else if (!kSeal && slot == WG_KEY_SLOT_NO_SESSION) status = WG_STATUS_NO_CURRENT_SESSION;
@@ -143,12 +165,28 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   auto load_block = [&](uint32_t b, uint4 (&x)[4]) {
     const uint32_t off = 64u * (b - 1u);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      x[q] = (b >= 1u && off + 16u * (uint32_t)q < P) ? xld16(in + off + 16u * (uint32_t)q, B) : make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < 4; ++q) {
+      const bool has = b >= 1u && off + 16u * (uint32_t)q < P;
+      if constexpr (kStage) x[q] = has ? gb[(off >> 4) + (uint32_t)q] : make_uint4(0, 0, 0, 0);
+      else x[q] = has ? xld16(in + off + 16u * (uint32_t)q, B) : make_uint4(0, 0, 0, 0);
+    }
   };
   uint4 x[4];
   const bool any = b0 < NB;
-  if (any) load_block(b0, x);
+  // staged: the group's input pieces (seal: the plaintext; open: ciphertext + tag),
+  // G consecutive pieces per load instruction, up to 8 per lane in flight at once
+  constexpr uint32_t kBatch = 8;
+  const uint32_t np_in = kSeal ? (P + 15u) / 16u : (P + 31u) / 16u;
+  uint4 sv[kBatch];
+  if constexpr (kStage) {
+#pragma unroll
+    for (uint32_t k = 0; k < kBatch; ++k) {
+      const uint32_t p = l + k * G;
+      sv[k] = p < np_in ? xld16(in + 16u * p, B) : make_uint4(0, 0, 0, 0);
+    }
+  } else {
+    if (any) load_block(b0, x);
+  }
   uint32_t key[8];
   uint32_t sidx, n1, n2;
   {
@@ -168,6 +206,34 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     }
   }
   const bool wr = kSeal || status == WG_STATUS_OK;  // (group-uniform)
+  uint32_t tw[8] = {0, 0, 0, 0, 0, 0, 0, 0};          // open: the received tag's two pieces
+  if constexpr (kStage) {
+    lds_wave_sync();  // (the group's previous packet has left the stage)
+#pragma unroll
+    for (uint32_t k = 0; k < kBatch; ++k) {
+      const uint32_t p = l + k * G;
+      if (p < np_in) gb[p] = sv[k];
+    }
+    for (uint32_t p0 = kBatch * G; p0 < np_in; p0 += kBatch * G) {  // (packets past 8 G pieces)
+#pragma unroll
+      for (uint32_t k = 0; k < kBatch; ++k) {
+        const uint32_t p = p0 + l + k * G;
+        sv[k] = p < np_in ? xld16(in + 16u * p, B) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kBatch; ++k) {
+        const uint32_t p = p0 + l + k * G;
+        if (p < np_in) gb[p] = sv[k];
+      }
+    }
+    lds_wave_sync();
+    if (any) load_block(b0, x);
+    if (!kSeal && l == Lu - 1u) {  // (before this lane's last block overwrites the tag's first bytes)
+      const uint4 ta = gb[P >> 4], tb = (P & 15u) ? gb[(P >> 4) + 1u] : make_uint4(0, 0, 0, 0);
+      tw[0] = ta.x; tw[1] = ta.y; tw[2] = ta.z; tw[3] = ta.w;
+      tw[4] = tb.x; tw[5] = tb.y; tw[6] = tb.z; tw[7] = tb.w;
+    }
+  }
 
   Poly ps;
   uint32_t kpieces = 0;  // pieces this lane absorbed
@@ -187,7 +253,10 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
           w[j] &= byte_mask((int)valid, j);
           c[j] &= byte_mask((int)valid, j);
         }
-        if (wr) xstore_partial(out + o, w, (int)valid, B);
+        if constexpr (kStage) gb[o >> 4] = make_uint4(w[0], w[1], w[2], w[3]);  // (in place, zeros past P)
+        else if (wr) xstore_partial(out + o, w, (int)valid, B);
+      } else if constexpr (kStage) {
+        gb[o >> 4] = make_uint4(w[0], w[1], w[2], w[3]);
       } else if (wr) {
         xst16(out + o, w[0], w[1], w[2], w[3], B);
       }
@@ -242,23 +311,54 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     uint32_t tag[4];
     poly_finish(ps, s, tag);
     if (kSeal) {
-      uint8_t *t = out + P;  // right after the ciphertext (session.rs:247-252)
-      if (xok((uint64_t)t, 16u, B.out_lo, B.out_hi, B)) {
+      if constexpr (kStage) {  // (into the stage, after this lane's last ciphertext piece)
+        uint8_t *t = reinterpret_cast<uint8_t *>(gb) + P;
 #pragma unroll
         for (int q = 0; q < 16; ++q) t[q] = (uint8_t)(tag[q / 4] >> (8 * (q % 4)));
+      } else {
+        uint8_t *t = out + P;  // right after the ciphertext (session.rs:247-252)
+        if (xok((uint64_t)t, 16u, B.out_lo, B.out_hi, B)) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) t[q] = (uint8_t)(tag[q / 4] >> (8 * (q % 4)));
+        }
       }
     } else {
       // received tag = bytes [P, P + 16) after the header: two aligned pieces
-      const uint32_t o = P & ~15u;
-      const uint4 ta = xld16(in + o, B);
-      const uint4 tb = (P & 15u) ? xld16(in + o + 16u, B) : make_uint4(0, 0, 0, 0);
-      const uint32_t tw[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+      if constexpr (!kStage) {
+        const uint32_t o = P & ~15u;
+        const uint4 ta = xld16(in + o, B);
+        const uint4 tb = (P & 15u) ? xld16(in + o + 16u, B) : make_uint4(0, 0, 0, 0);
+        tw[0] = ta.x; tw[1] = ta.y; tw[2] = ta.z; tw[3] = ta.w;
+        tw[4] = tb.x; tw[5] = tb.y; tw[6] = tb.z; tw[7] = tb.w;
+      }
       const int sh = (int)(P & 15u);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bad |= bytes_at(tw, sh + 4 * j) ^ tag[j];
     }
   }
-  if (kSeal) {
+  if constexpr (kStage) {
+    // the group's output, G consecutive pieces per store instruction (seal: ciphertext
+    // + tag after the header; open: the plaintext, or ring's zeros on a failed tag)
+    if (!kSeal) {
+      bad = gshfl<G>(bad, Lu - 1u);
+      if (bad && wr) status = WG_STATUS_INVALID_AEAD_TAG;
+    }
+    lds_wave_sync();
+    if (wr) {
+      const uint32_t nb_out = kSeal ? P + 16u : P, np_out = (nb_out + 15u) / 16u;
+      for (uint32_t p = l; p < np_out; p += G) {
+        const uint4 y = bad ? make_uint4(0, 0, 0, 0) : gb[p];
+        const uint32_t o = 16u * p;
+        if (o + 16u <= nb_out) {
+          xst16(out + o, y.x, y.y, y.z, y.w, B);
+        } else {
+          const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
+          xstore_partial(out + o, yw, (int)(nb_out - o), B);
+        }
+      }
+      if (kSeal && l == 0u) xst16(dst, WG_MSG_DATA, sidx, n1, n2, B);  // header (session.rs:224-229)
+    }
+  } else if (kSeal) {
     if (l == 0u) xst16(dst, WG_MSG_DATA, sidx, n1, n2, B);  // header (session.rs:224-229)
   } else {
     bad = gshfl<G>(bad, Lu - 1u);
@@ -318,8 +418,17 @@ __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_kernel(DescParams pr
   if (prm.done_flag) grid_done(prm.done_count, prm.done_flag, prm.done_seq);  // (kernel-uniform)
 }
 
+// a packet of `len` input bytes fits a group's stage (xlane_packet kStage)
+template <bool kSeal, uint32_t G>
+__device__ __forceinline__ bool stage_fits(uint32_t len) {
+  const uint32_t P = kSeal ? len : (len >= WG_DATA_OVERHEAD_SZ ? len - WG_DATA_OVERHEAD_SZ : 0u);
+  return (P + 31u) / 16u <= stage_cap<G>();
+}
+
+// (the Tunn's small calls: packets in host memory -- staged where they fit)
 template <bool kSeal, uint32_t G>
 __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_inline_kernel(XlaneInlineParams ip) {
+  __shared__ uint4 stage[kXlaneStagePieces];
   const DescParams &prm = ip.prm;
   const uint32_t gid = blockIdx.x * (kXlaneThreads / G) + threadIdx.x / G;  // packet (batch position)
   const uint32_t l = threadIdx.x & (G - 1u);
@@ -327,8 +436,13 @@ __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_inline_kernel(XlaneI
     const wg_packet_desc d = ip.d[gid];
     const uint8_t *src = reinterpret_cast<const uint8_t *>(reinterpret_cast<uint64_t>(prm.src) + d.src_off);
     uint8_t *dst = reinterpret_cast<uint8_t *>(reinterpret_cast<uint64_t>(prm.dst) + d.dst_off);
-    xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, prm.status + gid,
-                           prm.keys, prm.key_index, prm.key_slots, gid);
+    if (stage_fits<kSeal, G>(d.len))  // (group-uniform)
+      xlane_packet<kSeal, G, true>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off,
+                                   prm.status + gid, prm.keys, prm.key_index, prm.key_slots, gid,
+                                   stage + (threadIdx.x / G) * stage_cap<G>());
+    else
+      xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, prm.status + gid,
+                             prm.keys, prm.key_index, prm.key_slots, gid);
   }
   if (prm.done_flag) grid_done(prm.done_count, prm.done_flag, prm.done_seq);  // (kernel-uniform)
 }
@@ -344,6 +458,123 @@ __global__ __launch_bounds__(kXlaneThreads) void aead_xlane_strided_kernel(Strid
   xlane_packet<kSeal, G>(l, prm.src + (uint64_t)i * prm.src_stride, prm.dst + (uint64_t)i * prm.dst_stride, prm.len,
                          prm.key_slot, prm.counter_base + i, 0u, prm.status ? prm.status + i : nullptr, prm.keys,
                          prm.key_index, 0xffffffffu, i);
+}
+
+// ---------------------------------------------------------------------------
+// Resident service (wg_aead_kernels.h SrvSlot; host side wg_tunn.cpp Service).
+// NepTUN's workers hand the data plane at most 50 packets at a time from every
+// physical core (packet_workers.rs:27, :113-131).  As launches, concurrent calls of
+// this size queue on the process's hardware queues (~13 us of queue time each: 8
+// callers ran 54 Gbit/s); posted to this kernel's slots, a call costs
+// its PCIe round trips and no launch.
+// ---------------------------------------------------------------------------
+namespace {
+
+// {seq, op, n, G} of a slot in one system-coherent 16-byte load (the host writes seq
+// last, so a new seq comes with its own op / n / G)
+typedef unsigned int srv_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 srv_poll(const SrvSlot *sl) {
+  srv_u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=v"(v)
+               : "v"(reinterpret_cast<uint64_t>(sl))
+               : "memory");
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// this workgroup's packets of the request (lane: its index among the slot's lanes)
+template <bool kSeal, uint32_t G>
+__device__ __forceinline__ void srv_packets(SrvSlot *sl, uint32_t lane, uint32_t n, const SrvParams &p,
+                                            uint4 *stage) {
+  const uint32_t l = lane & (G - 1u);
+  uint4 *gb = stage + ((lane % kXlaneThreads) / G) * stage_cap<G>();
+  for (uint32_t i = lane / G; i < n; i += kSrvLanes / G) {  // (group-uniform)
+    const wg_packet_desc d = sl->d[i];
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(d.src_off);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(d.dst_off);
+    if (stage_fits<kSeal, G>(d.len))
+      xlane_packet<kSeal, G, true>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, sl->st + i,
+                                   p.keys, p.key_index, p.key_slots, i, gb);
+    else
+      xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, sl->st + i, p.keys,
+                             p.key_index, p.key_slots, i);
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kXlaneThreads) void xlane_service_kernel(SrvParams p) {
+  __shared__ uint32_t s_req[5];
+  __shared__ uint4 stage[kXlaneStagePieces];
+  const uint32_t slot = blockIdx.x / kSrvGroup, part = blockIdx.x % kSrvGroup;
+  SrvSlot *sl = p.slots + slot;
+  const uint64_t t0 = wall_clock64();
+  // the last request of this slot the host saw done (it posts the next one only then)
+  uint32_t last = 0;
+  if (threadIdx.x == 0u) last = __hip_atomic_load(&sl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    if (threadIdx.x == 0u) {
+      uint32_t go = 0u;
+      uint4 h = make_uint4(last, 0u, 0u, 0u);
+      for (uint32_t i = 0;; ++i) {
+        h = srv_poll(sl);
+        if (h.x != last) {
+          go = 1u;
+          break;
+        }
+        if ((i & 15u) == 0u && (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u ||
+                                wall_clock64() - t0 > p.lease_ticks))
+          break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_req[0] = go;
+      s_req[1] = h.x;
+      s_req[2] = h.y;
+      s_req[3] = h.z;
+      s_req[4] = h.w;
+    }
+    __syncthreads();
+    const uint32_t go = s_req[0], seq = s_req[1], op = s_req[2], n = s_req[3], G = s_req[4];
+    __syncthreads();  // (s_req is rewritten by the next poll)
+    if (!go) return;  // (workgroup-uniform: stop or lease)
+    const bool stamp = p.stamp && part == 0u && threadIdx.x == 0u;
+    if (stamp) sl->stamp[0] = wall_clock64();
+    // the request's bytes (descriptors, packets) were written by the host before seq:
+    // drop whatever the caches hold of earlier requests at those addresses
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (stamp) sl->stamp[1] = wall_clock64();
+    const uint32_t lane = part * kXlaneThreads + threadIdx.x;
+    if (n <= kSrvDescs && n * G <= kSrvLanes) {  // (the host never posts more)
+      switch ((op ? 128u : 0u) | G) {
+        case 128u | 64u: srv_packets<true, 64>(sl, lane, n, p, stage); break;
+        case 128u | 32u: srv_packets<true, 32>(sl, lane, n, p, stage); break;
+        case 128u | 16u: srv_packets<true, 16>(sl, lane, n, p, stage); break;
+        case 128u | 8u: srv_packets<true, 8>(sl, lane, n, p, stage); break;
+        case 64u: srv_packets<false, 64>(sl, lane, n, p, stage); break;
+        case 32u: srv_packets<false, 32>(sl, lane, n, p, stage); break;
+        case 16u: srv_packets<false, 16>(sl, lane, n, p, stage); break;
+        case 8u: srv_packets<false, 8>(sl, lane, n, p, stage); break;
+        default: break;
+      }
+    }
+    // arrival: this workgroup's outputs and statuses acknowledged, one system-scope
+    // release each; the last of the slot's workgroups publishes seq (grid_done's shape)
+    if (stamp) sl->stamp[2] = wall_clock64();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (stamp) sl->stamp[3] = wall_clock64();
+    if (threadIdx.x == 0u) {
+      uint32_t *cnt = p.d_count + (threadIdx.x + slot * 32u);
+      const uint32_t prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (prev == kSrvGroup - 1u) {
+        if (p.stamp) sl->stamp[4] = wall_clock64();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sl->done + threadIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      last = seq;
+    }
+  }
 }
 
 template __global__ void aead_xlane_kernel<true, 64>(DescParams);

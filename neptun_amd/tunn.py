@@ -47,7 +47,8 @@ class Phases(ctypes.Structure):
 class EngineInfo(ctypes.Structure):
     """wg_engine_info: what a shared engine holds."""
     _fields_ = [(f, ctypes.c_uint32) for f in ("tunns", "lanes", "max_lanes", "pool_threads", "streams",
-                                               "combined")]
+                                               "combined")] + [(f, ctypes.c_uint64) for f in
+                                                               ("served", "service_launches")]
 
 
 def _bind(L):

@@ -25,6 +25,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C ABI)")
 
 
+def pytest_unconfigure(config):
+    # a process that does not exit within a minute of the session's end dumps every
+    # thread's Python stack and exits (a hang at interpreter or runtime teardown)
+    import faulthandler
+    faulthandler.dump_traceback_later(60, exit=True)
+
+
 @pytest.fixture(scope="session")
 def torch_cuda():
     import torch

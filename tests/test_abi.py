@@ -82,8 +82,11 @@ def test_engine_entry_points_fail_loudly_on_null():
         assert b"_multi: null" in lib.wg_gpu_last_error()
     text = open(neptun_amd.HEADER_PATH.replace("neptun_gpu.h", "neptun_tunn.h")).read()
     body = re.search(r"typedef struct wg_engine_info \{(.*?)\}", text, re.S).group(1)
-    names = [n.strip() for decl in re.findall(r"uint32_t([^;]*);", body) for n in decl.split(",")]
-    assert names == [f for f, _ in EngineInfo._fields_] and ctypes.sizeof(EngineInfo) == 4 * len(names)
+    fields = [(n.strip(), int(w) // 8) for w, decl in re.findall(r"uint(32|64)_t([^;]*);", body)
+              for n in decl.split(",")]
+    assert [n for n, _ in fields] == [f for f, _ in EngineInfo._fields_]
+    assert [ctypes.sizeof(t) for _, t in EngineInfo._fields_] == [w for _, w in fields]
+    assert ctypes.sizeof(EngineInfo) == 4 * 6 + 8 * 2  # (the two 64-bit counters 8-aligned after six words)
 
 
 def test_library_is_gfx950_code_object():

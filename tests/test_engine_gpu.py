@@ -330,6 +330,7 @@ def test_concurrent_small_calls_combine_into_shared_launches(big_ctx, monkeypatc
 
     from test_tunn_gpu import Arena
     monkeypatch.setenv("WG_TUNN_FLAG", "64")
+    monkeypatch.setenv("WG_TUNN_SRV", "0")  # (the resident service would take these calls)
     monkeypatch.setenv("WG_COMBINE", "1")  # (off by default: DESIGN 8)
     monkeypatch.setenv("WG_COMBINE_DEPTH", depth)
     rng = random.Random(808 + int(depth))
@@ -393,6 +394,118 @@ def test_concurrent_small_calls_combine_into_shared_launches(big_ctx, monkeypatc
     assert eng.info()["combined"] > 0, "no two concurrent small calls shared a launch"
     for _, tg, _ in pairs:
         tg.close()
+    eng.close()
+
+
+def _small_call_traffic(big_ctx, pairs, k, seed, calls, rekey_at=None, pause_at=None):
+    """calls of 1-64 packets on pair k (staged and registered, encapsulate and decapsulate
+    with damaged traffic), each checked against the pair's sequential model; at call
+    rekey_at the pair installs a new session (new keys in the context's table), at call
+    pause_at the thread sleeps past the service's lease"""
+    import time
+
+    from test_tunn_gpu import Arena
+    r = random.Random(seed)
+    tm, tg, ses = pairs[k]
+    ctr_state = {}
+    for call in range(calls):
+        if call == rekey_at:
+            local = (ses[0][0] + 4) & 0xFFFFFFFF
+            rk, sk, peer = r.randbytes(32), r.randbytes(32), r.getrandbits(32)
+            for t in (tm, tg):
+                t.set_time(100 + call)
+                t.install_session(local, peer, rk, sk, True)
+            ses[:] = [(local, peer, rk, sk)]
+            ctr_state.clear()
+        if call == pause_at:
+            time.sleep(0.06)
+        n = r.choice([1, 16, 50, 50, 64])
+        reg = call % 3 == 1
+        if call % 2 == 0:
+            srcs = [ipv4(r, r.choice([64, 1350, r.randrange(20, 1500)])) for _ in range(n)]
+            caps = [len(x) + 32 for x in srcs]
+            dm = [bytearray(b"\xee" * c) for c in caps]
+            res_m = [tm.encapsulate(x, d) for x, d in zip(srcs, dm)]
+            if reg:
+                a, b = Arena(srcs, [0] * n), Arena([b""] * n, caps)
+                for x in (a, b):
+                    big_ctx.register_host(*x.window())
+                res_g = tg.encapsulate_ptrs(a.ptrs, a.lens, b.ptrs, np.array(caps, np.uint32))
+                dg = [bytearray(b.get(j, caps[j])) for j in range(n)]
+                for x in (a, b):
+                    big_ctx.unregister_host(x.window()[0])
+            else:
+                dg = [bytearray(b"\xee" * c) for c in caps]
+                res_g = tg.encapsulate_batch(srcs, dg)
+            check_same(res_g, res_m, dg, dm, f"pair {k} encap {call}")
+        else:
+            dgs = datagrams(r, ses, n, ctr_state)
+            caps = [max(len(d) - 16, 1) for d in dgs]
+            dm = [bytearray(b"\xee" * c) for c in caps]
+            res_m = [tm.decapsulate(d, x) for d, x in zip(dgs, dm)]
+            if reg:
+                a, b = Arena(dgs, [0] * n), Arena([b""] * n, caps)
+                for x in (a, b):
+                    big_ctx.register_host(*x.window())
+                res_g = tg.decapsulate_ptrs(a.ptrs, a.lens, b.ptrs, np.array(caps, np.uint32))
+                dg = [bytearray(b.get(j, caps[j])) for j in range(n)]
+                for x in (a, b):
+                    big_ctx.unregister_host(x.window()[0])
+            else:
+                dg = [bytearray(b"\xee" * c) for c in caps]
+                res_g = tg.decapsulate_batch(dgs, dg)
+            check_same(res_g, res_m, dg, dm, f"pair {k} decap {call}")
+
+
+def test_resident_service_serves_concurrent_small_calls(big_ctx, monkeypatch):
+    """The engine's resident kernel (wg_xlane.hip xlane_service_kernel) takes the small
+    calls of 8 concurrent threads, each on its own peer's Tunn: every call equals its
+    model, across lease renewals (a 20 ms lease here), a key-table update in the middle
+    (one peer installs a new session: the kernel is relaunched before the next post,
+    so no call reads old keys), and a pause past the lease (the next call relaunches)."""
+    from neptun_amd import Engine
+    monkeypatch.setenv("WG_TUNN_SRV_LEASE_US", "20000")
+    rng = random.Random(909)
+    eng = Engine(big_ctx)
+    pairs = peers_with_sessions(rng, eng, 8, first=700, sessions=(1,))
+    errors = []
+    seeds = [rng.getrandbits(32) for _ in pairs]
+
+    def work(k):
+        try:
+            _small_call_traffic(big_ctx, pairs, k, seeds[k], 120, rekey_at=60 if k == 3 else None,
+                                pause_at=90 if k == 5 else None)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(len(pairs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[0]
+    check_state(pairs)
+    info = eng.info()
+    # (every call with packets for the GPU is one chunk; a batch whose every datagram
+    # fails its header checks sends none)
+    assert info["served"] >= 0.9 * 8 * 120, info
+    assert info["service_launches"] >= 2, info
+    for _, tg, _ in pairs:
+        tg.close()
+    eng.close()
+
+
+def test_resident_service_off_matches_too(big_ctx, monkeypatch):
+    """WG_TUNN_SRV=0: the same traffic through one launch per call; nothing served."""
+    from neptun_amd import Engine
+    monkeypatch.setenv("WG_TUNN_SRV", "0")
+    rng = random.Random(910)
+    eng = Engine(big_ctx)
+    pairs = peers_with_sessions(rng, eng, 1, first=720, sessions=(1,))
+    _small_call_traffic(big_ctx, pairs, 0, 77, 60, rekey_at=30)
+    check_state(pairs)
+    assert eng.info()["served"] == 0
+    pairs[0][1].close()
     eng.close()
 
 

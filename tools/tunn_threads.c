@@ -149,20 +149,24 @@ int main(int argc, char **argv) {
   }
   const double calls_all = (double)T * calls;
   uint32_t combined = 0;
+  unsigned long long served = 0, srv_launches = 0;
 #ifdef TT_ENGINES
   {
     wg_engine_info info;
-    if (!getenv("GW_PRIVATE_ENGINES") && wg_engine_get_info(wg_tunn_engine(jobs[0].a), &info) == 0)
+    if (!getenv("GW_PRIVATE_ENGINES") && wg_engine_get_info(wg_tunn_engine(jobs[0].a), &info) == 0) {
       combined = info.combined;
+      served = info.served;
+      srv_launches = info.service_launches;
+    }
   }
 #endif
   printf("{\"threads\": %u, \"batch\": %u, \"P\": %u, \"calls_per_thread\": %u, \"registered\": %d, "
-         "\"combined_calls\": %u, \"seconds\": %.4f, "
+         "\"combined_calls\": %u, \"served_calls\": %llu, \"service_launches\": %llu, \"seconds\": %.4f, "
          "\"roundtrip_gbps\": %.2f, \"encap_ms_per_call\": %.3f, \"decap_ms_per_call\": %.3f, "
          "\"encap_us\": {\"checks\": %.1f, \"pack\": %.1f, \"submit\": %.1f, \"wait\": %.1f, \"copy_out\": %.1f}, "
          "\"decap_us\": {\"checks\": %.1f, \"pack\": %.1f, \"submit\": %.1f, \"wait\": %.1f, \"decide\": %.1f, "
          "\"copy_out\": %.1f}}\n",
-         T, B, P, calls, getenv("TT_REGISTER") && atoi(getenv("TT_REGISTER")), combined, secs, calls_all * B * P * 8.0 / secs / 1e9, te / calls_all * 1e3, td / calls_all * 1e3,
+         T, B, P, calls, getenv("TT_REGISTER") && atoi(getenv("TT_REGISTER")), combined, served, srv_launches, secs, calls_all * B * P * 8.0 / secs / 1e9, te / calls_all * 1e3, td / calls_all * 1e3,
          sa.checks_us / calls_all, sa.pack_us / calls_all, sa.submit_us / calls_all, sa.wait_us / calls_all,
          sa.copy_out_us / calls_all, sb.checks_us / calls_all, sb.pack_us / calls_all, sb.submit_us / calls_all,
          sb.wait_us / calls_all, sb.decide_us / calls_all, sb.copy_out_us / calls_all);
