@@ -99,10 +99,11 @@ int wg_tunn_create_on(wg_engine *e, uint32_t first_slot, wg_tunn **out);
  * call (WG_COMBINE=1, off by default: one latency-form launch for the engine's
  * concurrent small calls of one direction, at most WG_COMBINE_DEPTH such launches in
  * flight, default 2); how many small calls' chunks were served by the engine's
- * resident kernel instead of a launch of their own (WG_TUNN_SRV, on by default:
- * chunks of up to 64 packets whose completion is the kernel's word) and how many
- * times that kernel was launched (a lease of 1 s, renewed by the next call; a new
- * launch after a key-table update) */
+ * resident kernel instead of a launch of their own (WG_TUNN_SRV=1, off by default:
+ * chunks of up to 64 packets whose completion is the kernel's word; while it runs,
+ * hipDeviceSynchronize and hipFree in the process wait for it to go idle) and how
+ * many times that kernel was launched (a lease of 1 s, renewed by the next call; a
+ * new launch after a key-table update or an idle stop) */
 typedef struct wg_engine_info {
   uint32_t tunns, lanes, max_lanes, pool_threads, streams;
   uint32_t combined;

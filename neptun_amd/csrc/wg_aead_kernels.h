@@ -149,7 +149,7 @@ template <bool kSeal, uint32_t G> __global__ void aead_xlane_strided_kernel(Stri
 // latency-form kernels do (statuses into st), and the last of them to finish stores
 // seq to `done`.  A workgroup leaves when the host sets *stop or its lease runs out
 // (s_memrealtime), so the grid always drains.
-constexpr uint32_t kSrvSlots = 8, kSrvGroup = 4, kSrvDescs = 64;
+constexpr uint32_t kSrvSlots = 8, kSrvGroup = 8, kSrvDescs = 64;
 constexpr uint32_t kSrvLanes = kSrvGroup * kXlaneThreads;
 struct alignas(128) SrvSlot {
   uint32_t seq, op, n, G;  // op: 1 seal, 0 open; seq written last

@@ -1459,7 +1459,12 @@ hipError_t comb_wait(Staging &S, uint32_t m) {
 // to hipDeviceSynchronize, which therefore waits for the engine to go idle that long.
 // The watchdog and a poster meet Dekker-style (live / inflight, sequentially
 // consistent): a posted call's kernel is never stopped under it.
-// WG_TUNN_SRV=0 turns it off (the calls launch as before).
+// Measured against the launches (profiles/r06n, r06o, r06r, r06s: 50 x 1350 B, 1 and 8
+// threads, staged and registered): no launch, but the same ~12-15 us of PCIe-bound
+// processing per request (device stamps), so 8 callers run 55-60 Gbit/s either way and
+// one caller +0-13 %; meanwhile a resident kernel makes hipDeviceSynchronize and hipFree
+// anywhere in the process wait for the engine's idle stop.  Off by default: WG_TUNN_SRV=1
+// turns it on.
 constexpr int64_t kSrvLeaseUs = 1000000, kSrvMarginUs = 5000;
 int64_t srv_idle_us() {  // (read per watchdog round)
   const char *e = std::getenv("WG_TUNN_SRV_IDLE_US");
@@ -1497,9 +1502,9 @@ struct Service {
   int64_t post_us[wg::kSrvSlots] = {};
 };
 
-bool srv_on() {  // (read per call)
+bool srv_on() {  // (read per call; off by default)
   const char *e = std::getenv("WG_TUNN_SRV");
-  return !e || std::atoi(e) != 0;
+  return e && std::atoi(e) != 0;
 }
 int64_t steady_us() {
   return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -1510,15 +1515,28 @@ int64_t steady_us() {
 // HIP runtime's own exit handlers, so it runs before them)
 std::mutex g_srv_mu;
 std::vector<Service *> g_srvs;
+void srv_stamp_dump(Service *V);
 void srv_atexit() {
   std::lock_guard<std::mutex> lk(g_srv_mu);
   bool any = false;
-  for (Service *V : g_srvs)
-    if (V->live.load()) {
-      __atomic_store_n(V->stop, 1u, __ATOMIC_RELEASE);
-      any = true;
-    }
-  if (any) std::this_thread::sleep_for(std::chrono::milliseconds(2));  // (the workgroups poll every ~2 us)
+  for (Service *V : g_srvs) {
+    srv_stamp_dump(V);
+    V->st_n = 0;
+  }
+  for (Service *V : g_srvs) {  // (stopped by the watchdog and still draining counts too)
+    __atomic_store_n(V->stop, 1u, __ATOMIC_RELEASE);
+    V->live.store(false);
+    any = true;
+  }
+  // the grids drained before the runtime tears the queues down (the workgroups see
+  // *stop within a poll, ~2 us; bounded at 100 ms)
+  const int64_t t0 = steady_us();
+  while (any && steady_us() - t0 < 100000) {
+    any = false;
+    for (Service *V : g_srvs)
+      if (V->stream && hipStreamQuery(V->stream) == hipErrorNotReady) any = true;
+    if (any) std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
 }
 
 // stop the kernel and wait (bounded) for its grid to drain; false: it did not

@@ -74,6 +74,18 @@ __device__ __forceinline__ bool xok(uint64_t a, uint32_t bytes, uint64_t lo, uin
 __device__ __forceinline__ uint4 xld16(const uint8_t *p, const XBounds &B) {
   return xok((uint64_t)p, 16u, B.in_lo, B.in_hi, B) ? ld16(p) : make_uint4(0, 0, 0, 0);
 }
+// a system-coherent 16-byte load (sc0 sc1: past the caches to memory): the resident
+// service's host-memory reads (kSys), made without a launch's cache invalidate
+typedef unsigned int xl_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16_sys(const uint8_t *p) {
+  // (a volatile global load: sc0 sc1 on gfx950, and the compiler places its waits)
+  const xl_u32x4 v =
+      *reinterpret_cast<const volatile __attribute__((address_space(1))) xl_u32x4 *>(reinterpret_cast<uint64_t>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 xld16_sys(const uint8_t *p, const XBounds &B) {
+  return xok((uint64_t)p, 16u, B.in_lo, B.in_hi, B) ? ld16_sys(p) : make_uint4(0, 0, 0, 0);
+}
 __device__ __forceinline__ void xst16(uint8_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d, const XBounds &B) {
   if (xok((uint64_t)p, 16u, B.out_lo, B.out_hi, B)) st16(p, a, b, c, d);
 }
@@ -129,7 +141,7 @@ __device__ __forceinline__ void lds_wave_sync() { asm volatile("s_waitcnt lgkmcn
 // packet's offsets OR-ed (misaligned -> WG_STATUS_MISALIGNED); st: its status (or null).
 // kStage: through the group's LDS region gb (stage_cap<G>() pieces; the caller checks
 // that the packet's (P + 31) / 16 pieces fit).
-template <bool kSeal, uint32_t G, bool kStage = false>
+template <bool kSeal, uint32_t G, bool kStage = false, bool kSys = false>
 __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uint8_t *dst, uint32_t len,
                                              uint32_t slot, uint64_t counter, uint64_t align, int32_t *st,
                                              const uint8_t *keys, const uint32_t *key_index, uint32_t key_slots,
@@ -182,7 +194,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
 #pragma unroll
     for (uint32_t k = 0; k < kBatch; ++k) {
       const uint32_t p = l + k * G;
-      sv[k] = p < np_in ? xld16(in + 16u * p, B) : make_uint4(0, 0, 0, 0);
+      sv[k] = p < np_in ? (kSys ? xld16_sys(in + 16u * p, B) : xld16(in + 16u * p, B)) : make_uint4(0, 0, 0, 0);
     }
   } else {
     if (any) load_block(b0, x);
@@ -198,7 +210,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       n1 = (uint32_t)counter;
       n2 = (uint32_t)(counter >> 32);
     } else {
-      const uint4 h = xld16(src, B);  // header: type, receiver_idx, counter (mod.rs:170-180)
+      const uint4 h = kSys ? xld16_sys(src, B) : xld16(src, B);  // header: type, receiver_idx, counter (mod.rs:170-180)
       if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
       else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
       n1 = h.z;
@@ -218,7 +230,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
 #pragma unroll
       for (uint32_t k = 0; k < kBatch; ++k) {
         const uint32_t p = p0 + l + k * G;
-        sv[k] = p < np_in ? xld16(in + 16u * p, B) : make_uint4(0, 0, 0, 0);
+        sv[k] = p < np_in ? (kSys ? xld16_sys(in + 16u * p, B) : xld16(in + 16u * p, B)) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (uint32_t k = 0; k < kBatch; ++k) {
@@ -489,15 +501,21 @@ __device__ __forceinline__ void srv_packets(SrvSlot *sl, uint32_t lane, uint32_t
   const uint32_t l = lane & (G - 1u);
   uint4 *gb = stage + ((lane % kXlaneThreads) / G) * stage_cap<G>();
   for (uint32_t i = lane / G; i < n; i += kSrvLanes / G) {  // (group-uniform)
-    const wg_packet_desc d = sl->d[i];
-    const uint8_t *src = reinterpret_cast<const uint8_t *>(d.src_off);
-    uint8_t *dst = reinterpret_cast<uint8_t *>(d.dst_off);
-    if (stage_fits<kSeal, G>(d.len))
-      xlane_packet<kSeal, G, true>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, sl->st + i,
-                                   p.keys, p.key_index, p.key_slots, i, gb);
-    else
-      xlane_packet<kSeal, G>(l, src, dst, d.len, d.key_slot, d.counter, d.src_off | d.dst_off, sl->st + i, p.keys,
-                             p.key_index, p.key_slots, i);
+    // the descriptor, past the caches (the host rewrote the slot since the last request)
+    const uint4 d0 = ld16_sys(reinterpret_cast<const uint8_t *>(&sl->d[i]));
+    const uint4 d1 = ld16_sys(reinterpret_cast<const uint8_t *>(&sl->d[i]) + 16u);
+    const uint64_t so = (uint64_t)d0.x | ((uint64_t)d0.y << 32), dn = (uint64_t)d0.z | ((uint64_t)d0.w << 32);
+    const uint64_t ctr = (uint64_t)d1.x | ((uint64_t)d1.y << 32);
+    const uint32_t len = d1.z, kslot = d1.w;
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(so);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(dn);
+    if (stage_fits<kSeal, G>(len)) {
+      xlane_packet<kSeal, G, true, true>(l, src, dst, len, kslot, ctr, so | dn, sl->st + i, p.keys, p.key_index,
+                                         p.key_slots, i, gb);
+    } else {  // (its plain loads: first drop what the caches hold of earlier requests)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      xlane_packet<kSeal, G>(l, src, dst, len, kslot, ctr, so | dn, sl->st + i, p.keys, p.key_index, p.key_slots, i);
+    }
   }
 }
 
@@ -539,9 +557,9 @@ __global__ __launch_bounds__(kXlaneThreads) void xlane_service_kernel(SrvParams 
     if (!go) return;  // (workgroup-uniform: stop or lease)
     const bool stamp = p.stamp && part == 0u && threadIdx.x == 0u;
     if (stamp) sl->stamp[0] = wall_clock64();
-    // the request's bytes (descriptors, packets) were written by the host before seq:
-    // drop whatever the caches hold of earlier requests at those addresses
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    // (the request's bytes -- descriptors, packets -- are read past the caches; no
+    // per-request invalidate: with a slot's workgroups on many CUs it cost 3-4 us a
+    // request under load, profiles/r06r)
     if (stamp) sl->stamp[1] = wall_clock64();
     const uint32_t lane = part * kXlaneThreads + threadIdx.x;
     if (n <= kSrvDescs && n * G <= kSrvLanes) {  // (the host never posts more)

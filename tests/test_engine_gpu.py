@@ -464,6 +464,7 @@ def test_resident_service_serves_concurrent_small_calls(big_ctx, monkeypatch):
     (one peer installs a new session: the kernel is relaunched before the next post,
     so no call reads old keys), and a pause past the lease (the next call relaunches)."""
     from neptun_amd import Engine
+    monkeypatch.setenv("WG_TUNN_SRV", "1")  # (off by default)
     monkeypatch.setenv("WG_TUNN_SRV_LEASE_US", "20000")
     rng = random.Random(909)
     eng = Engine(big_ctx)
@@ -496,7 +497,8 @@ def test_resident_service_serves_concurrent_small_calls(big_ctx, monkeypatch):
 
 
 def test_resident_service_off_matches_too(big_ctx, monkeypatch):
-    """WG_TUNN_SRV=0: the same traffic through one launch per call; nothing served."""
+    """WG_TUNN_SRV=0 (the default): the same traffic through one launch per call (the
+    staged latency form); nothing served."""
     from neptun_amd import Engine
     monkeypatch.setenv("WG_TUNN_SRV", "0")
     rng = random.Random(910)

@@ -268,15 +268,19 @@ def test_xlane_strided_matches_throughput_form_and_oracle(torch_cuda, xl, G, n, 
         assert (b[i * S + P:(i + 1) * S] == 0x5A).all(), i
 
 
-def test_tunn_small_calls_on_the_checked_build(gpu_checked, monkeypatch):
+@pytest.mark.parametrize("srv", ["0", "1"])
+def test_tunn_small_calls_on_the_checked_build(gpu_checked, monkeypatch, srv):
     """The Tunn's small calls -- the latency form with descriptors in the kernel
-    arguments, the completion word, registered datagrams read and registered dsts
-    written in place on speculated replay decisions -- on the checked build: every
-    call equals the sequential model and no access leaves its packet."""
+    arguments (LDS-staged: packets in host memory), the completion word, registered
+    datagrams read and registered dsts written in place on speculated replay decisions
+    -- and, srv = 1, the same calls posted to the engine's resident kernel, on the
+    checked build: every call equals the sequential model and no access leaves its
+    packet."""
     import random
 
     from test_tunn_gpu import Arena, check_same, datagrams, ipv4, make_pair
     monkeypatch.setenv("WG_TUNN_FLAG", "64")
+    monkeypatch.setenv("WG_TUNN_SRV", srv)
     ctx = gpu_checked
     ctx.xlane_check(reset=True)
     rng = random.Random(606)

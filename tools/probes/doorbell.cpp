@@ -14,7 +14,9 @@
 //              kernel's hardware queue would wait for the lease)
 // for the resident kernel on a CU-masked stream (every CU in the mask: the runtime gives
 // such a stream a hardware queue of its own) and, as the control, on an ordinary
-// stream.  One JSON object per variant.  (A mask of CUs 0-31 hung: on gfx950 the
+// stream.  One JSON object per variant.  "vram" (run alone): the slots in fine-grained
+// device memory, written by the host through its mapping of the BAR (the kernel polls
+// HBM instead of reading over PCIe).  (A mask of CUs 0-31 hung: on gfx950 the
 // workgroups are dealt round robin to the 8 XCDs, and those of an XCD without a CU in
 // the mask never start -- a mask must cover every XCD.)
 //   hipcc --offload-arch=gfx950 -O2 doorbell.cpp -o doorbell -lpthread
@@ -98,11 +100,16 @@ static bool call(Slot *s, uint32_t seq) {  // post and spin; false after 100 ms
   }
 }
 
-static int variant(const char *name, bool masked, int cus, int total_cus) {
+static int variant(const char *name, bool masked, int cus, int total_cus, bool vram = false) {
   constexpr int W = 16;
   Slot *slots = nullptr;
   uint32_t *stop = nullptr;
-  CHECK(hipHostMalloc((void **)&slots, sizeof(Slot) * W, hipHostMallocCoherent));
+  if (vram) {  // (fine-grained device memory the host writes through its BAR mapping)
+    CHECK(hipExtMallocWithFlags((void **)&slots, sizeof(Slot) * W, hipDeviceMallocFinegrained));
+    fprintf(stderr, "%s: device slots at %p, host write test\n", name, (void *)slots);
+  } else {
+    CHECK(hipHostMalloc((void **)&slots, sizeof(Slot) * W, hipHostMallocCoherent));
+  }
   CHECK(hipHostMalloc((void **)&stop, 64, hipHostMallocCoherent));
   for (int i = 0; i < W; ++i) slots[i].seq = slots[i].done = 0;
   *stop = 0;
@@ -119,6 +126,22 @@ static int variant(const char *name, bool masked, int cus, int total_cus) {
   hipLaunchKernelGGL(resident_kernel, dim3(W), dim3(256), 0, rs, slots, stop, lease);
   CHECK(hipGetLastError());
   printf("{\"variant\": \"%s\", \"masked_cus\": %d", name, masked ? cus : 0);
+  if (vram) {  // host stores of a request's 2 KiB of descriptors into the mapped VRAM
+    static uint8_t src[2048];
+    for (int i = 0; i < 2048; ++i) src[i] = (uint8_t)i;
+    uint8_t *dstp = nullptr;
+    CHECK(hipExtMallocWithFlags((void **)&dstp, 2048, hipDeviceMallocFinegrained));
+    std::vector<double> t;
+    for (int r = 0; r < 1100; ++r) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < 2048; i += 16) __builtin_memcpy(dstp + i, src + i, 16);
+      __builtin_ia32_sfence();
+      if (r >= 100) t.push_back(us_since(t0));
+    }
+    std::sort(t.begin(), t.end());
+    printf(", \"host_store_2k_us\": %.3f", t[t.size() / 2]);
+    CHECK(hipFree(dstp));
+  }
   fflush(stdout);
   fprintf(stderr, "%s: launched\n", name);
   // first answer (the kernel's start)
@@ -203,7 +226,8 @@ static int variant(const char *name, bool masked, int cus, int total_cus) {
   printf(", \"stop_us\": %.1f}\n", us_since(ts));
   fflush(stdout);
   CHECK(hipStreamDestroy(rs));
-  CHECK(hipHostFree(slots));
+  if (vram) CHECK(hipFree(slots));
+  else CHECK(hipHostFree(slots));
   CHECK(hipHostFree(stop));
   return 0;
 }
@@ -215,5 +239,6 @@ int main(int argc, char **argv) {
   auto want = [&](const char *v) { return !only || std::string(only) == v; };
   if (want("masked_all") && variant("masked_all", true, cus, cus)) return 1;
   if (want("plain_stream") && variant("plain_stream", false, 0, cus)) return 1;
+  if (only && std::string(only) == "vram" && variant("vram", false, 0, cus, true)) return 1;
   return 0;
 }
