@@ -391,7 +391,9 @@ def test_concurrent_small_calls_combine_into_shared_launches(big_ctx, monkeypatc
         t.join()
     assert not errors, errors[0]
     check_state(pairs)
-    assert eng.info()["combined"] > 0, "no two concurrent small calls shared a launch"
+    if depth == "1":  # (one launch in flight: calls arriving meanwhile must share the next;
+        # with two, whether any call waits for a slot depends on the kernels' speed)
+        assert eng.info()["combined"] > 0, "no two concurrent small calls shared a launch"
     for _, tg, _ in pairs:
         tg.close()
     eng.close()
