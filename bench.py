@@ -35,7 +35,10 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    # (100 untimed steps, ~0.15 s: the package power controller clamps the clock for ~25
+    # steps after a cold start and then settles; the timed steps are the
+    # steady state a loaded gateway runs at)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
     ap.add_argument("--packets", type=int, default=0,
                     help="config 2: packets per GPU (0 = 1M at 1350 B; other --size values keep the "
