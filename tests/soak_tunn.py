@@ -4,7 +4,8 @@ sequential Tunn model -- TEST INFRASTRUCTURE (imports oracle/, like tests/).
 
 Each round draws a batch size (1 .. 40,000, skewed small; the early start takes >= 16,384),
 a slot size, an output mode (WG_TUNN_DMA_OUT direct / scatter / default), chunk size,
-stream form and completion-word policy (WG_TUNN_FLAG), encapsulates a batch of mostly-1350-byte packets from registered slots and
+stream form, completion-word policy (WG_TUNN_FLAG) and small-call path (WG_TUNN_SRV),
+encapsulates a batch of mostly-1350-byte packets from registered slots and
 decapsulates the peer's traffic with replays, too-old counters, tampered tags, forged-
 then-real counters, wrong indices and keepalives -- with destination slots on 128-byte
 lines, 16 bytes past one, or 8 bytes off 16-byte alignment (each output mode's case) or one dst
@@ -52,7 +53,9 @@ def main():
                "WG_TUNN_SETS": rng.choice(["", "3"]),
                # the kernel's completion word: default (chunks <= 128 packets), never,
                # or every zero-copy latency-form chunk (grids of up to 4096 packets)
-               "WG_TUNN_FLAG": rng.choice(["", "0", "4096"])}
+               "WG_TUNN_FLAG": rng.choice(["", "0", "4096"]),
+               # small calls posted to the engine's resident kernel (round 6, off by default)
+               "WG_TUNN_SRV": rng.choice(["", "1"])}
         for k, v in env.items():
             if v:
                 os.environ[k] = v

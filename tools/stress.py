@@ -13,7 +13,7 @@ unordered descriptor launch draws its form at random (round 5): the throughput k
 the default selection, or the latency form with a forced group of 2 .. 64 lanes per
 packet (wg_xlane.hip) -- and so does the descriptor open.  Round 6: long packets (up to
 8192 B) too, and the strided seal draws its split (wg_gpu_ctx_set_split: the default
-choice, unsplit, or K = 2 / 4 / 8 parts per wave with the finish kernel).  A one-in-a-million
+choice, unsplit, or K = 2 ... 8 parts per wave with the finish kernel).  A one-in-a-million
 corruption in any form shows up as a mismatch between forms that share no kernel.
 Prints one JSON summary line.
 
@@ -99,7 +99,7 @@ def main():
             w = torch.full((n * S + 64,), 0xA5, dtype=torch.uint8, device=dev)
             st = torch.full((n,), -1, dtype=torch.int32, device=dev)
             if form == "strided":
-                K = int(rng.choice([-1, 1, 2, 4, 8]))
+                K = int(rng.choice([-1, 1, 2, 3, 4, 5, 6, 7, 8]))
                 ctx.set_split(K)
                 form = f"strided-split{K}"
                 ctx.seal_strided(n, int(sizes[0]), 0, ctr0, pt, S, w, S, st)
@@ -135,7 +135,7 @@ def main():
             ctx.open_batch(torch.from_numpy(d2.view(np.uint8)).to(dev), n, outs[0], back, st2)
             ctx.set_xlane_lanes(0)
         else:
-            K = int(rng.choice([-1, 1, 2, 4, 8]))
+            K = int(rng.choice([-1, 1, 2, 3, 4, 5, 6, 7, 8]))
             ctx.set_split(K)
             tag = f"open-strided-split{K}"
             stats["forms"][tag] = stats["forms"].get(tag, 0) + 1
