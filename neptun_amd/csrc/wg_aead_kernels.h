@@ -160,9 +160,10 @@ struct alignas(128) SrvSlot {
   uint32_t pad1[31];
   // (SrvParams::stamp) s_memrealtime of the request's phases: seen, acquired, the
   // packets done, their stores acknowledged (workgroup 0 of the slot), published (the
-  // last workgroup)
-  uint64_t stamp[5];
-  uint64_t pad2[11];
+  // last workgroup); then inside packet 0 (its group's lane 0): descriptor read, input
+  // staged, tag formed, output stores issued
+  uint64_t stamp[9];
+  uint64_t pad2[7];
 };
 struct SrvParams {
   SrvSlot *slots;

@@ -1497,7 +1497,8 @@ struct Service {
   // the host's post-to-seen time, summed; written to path when the service ends
   const char *stamp_path = nullptr;
   std::mutex stamp_mu;
-  double st_sum[6] = {};  // us: seen->acquired, ->packets, ->acked, ->published, device total, host total
+  double st_sum[10] = {};  // us: seen->acquired, ->packets, ->acked, ->published, device total, host total;
+                           // packet 0: acquired->descriptor, ->staged, ->tag, ->stores issued
   uint64_t st_n = 0;
   int64_t post_us[wg::kSrvSlots] = {};
 };
@@ -1576,9 +1577,11 @@ void srv_stamp_dump(Service *V) {
     std::fprintf(f,
                  "{\"requests\": %llu, \"us\": {\"seen_to_acquired\": %.2f, \"acquired_to_packets\": %.2f, "
                  "\"packets_to_acked\": %.2f, \"acked_to_published\": %.2f, \"device_seen_to_published\": %.2f, "
-                 "\"host_post_to_seen_done\": %.2f}}\n",
+                 "\"host_post_to_seen_done\": %.2f, \"pkt0_descriptor\": %.2f, \"pkt0_staged\": %.2f, "
+                 "\"pkt0_keystream_mac\": %.2f, \"pkt0_store_issue\": %.2f}}\n",
                  (unsigned long long)V->st_n, V->st_sum[0] / n, V->st_sum[1] / n, V->st_sum[2] / n, V->st_sum[3] / n,
-                 V->st_sum[4] / n, V->st_sum[5] / n);
+                 V->st_sum[4] / n, V->st_sum[5] / n, V->st_sum[6] / n, V->st_sum[7] / n, V->st_sum[8] / n,
+                 V->st_sum[9] / n);
     std::fclose(f);
   }
 }
@@ -1779,6 +1782,8 @@ hipError_t srv_wait(Staging &S, uint32_t m) {
       for (int k = 0; k < 4; ++k) V.st_sum[k] += (double)(t[k + 1] - t[k]) / 100.0;
       V.st_sum[4] += (double)(t[4] - t[0]) / 100.0;
       V.st_sum[5] += host;
+      V.st_sum[6] += (double)(t[5] - t[1]) / 100.0;
+      for (int k = 0; k < 3; ++k) V.st_sum[7 + k] += (double)(t[6 + k] - t[5 + k]) / 100.0;
       ++V.st_n;
     }
   } else {

@@ -145,7 +145,9 @@ template <bool kSeal, uint32_t G, bool kStage = false, bool kSys = false>
 __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uint8_t *dst, uint32_t len,
                                              uint32_t slot, uint64_t counter, uint64_t align, int32_t *st,
                                              const uint8_t *keys, const uint32_t *key_index, uint32_t key_slots,
-                                             uint32_t pkt, uint4 *gb = nullptr) {
+                                             uint32_t pkt, uint4 *gb = nullptr, uint64_t *stamps = nullptr) {
+  // (stamps: the service's phase stamps of this packet, its group's lane 0 writes them)
+  const bool stamp = stamps && l == 0u;
   int32_t status = WG_STATUS_OK;
   if (!kSeal && slot == WG_KEY_SLOT_INVALID_PACKET) status = WG_STATUS_INVALID_PACKET;
   else if (!kSeal && slot == WG_KEY_SLOT_NO_SESSION) status = WG_STATUS_NO_CURRENT_SESSION;
@@ -239,6 +241,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       }
     }
     lds_wave_sync();
+    if (stamp) stamps[1] = wall_clock64();
     if (any) load_block(b0, x);
     if (!kSeal && l == Lu - 1u) {  // (before this lane's last block overwrites the tag's first bytes)
       const uint4 ta = gb[P >> 4], tb = (P & 15u) ? gb[(P >> 4) + 1u] : make_uint4(0, 0, 0, 0);
@@ -356,6 +359,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       if (bad && wr) status = WG_STATUS_INVALID_AEAD_TAG;
     }
     lds_wave_sync();
+    if (stamp) stamps[2] = wall_clock64();
     if (wr) {
       const uint32_t nb_out = kSeal ? P + 16u : P, np_out = (nb_out + 15u) / 16u;
       for (uint32_t p = l; p < np_out; p += G) {
@@ -370,6 +374,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       }
       if (kSeal && l == 0u) xst16(dst, WG_MSG_DATA, sidx, n1, n2, B);  // header (session.rs:224-229)
     }
+    if (stamp) stamps[3] = wall_clock64();
   } else if (kSeal) {
     if (l == 0u) xst16(dst, WG_MSG_DATA, sidx, n1, n2, B);  // header (session.rs:224-229)
   } else {
@@ -509,9 +514,14 @@ __device__ __forceinline__ void srv_packets(SrvSlot *sl, uint32_t lane, uint32_t
     const uint32_t len = d1.z, kslot = d1.w;
     const uint8_t *src = reinterpret_cast<const uint8_t *>(so);
     uint8_t *dst = reinterpret_cast<uint8_t *>(dn);
+    uint64_t *stamps = p.stamp && i == 0u ? sl->stamp + 5 : nullptr;  // (packet 0: stamp[5 ..])
+    if (stamps && l == 0u) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamps[0] = wall_clock64();
+    }
     if (stage_fits<kSeal, G>(len)) {
       xlane_packet<kSeal, G, true, true>(l, src, dst, len, kslot, ctr, so | dn, sl->st + i, p.keys, p.key_index,
-                                         p.key_slots, i, gb);
+                                         p.key_slots, i, gb, stamps);
     } else {  // (its plain loads: first drop what the caches hold of earlier requests)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       xlane_packet<kSeal, G>(l, src, dst, len, kslot, ctr, so | dn, sl->st + i, p.keys, p.key_index, p.key_slots, i);
