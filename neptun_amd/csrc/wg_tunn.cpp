@@ -1666,6 +1666,13 @@ int srv_restart(Service &V) {
   __atomic_store_n(V.stop, 1u, __ATOMIC_RELEASE);
   V.live.store(false, std::memory_order_seq_cst);
   TUNN_HIP(hipStreamSynchronize(V.stream), "tunn: service stop");
+  // a request left unanswered (a failed wait) is withdrawn: the next kernel starts from
+  // every slot's done word and must not find an old sequence number waiting there
+  for (uint32_t k = 0; k < wg::kSrvSlots; ++k) {
+    const uint32_t done = __atomic_load_n(&V.slots[k].done, __ATOMIC_ACQUIRE);
+    __atomic_store_n(&V.slots[k].seq, done, __ATOMIC_RELEASE);
+    V.seq[k] = done;
+  }
   __atomic_store_n(V.stop, 0u, __ATOMIC_RELEASE);
   TUNN_HIP(hipMemsetAsync(V.d_count, 0, wg::kSrvSlots * 32 * 4, V.stream), "tunn: service counters");
   // (a key update that completes after this read is seen as a new generation next time)
