@@ -86,6 +86,14 @@ __device__ __forceinline__ uint4 ld16_sys(const uint8_t *p) {
 __device__ __forceinline__ uint4 xld16_sys(const uint8_t *p, const XBounds &B) {
   return xok((uint64_t)p, 16u, B.in_lo, B.in_hi, B) ? ld16_sys(p) : make_uint4(0, 0, 0, 0);
 }
+// a global-address-space 16-byte load: a flat load also counts against the LDS counter,
+// and the compiler then waits for every load at once (vmcnt(0) lgkmcnt(0)) where a
+// global one lets the key loads issued before the input be waited for alone
+__device__ __forceinline__ uint4 xld16_g(const uint8_t *p, const XBounds &B) {
+  if (!xok((uint64_t)p, 16u, B.in_lo, B.in_hi, B)) return make_uint4(0, 0, 0, 0);
+  const xl_u32x4 v = *reinterpret_cast<const __attribute__((address_space(1))) xl_u32x4 *>(reinterpret_cast<uint64_t>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void xst16(uint8_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d, const XBounds &B) {
   if (xok((uint64_t)p, 16u, B.out_lo, B.out_hi, B)) st16(p, a, b, c, d);
 }
@@ -192,18 +200,9 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   constexpr uint32_t kBatch = 8;
   const uint32_t np_in = kSeal ? (P + 15u) / 16u : (P + 31u) / 16u;
   uint4 sv[kBatch];
-  if constexpr (kStage) {
-#pragma unroll
-    for (uint32_t k = 0; k < kBatch; ++k) {
-      const uint32_t p = l + k * G;
-      sv[k] = p < np_in ? (kSys ? xld16_sys(in + 16u * p, B) : xld16(in + 16u * p, B)) : make_uint4(0, 0, 0, 0);
-    }
-  } else {
-    if (any) load_block(b0, x);
-  }
   uint32_t key[8];
-  uint32_t sidx, n1, n2;
-  {
+  uint32_t sidx = 0, n1 = 0, n2 = 0;
+  auto load_key = [&]() {
     const uint4 a = ld16(keys + 32u * slot), b = ld16(keys + 32u * slot + 16u);
     key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
     key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
@@ -212,14 +211,53 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       n1 = (uint32_t)counter;
       n2 = (uint32_t)(counter >> 32);
     } else {
-      const uint4 h = kSys ? xld16_sys(src, B) : xld16(src, B);  // header: type, receiver_idx, counter (mod.rs:170-180)
+      const uint4 h = kSys ? xld16_sys(src, B) : kStage ? xld16_g(src, B) : xld16(src, B);  // header: type, receiver_idx, counter (mod.rs:170-180)
       if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
       else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
       n1 = h.z;
       n2 = h.w;
     }
+  };
+  // staged seal: the nonce is the descriptor's counter, so the key goes out first (HBM)
+  // and the span's first keystream block, the Poly1305 key and the combine's first power
+  // of r are computed while the input crosses PCIe (open waits for its header first)
+  constexpr bool kEarlyKs = kStage && kSeal;
+  if constexpr (kEarlyKs) load_key();
+  if constexpr (kStage) {
+    // (straight-line loads: a piece past the input reloads piece 0 and is not staged --
+    // a conditional load's zero default makes the compiler copy, and wait, per load)
+#pragma unroll
+    for (uint32_t k = 0; k < kBatch; ++k) {
+      const uint32_t p = l + k * G, pp = p < np_in ? p : 0u;
+      sv[k] = kSys ? xld16_sys(in + 16u * pp, B) : xld16_g(in + 16u * pp, B);
+    }
+  } else {
+    if (any) load_block(b0, x);
   }
+  if constexpr (!kEarlyKs) load_key();
   const bool wr = kSeal || status == WG_STATUS_OK;  // (group-uniform)
+  Poly ps;
+  uint32_t ks[16];
+  uint32_t rk[8];
+  F26 r26, R0;  // (r, and r^(4 C): the combine's first level)
+  // first block of the span (lane 0: block 0, the one-time key), r and s to every lane
+  auto first_block = [&]() {
+    if (any) {
+      chacha20_block(ks, key, b0, n1, n2);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ks[j] = 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rk[j] = gshfl<G>(ks[j], 0u);
+    poly_init(ps, rk);
+    r26 = f26_from32(ps.r0, ps.r1, ps.r2, ps.r3, 0u);
+    R0 = Lu > 2u ? f26_pow(r26, 4u * C) : r26;
+  };
+  if constexpr (kEarlyKs) {
+    asm volatile("" ::: "memory");  // (the input loads above go out before the keystream)
+    first_block();
+  }
   uint32_t tw[8] = {0, 0, 0, 0, 0, 0, 0, 0};          // open: the received tag's two pieces
   if constexpr (kStage) {
     lds_wave_sync();  // (the group's previous packet has left the stage)
@@ -232,7 +270,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
 #pragma unroll
       for (uint32_t k = 0; k < kBatch; ++k) {
         const uint32_t p = p0 + l + k * G;
-        sv[k] = p < np_in ? (kSys ? xld16_sys(in + 16u * p, B) : xld16(in + 16u * p, B)) : make_uint4(0, 0, 0, 0);
+        sv[k] = p < np_in ? (kSys ? xld16_sys(in + 16u * p, B) : xld16_g(in + 16u * p, B)) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (uint32_t k = 0; k < kBatch; ++k) {
@@ -250,7 +288,6 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     }
   }
 
-  Poly ps;
   uint32_t kpieces = 0;  // pieces this lane absorbed
   // one data block b >= 1: XOR, store, and (once r is known) absorb its pieces
   auto data_block = [&](uint32_t b, const uint32_t (&ks)[16], const uint4 (&x)[4]) {
@@ -280,18 +317,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     }
   };
 
-  // first block of the span (lane 0: block 0, the one-time key)
-  uint32_t ks[16];
-  if (any) {
-    chacha20_block(ks, key, b0, n1, n2);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) ks[j] = 0u;
-  }
-  uint32_t rk[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) rk[j] = gshfl<G>(ks[j], 0u);
-  poly_init(ps, rk);
+  if constexpr (!kEarlyKs) first_block();
   if (any && b0 >= 1u) data_block(b0, ks, x);
   for (uint32_t b = b0 + 1u; b < b1; ++b) {
     load_block(b, x);
@@ -300,10 +326,9 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   }
 
   // combine: T = sum_{l < Lu-1} h_l r^(S (Lu - 2 - l)) in lane Lu - 2, by levels
-  const F26 r26 = f26_from32(ps.r0, ps.r1, ps.r2, ps.r3, 0u);
   F26 v = l + 1u < Lu ? f26_from32(ps.h0, ps.h1, ps.h2, ps.h3, ps.h4) : f26_zero();
   if (Lu > 2u) {
-    F26 R = f26_pow(r26, 4u * C);
+    F26 R = R0;
     const int dd = (int)Lu - 2 - (int)l;
     for (uint32_t k = 0; (1u << k) < Lu - 1u; ++k) {
       const uint32_t step = 1u << k;
