@@ -6,6 +6,7 @@
  *   tunn_threads T B [calls] [P]   -> one JSON line per run
  * GW_PRIVATE_ENGINES=1: one engine per Tunn (else the context's default engine).
  * TT_REGISTER=1: every thread's buffers registered (wg_gpu_register_host): registered calls.
+ * TT_HUGE=1: those buffers on transparent huge pages (one 2 MiB-aligned region).
  * The line also gives how many calls went out in a launch shared with another call
  * (wg_engine_info.combined: the engine's combiner, WG_COMBINE).
  */
@@ -15,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "neptun_gpu.h"
@@ -37,7 +39,24 @@ typedef struct {
 static void *run(void *arg) {
   job_t *j = arg;
   const uint32_t B = j->B, P = j->P, slot = (P + 64 + 127) & ~127u;
-  uint8_t *src = calloc((size_t)B, slot), *wire = calloc((size_t)B, slot), *back = calloc((size_t)B, slot);
+  uint8_t *src, *wire, *back;
+  if (getenv("TT_HUGE") && atoi(getenv("TT_HUGE"))) {
+    /* the three pools in one 2 MiB-aligned region on transparent huge pages (fewer IOMMU
+       translations for the kernel's zero-copy reads and writes) */
+    const size_t one = ((size_t)B * slot + 4095) & ~(size_t)4095, need = 3 * one;
+    const size_t huge = (size_t)2 << 20, len = (need + huge - 1) & ~(huge - 1);
+    uint8_t *m = mmap(NULL, len + huge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) {
+      j->rc = 98;
+      return NULL;
+    }
+    uint8_t *a = (uint8_t *)(((uintptr_t)m + huge - 1) & ~(uintptr_t)(huge - 1));
+    madvise(a, len, MADV_HUGEPAGE);
+    memset(a, 0, len);
+    src = a, wire = a + one, back = a + 2 * one;
+  } else {
+    src = calloc((size_t)B, slot), wire = calloc((size_t)B, slot), back = calloc((size_t)B, slot);
+  }
   const uint8_t **sp = calloc(B, sizeof *sp), **wp = calloc(B, sizeof *wp);
   uint8_t **wd = calloc(B, sizeof *wd), **bd = calloc(B, sizeof *bd);
   uint32_t *len = calloc(B, 4), *cap = calloc(B, 4), *wlen = calloc(B, 4);
@@ -78,7 +97,10 @@ static void *run(void *arg) {
     wg_gpu_unregister_host(j->ctx, wire);
     wg_gpu_unregister_host(j->ctx, back);
   }
-  free(src); free(wire); free(back); free(sp); free(wp); free(wd); free(bd); free(len); free(cap); free(wlen);
+  if (!(getenv("TT_HUGE") && atoi(getenv("TT_HUGE")))) {  /* (the huge region is the process's until exit) */
+    free(src); free(wire); free(back);
+  }
+  free(sp); free(wp); free(wd); free(bd); free(len); free(cap); free(wlen);
   free(res);
   return NULL;
 }
