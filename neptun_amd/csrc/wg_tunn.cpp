@@ -668,6 +668,16 @@ void free_buffers(Staging &s) {
   s.bytes = s.descs = 0;
 }
 
+// (WG_TUNN_STAGE_NC=1: packet staging as non-coherent pinned memory -- the kernels'
+// zero-copy reads then fill whole L2 lines; an A/B of the small-call cap)
+unsigned stage_data_flags(unsigned fl) {
+  static const bool nc = [] {
+    const char *e = std::getenv("WG_TUNN_STAGE_NC");
+    return e && std::atoi(e) != 0;
+  }();
+  return nc ? (fl | hipHostMallocNonCoherent) : fl;
+}
+
 hipError_t reserve(Staging &s, size_t bytes, size_t descs) {
   hipError_t e = hipSuccess;
   const unsigned fl = s.host_flags;
@@ -678,8 +688,8 @@ hipError_t reserve(Staging &s, size_t bytes, size_t descs) {
     (void)hipFree(s.d_out);
     s.h_in = s.h_out = s.d_in = s.d_out = nullptr;
     s.bytes = 0;
-    if ((e = hipHostMalloc(&s.h_in, bytes, fl)) != hipSuccess) return e;
-    if ((e = hipHostMalloc(&s.h_out, bytes, fl)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&s.h_in, bytes, stage_data_flags(fl))) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&s.h_out, bytes, stage_data_flags(fl))) != hipSuccess) return e;
     if ((e = hipMalloc(&s.d_in, bytes)) != hipSuccess) return e;
     if ((e = hipMalloc(&s.d_out, bytes)) != hipSuccess) return e;
     s.bytes = bytes;
