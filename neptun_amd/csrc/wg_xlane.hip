@@ -45,6 +45,11 @@
 #define WG_XLANE_CHECK 0
 #endif
 
+// (A/B: 0 = the staged path's key in vector loads, as the other paths)
+#ifndef WG_XLANE_SCALAR_KEY
+#define WG_XLANE_SCALAR_KEY 1
+#endif
+
 namespace wg {
 #if WG_XLANE_CHECK
 __device__ unsigned long long g_xlane_check[4];  // violations, first address, its packet, its lane
@@ -99,6 +104,34 @@ __device__ __forceinline__ void xst16(uint8_t *p, uint32_t a, uint32_t b, uint32
 }
 __device__ __forceinline__ void xstore_partial(uint8_t *p, const uint32_t w[4], int k, const XBounds &B) {
   if (xok((uint64_t)p, (uint32_t)k, B.out_lo, B.out_hi, B)) store_partial(p, w, k);
+}
+
+// The key of `slot` in scalar registers, for groups of a whole or half wave (the staged
+// path): a scalar load counts against lgkmcnt, not vmcnt, so the first keystream block
+// waits for the key alone and runs while the input's vector loads are in flight (a key
+// of vector loads issued before them is waited for with vmcnt(0), the input included).
+// readlane of a lane whose group has no packet gives a stray slot: clamped, and unused.
+template <uint32_t G>
+__device__ __forceinline__ void key_load_scalar(const uint8_t *keys, uint32_t slot, uint32_t key_slots,
+                                                uint32_t (&key)[8]) {
+  static_assert(G == 64u || G == 32u, "one or two groups per wave");
+  typedef const __attribute__((address_space(4))) uint32_t kc_u32;
+  auto sload = [&](uint32_t s, uint32_t (&k)[8]) {
+    s = s < key_slots ? s : 0u;
+    const kc_u32 *q = reinterpret_cast<const kc_u32 *>(reinterpret_cast<uint64_t>(keys) + 32ull * s);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k[j] = q[j];
+  };
+  if constexpr (G == 64u) {
+    sload(__builtin_amdgcn_readfirstlane(slot), key);
+  } else {
+    uint32_t a[8], b[8];
+    sload(__builtin_amdgcn_readlane(slot, 0), a);
+    sload(__builtin_amdgcn_readlane(slot, 32), b);
+    const bool hi = (threadIdx.x & 32u) != 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) key[j] = hi ? b[j] : a[j];
+  }
 }
 
 // value of lane `src` (0 .. G-1) of this lane's group
@@ -203,9 +236,13 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   uint32_t key[8];
   uint32_t sidx = 0, n1 = 0, n2 = 0;
   auto load_key = [&]() {
-    const uint4 a = ld16(keys + 32u * slot), b = ld16(keys + 32u * slot + 16u);
-    key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
-    key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
+    if constexpr (kStage && G >= 32u && WG_XLANE_SCALAR_KEY) {
+      key_load_scalar<G>(keys, slot, key_slots, key);
+    } else {
+      const uint4 a = ld16(keys + 32u * slot), b = ld16(keys + 32u * slot + 16u);
+      key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
+      key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
+    }
     sidx = key_index[slot];
     if (kSeal) {
       n1 = (uint32_t)counter;
@@ -224,12 +261,16 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   constexpr bool kEarlyKs = kStage && kSeal;
   if constexpr (kEarlyKs) load_key();
   if constexpr (kStage) {
-    // (straight-line loads: a piece past the input reloads piece 0 and is not staged --
-    // a conditional load's zero default makes the compiler copy, and wait, per load)
+    // (straight-line loads: a lane past the input reloads the input's last piece -- the
+    // line its neighbours fetch in the same instruction -- and does not stage it.  A
+    // per-lane zero default, or a branch around each load, makes the compiler copy, and
+    // wait, after every load.  An empty seal reads nothing: its source may be null.)
+    if (np_in != 0u) {  // (group-uniform)
 #pragma unroll
-    for (uint32_t k = 0; k < kBatch; ++k) {
-      const uint32_t p = l + k * G, pp = p < np_in ? p : 0u;
-      sv[k] = kSys ? xld16_sys(in + 16u * pp, B) : xld16_g(in + 16u * pp, B);
+      for (uint32_t k = 0; k < kBatch; ++k) {
+        const uint32_t p = l + k * G, pp = p < np_in ? p : np_in - 1u;
+        sv[k] = kSys ? xld16_sys(in + 16u * pp, B) : xld16_g(in + 16u * pp, B);
+      }
     }
   } else {
     if (any) load_block(b0, x);

@@ -10,6 +10,7 @@ hand-written gfx950 kernels in neptun_amd/csrc/wg_aead.hip.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import numpy as np
 
@@ -98,6 +99,9 @@ class GpuContext:
     """One GPU + device key table.  Replaces per-session ring keys."""
 
     def __init__(self, device: int = 0, key_slots: int = 1, lib_path: str | None = None):
+        # (the Tunns, engines and pipes made on it: their native objects refer to it, so
+        # close() closes them first -- Tunns and pipes, then engines)
+        self._dependents = weakref.WeakSet()
         # lib_path: another build of the same sources (the tests' checked build)
         self._lib = load(lib_path) if lib_path else load()
         h = ctypes.c_void_p()
@@ -118,9 +122,14 @@ class GpuContext:
         return tuple(int(x) for x in out)
 
     def close(self) -> None:
+        for dep in sorted(getattr(self, "_dependents", ()), key=lambda d: d._close_order):
+            dep.close()
         if getattr(self, "_h", None):
             self._lib.wg_gpu_ctx_destroy(self._h)
             self._h = None
+
+    def _attach(self, dep) -> None:
+        self._dependents.add(dep)
 
     def __del__(self):
         try:
@@ -306,6 +315,8 @@ class GpuPipe:
     memory); pass pinned host tensors for overlapped copies.
     """
 
+    _close_order = 0  # (GpuContext.close: Tunns and pipes before engines)
+
     def __init__(self, ctx: GpuContext, chunk_bytes: int = 64 << 20, depth: int = 3):
         self._lib = ctx._lib
         self._ctx = ctx  # keep the context alive
@@ -313,6 +324,7 @@ class GpuPipe:
         check(self._lib.wg_gpu_pipe_create(ctx._h, chunk_bytes, depth, ctypes.byref(h)),
               "wg_gpu_pipe_create")
         self._h = h
+        ctx._attach(self)
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -123,12 +123,15 @@ class Engine:
     """wg_engine: a per-GPU engine (host pool, lanes of streams and staging) that any
     number of Tunns share; multi-peer batches mix packets of its Tunns."""
 
+    _close_order = 1  # (GpuContext.close: Tunns and pipes before engines)
+
     def __init__(self, ctx):
         self._lib = _bind(ctx._lib)
         self._ctx = ctx
         h = ctypes.c_void_p()
         check(self._lib.wg_engine_create(ctx._h, ctypes.byref(h)), "wg_engine_create")
         self._h = h
+        ctx._attach(self)
 
     def tunn(self, first_slot: int) -> "Tunn":
         """A Tunn on this engine over key slots [first_slot, first_slot + 16) of the
@@ -229,6 +232,8 @@ def multi_ptrs(seal: bool, tunn_ptrs, src_ptrs, src_lens, dst_ptrs, dst_caps, li
 class Tunn:
     """Tunn mirror bound to a GpuContext; uses 16 key slots from `first_slot`."""
 
+    _close_order = 0  # (GpuContext.close: Tunns and pipes before engines)
+
     def __init__(self, ctx, first_slot: int = 0, engine: Engine | None = None):
         """ctx: one GpuContext (the Tunn attaches to its default engine, or to `engine`),
         or a list of them (wg_tunn_create_multi: batches are split across the contexts' GPUs)."""
@@ -247,6 +252,8 @@ class Tunn:
             check(self._lib.wg_tunn_create_multi(arr, len(ctxs), first_slot, ctypes.byref(h)),
                   "wg_tunn_create_multi")
         self._h = h
+        for c in ctxs:
+            c._attach(self)
 
     def engines(self):
         """[(device, numa_node)] of the Tunn's engines."""

@@ -393,6 +393,35 @@ def test_concurrent_small_calls_combine_into_shared_launches(big_ctx, monkeypatc
     check_state(pairs)
     if depth == "1":  # (one launch in flight: calls arriving meanwhile must share the next;
         # with two, whether any call waits for a slot depends on the kernels' speed)
+        # The calls above spend most of their time in Python between launches, so whether
+        # two overlap is chance; a burst released at one barrier makes 8 calls arrive
+        # within microseconds of each other.
+        bar = threading.Barrier(len(pairs))
+
+        def burst(k):
+            try:
+                r = random.Random(seeds[k] ^ 0x5A5A)
+                tm, tg, _ = pairs[k]
+                for rep in range(20):
+                    srcs = [ipv4(r, 1350) for _ in range(50)]
+                    caps = [len(x) + 32 for x in srcs]
+                    dm = [bytearray(b"\xee" * c) for c in caps]
+                    res_m = [tm.encapsulate(x, d) for x, d in zip(srcs, dm)]
+                    dg = [bytearray(b"\xee" * c) for c in caps]
+                    bar.wait(timeout=60)
+                    res_g = tg.encapsulate_batch(srcs, dg)
+                    check_same(res_g, res_m, dg, dm, f"thread {k} burst {rep}")
+            except Exception as e:  # noqa: BLE001 (reported below)
+                errors.append(e)
+                bar.abort()
+
+        th = [threading.Thread(target=burst, args=(k,)) for k in range(len(pairs))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors, errors[0]
+        check_state(pairs)
         assert eng.info()["combined"] > 0, "no two concurrent small calls shared a launch"
     for _, tg, _ in pairs:
         tg.close()
@@ -611,3 +640,20 @@ def test_multi_peer_batches_across_engines_match_sequential_tunns(two_ctx, n_pee
         tg.close()
     for e in engs:
         e.close()
+
+
+def test_closing_the_context_closes_its_tunns_and_engines_first(torch_cuda):
+    """A Tunn, an engine and a pipe still open when their context closes: the context
+    closes them first (their native objects refer to it), so nothing is left to touch a
+    freed context at garbage collection or interpreter exit."""
+    from neptun_amd import Engine, Tunn
+    from neptun_amd.gpu import GpuContext, GpuPipe
+
+    ctx = GpuContext(0, key_slots=64)
+    eng = Engine(ctx)
+    tunns = [Tunn(ctx, first_slot=16 * k, engine=eng) for k in range(2)]
+    pipe = GpuPipe(ctx, chunk_bytes=1 << 20, depth=2)
+    tunns[0].install_session(7, 9, bytes(32), bytes(range(32)), True)
+    ctx.close()
+    assert all(t._h is None for t in tunns) and eng._h is None and pipe._h is None
+    ctx.close()  # (twice: nothing left to do)
