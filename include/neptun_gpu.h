@@ -130,6 +130,8 @@ const char *wg_gpu_last_error(void);
  * handshake derives (handshake.rs:694, :948) are uploaded with wg_gpu_set_keys.
  */
 int wg_gpu_ctx_create(int device, uint32_t key_slots, wg_gpu_ctx **out);
+/* Destroy the Tunns, engines and pipes made on a context before the context
+ * (they refer to it); the Python mirror's GpuContext.close() does so itself. */
 int wg_gpu_ctx_destroy(wg_gpu_ctx *ctx);
 uint32_t wg_gpu_ctx_key_slots(const wg_gpu_ctx *ctx);
 

@@ -112,25 +112,22 @@ __device__ __forceinline__ void xstore_partial(uint8_t *p, const uint32_t w[4], 
 // of vector loads issued before them is waited for with vmcnt(0), the input included).
 // readlane of a lane whose group has no packet gives a stray slot: clamped, and unused.
 template <uint32_t G>
-__device__ __forceinline__ void key_load_scalar(const uint8_t *keys, uint32_t slot, uint32_t key_slots,
-                                                uint32_t (&key)[8]) {
+__device__ __forceinline__ void key_issue_scalar(const uint8_t *keys, const uint32_t *key_index, uint32_t slot,
+                                                 uint32_t key_slots, uint32_t (&kr)[2][9]) {
   static_assert(G == 64u || G == 32u, "one or two groups per wave");
   typedef const __attribute__((address_space(4))) uint32_t kc_u32;
-  auto sload = [&](uint32_t s, uint32_t (&k)[8]) {
+  auto sload = [&](uint32_t s, uint32_t (&k)[9]) {
     s = s < key_slots ? s : 0u;
     const kc_u32 *q = reinterpret_cast<const kc_u32 *>(reinterpret_cast<uint64_t>(keys) + 32ull * s);
 #pragma unroll
     for (int j = 0; j < 8; ++j) k[j] = q[j];
+    k[8] = reinterpret_cast<const kc_u32 *>(reinterpret_cast<uint64_t>(key_index))[s];
   };
   if constexpr (G == 64u) {
-    sload(__builtin_amdgcn_readfirstlane(slot), key);
+    sload(__builtin_amdgcn_readfirstlane(slot), kr[0]);
   } else {
-    uint32_t a[8], b[8];
-    sload(__builtin_amdgcn_readlane(slot, 0), a);
-    sload(__builtin_amdgcn_readlane(slot, 32), b);
-    const bool hi = (threadIdx.x & 32u) != 0u;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) key[j] = hi ? b[j] : a[j];
+    sload(__builtin_amdgcn_readlane(slot, 0), kr[0]);
+    sload(__builtin_amdgcn_readlane(slot, 32), kr[1]);
   }
 }
 
@@ -235,37 +232,59 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   uint4 sv[kBatch];
   uint32_t key[8];
   uint32_t sidx = 0, n1 = 0, n2 = 0;
+  // (open waits for its header, a vector load, before its first block in any case)
+  constexpr bool kScalarKey = kStage && kSeal && G >= 32u && WG_XLANE_SCALAR_KEY;
+  uint32_t kr[2][9];  // (kScalarKey: each half wave's key and index)
+  auto header_checks = [&](const uint4 &h) {  // header: type, receiver_idx, counter (mod.rs:170-180)
+    if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
+    else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
+    n1 = h.z;
+    n2 = h.w;
+  };
   auto load_key = [&]() {
-    if constexpr (kStage && G >= 32u && WG_XLANE_SCALAR_KEY) {
-      key_load_scalar<G>(keys, slot, key_slots, key);
+    if (kSeal) {
+      n1 = (uint32_t)counter;
+      n2 = (uint32_t)(counter >> 32);
+    }
+    if constexpr (kScalarKey) {  // (issued here, taken by settle_key)
+      key_issue_scalar<G>(keys, key_index, slot, key_slots, kr);
     } else {
       const uint4 a = ld16(keys + 32u * slot), b = ld16(keys + 32u * slot + 16u);
       key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
       key[4] = b.x; key[5] = b.y; key[6] = b.z; key[7] = b.w;
+      sidx = key_index[slot];
+      if constexpr (!kSeal) header_checks(kSys ? xld16_sys(src, B) : kStage ? xld16_g(src, B) : xld16(src, B));
     }
-    sidx = key_index[slot];
-    if (kSeal) {
-      n1 = (uint32_t)counter;
-      n2 = (uint32_t)(counter >> 32);
-    } else {
-      const uint4 h = kSys ? xld16_sys(src, B) : kStage ? xld16_g(src, B) : xld16(src, B);  // header: type, receiver_idx, counter (mod.rs:170-180)
-      if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
-      else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
-      n1 = h.z;
-      n2 = h.w;
+  };
+  // (kScalarKey, after the input's loads: the values pass an empty asm each, so no use of
+  // them -- and no wait for the header's PCIe round trip -- is scheduled among the loads)
+  auto settle_key = [&]() {
+    asm volatile("" ::: "memory");
+    constexpr int kHalves = G == 64u ? 1 : 2;
+#pragma unroll
+    for (int q = 0; q < kHalves; ++q) {
+#pragma unroll
+      for (int j = 0; j < 9; ++j) asm volatile("" : "+s"(kr[q][j]));
     }
+    const bool h1 = kHalves == 2 && (threadIdx.x & 32u) != 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) key[j] = h1 ? kr[kHalves - 1][j] : kr[0][j];
+    sidx = h1 ? kr[kHalves - 1][8] : kr[0][8];
   };
   // staged seal: the nonce is the descriptor's counter, so the key goes out first (HBM)
   // and the span's first keystream block, the Poly1305 key and the combine's first power
   // of r are computed while the input crosses PCIe (open waits for its header first)
   constexpr bool kEarlyKs = kStage && kSeal;
-  if constexpr (kEarlyKs) load_key();
+  if constexpr (kEarlyKs) {
+    load_key();
+    asm volatile("" ::: "memory");  // (the key and header loads go out before the input's)
+  }
   if constexpr (kStage) {
     // (straight-line loads: a lane past the input reloads the input's last piece -- the
     // line its neighbours fetch in the same instruction -- and does not stage it.  A
     // per-lane zero default, or a branch around each load, makes the compiler copy, and
     // wait, after every load.  An empty seal reads nothing: its source may be null.)
-    if (np_in != 0u) {  // (group-uniform)
+    if (!kSeal || np_in != 0u) {  // (group-uniform; an open always has its tag)
 #pragma unroll
       for (uint32_t k = 0; k < kBatch; ++k) {
         const uint32_t p = l + k * G, pp = p < np_in ? p : np_in - 1u;
@@ -275,6 +294,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   } else {
     if (any) load_block(b0, x);
   }
+  if constexpr (kScalarKey) settle_key();
   if constexpr (!kEarlyKs) load_key();
   const bool wr = kSeal || status == WG_STATUS_OK;  // (group-uniform)
   Poly ps;
