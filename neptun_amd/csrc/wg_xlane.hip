@@ -131,6 +131,38 @@ __device__ __forceinline__ void key_issue_scalar(const uint8_t *keys, const uint
   }
 }
 
+// Open's header (the packet's first 16 bytes, the nonce) the same way, for the launched
+// kernel only: a launch starts with the scalar cache invalidated, so it cannot hold an
+// earlier call's bytes (the resident service reads packets with vector loads past the
+// caches).  A half wave without a packet (exec) reads the other half's header: its lanes'
+// addresses are stale.  (Addresses are chosen before the loads, not loads under a branch:
+// a join's copy of the result waits for every scalar load.)
+template <uint32_t G>
+__device__ __forceinline__ void hdr_issue_scalar(const uint8_t *src, uint4 (&hr)[2]) {
+  static_assert(G == 64u || G == 32u, "one or two groups per wave");
+  typedef const __attribute__((address_space(4))) xl_u32x4 hc_u32x4;
+  const uint64_t a = reinterpret_cast<uint64_t>(src);
+  const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+  auto addr = [&](int ln) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, ln) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, ln) << 32);
+  };
+  auto sload = [&](uint64_t q) {
+    const xl_u32x4 v = *reinterpret_cast<const hc_u32x4 *>(q);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  };
+  if constexpr (G == 64u) {
+    hr[0] = hr[1] = sload(addr(0));  // (the group is the wave: lane 0 is active)
+  } else {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    const uint64_t p0 = addr(0), p1 = addr(32);
+    const uint64_t q0 = (ex & 1ull) ? p0 : p1;  // (some half is active)
+    const uint64_t q1 = ((ex >> 32) & 1ull) ? p1 : q0;
+    hr[0] = sload(q0);
+    hr[1] = sload(q1);
+  }
+}
+
 // value of lane `src` (0 .. G-1) of this lane's group
 template <uint32_t G>
 __device__ __forceinline__ uint32_t gshfl(uint32_t x, uint32_t src) {
@@ -232,9 +264,11 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
   uint4 sv[kBatch];
   uint32_t key[8];
   uint32_t sidx = 0, n1 = 0, n2 = 0;
-  // (open waits for its header, a vector load, before its first block in any case)
-  constexpr bool kScalarKey = kStage && kSeal && G >= 32u && WG_XLANE_SCALAR_KEY;
-  uint32_t kr[2][9];  // (kScalarKey: each half wave's key and index)
+  // (the service's open reads its header with a vector load past the caches, and waits for
+  // it -- and so for the input -- before its first block)
+  constexpr bool kScalarKey = kStage && G >= 32u && (kSeal || !kSys) && WG_XLANE_SCALAR_KEY;
+  uint32_t kr[2][9];  // (kScalarKey: each half wave's key and index, and open's header)
+  uint4 hr[2];
   auto header_checks = [&](const uint4 &h) {  // header: type, receiver_idx, counter (mod.rs:170-180)
     if (h.x != WG_MSG_DATA) status = WG_STATUS_INVALID_PACKET;
     else if (h.y != sidx) status = WG_STATUS_WRONG_INDEX;  // session.rs:275-277
@@ -248,6 +282,7 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
     }
     if constexpr (kScalarKey) {  // (issued here, taken by settle_key)
       key_issue_scalar<G>(keys, key_index, slot, key_slots, kr);
+      if constexpr (!kSeal) hdr_issue_scalar<G>(src, hr);
     } else {
       const uint4 a = ld16(keys + 32u * slot), b = ld16(keys + 32u * slot + 16u);
       key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
@@ -256,28 +291,33 @@ __device__ __forceinline__ void xlane_packet(uint32_t l, const uint8_t *src, uin
       if constexpr (!kSeal) header_checks(kSys ? xld16_sys(src, B) : kStage ? xld16_g(src, B) : xld16(src, B));
     }
   };
-  // (kScalarKey, after the input's loads: the values pass an empty asm each, so no use of
-  // them -- and no wait for the header's PCIe round trip -- is scheduled among the loads)
+  // (kScalarKey, after the input's loads: a scheduling barrier and an empty asm per value,
+  // so no use or copy of them -- and no wait for the header's PCIe round trip -- lands
+  // among the loads)
   auto settle_key = [&]() {
     asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     constexpr int kHalves = G == 64u ? 1 : 2;
 #pragma unroll
     for (int q = 0; q < kHalves; ++q) {
 #pragma unroll
       for (int j = 0; j < 9; ++j) asm volatile("" : "+s"(kr[q][j]));
+      if constexpr (!kSeal) asm volatile("" : "+s"(hr[q].x), "+s"(hr[q].y), "+s"(hr[q].z), "+s"(hr[q].w));
     }
     const bool h1 = kHalves == 2 && (threadIdx.x & 32u) != 0u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) key[j] = h1 ? kr[kHalves - 1][j] : kr[0][j];
     sidx = h1 ? kr[kHalves - 1][8] : kr[0][8];
+    if constexpr (!kSeal) header_checks(h1 ? hr[kHalves - 1] : hr[0]);
   };
-  // staged seal: the nonce is the descriptor's counter, so the key goes out first (HBM)
-  // and the span's first keystream block, the Poly1305 key and the combine's first power
-  // of r are computed while the input crosses PCIe (open waits for its header first)
-  constexpr bool kEarlyKs = kStage && kSeal;
+  // staged: the key (HBM) and the nonce -- seal's descriptor counter, or open's header
+  // in a scalar load -- go out first, and the span's first keystream block, the Poly1305
+  // key and the combine's first power of r are computed while the input crosses PCIe
+  constexpr bool kEarlyKs = kStage && (kSeal || kScalarKey);
   if constexpr (kEarlyKs) {
     load_key();
     asm volatile("" ::: "memory");  // (the key and header loads go out before the input's)
+    __builtin_amdgcn_sched_barrier(0);
   }
   if constexpr (kStage) {
     // (straight-line loads: a lane past the input reloads the input's last piece -- the
